@@ -1,0 +1,163 @@
+/*
+ * zs3gpu.h — C ABI of the MI355X erasure-shard + bitrot-hash data path.
+ *
+ * Drop-in boundary for 0chain/zs3server's server-mode data path:
+ * a cgo shim binds these entry points under the reference's
+ *   - Erasure type           cmd/erasure-coding.go:35-150
+ *   - bitrot hash factory    cmd/bitrot.go:47-64 (HighwayHash256S, key :37)
+ *   - streaming bitrot I/O   cmd/bitrot-streaming.go:43-65, :142-189
+ *   - encode / decode loops  cmd/erasure-encode.go:76-113, cmd/erasure-decode.go:206-332
+ * replacing the arithmetic of github.com/klauspost/reedsolomon v1.11.8 and
+ * github.com/minio/highwayhash v1.0.2.
+ *
+ * Conventions
+ *   - Every function returns an int status: 0 = ZS3_OK, < 0 = one of the codes
+ *     below, each mapped 1:1 to a reference error sentinel.  Size helpers return
+ *     int64_t values exactly as the Go methods do.
+ *   - Pointers named d_* are DEVICE pointers (HBM, from zs3_dev_alloc or any HIP
+ *     allocation on the current device); h_* are host pointers.  The caller owns
+ *     all memory it passes in; the library owns its codec tables and staging.
+ *   - `stream` is a hipStream_t (NULL = the default stream of the current device).
+ *     Device-batch calls are asynchronous on that stream; host calls are synchronous.
+ *   - Shard layout inside one block ("stripe"): shard i is the S bytes at
+ *     base + i*S, S = ShardSize = ceil(block_len / k) (erasure-coding.go:122).  This
+ *     is exactly the reference's in-place Split layout in the bpool buffer
+ *     (erasure-coding.go:81, cap = 2*blockSize, erasure-sets.go:383-387).
+ *   - Thread-safety: codecs are immutable after creation except for internal
+ *     caches guarded by a mutex; every entry point may be called concurrently.
+ *     Host-pointer calls use per-OS-thread staging buffers and streams.
+ */
+#ifndef ZS3GPU_H
+#define ZS3GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes (reference sentinel each one maps to) ------------------ */
+#define ZS3_OK                  0
+#define ZS3_ERR_INV_SHARD_NUM  -1  /* reedsolomon.ErrInvShardNum  (erasure-coding.go:45)    */
+#define ZS3_ERR_MAX_SHARD_NUM  -2  /* reedsolomon.ErrMaxShardNum  (erasure-coding.go:49)    */
+#define ZS3_ERR_TOO_FEW_SHARDS -3  /* reedsolomon.ErrTooFewShards (erasure-utils.go:52)     */
+#define ZS3_ERR_SHARD_NO_DATA  -4  /* reedsolomon.ErrShardNoData                            */
+#define ZS3_ERR_SHARD_SIZE     -5  /* reedsolomon.ErrShardSize                              */
+#define ZS3_ERR_SHORT_DATA     -6  /* reedsolomon.ErrShortData    (erasure-utils.go:58)     */
+#define ZS3_ERR_FILE_CORRUPT   -7  /* errFileCorrupt (bitrot-streaming.go:185, bitrot.go:171) */
+#define ZS3_ERR_INVALID_ARG    -8  /* errInvalidArgument / errUnexpected                    */
+#define ZS3_ERR_DEVICE         -9  /* HIP runtime / kernel launch failure                   */
+#define ZS3_ERR_NOMEM         -10  /* allocation failure                                    */
+#define ZS3_ERR_SINGULAR      -11  /* internal: singular decode matrix (cannot happen for a valid pattern) */
+
+const char* zs3_strerror(int code);
+int zs3_version(void);                 /* (major << 16) | (minor << 8) | patch */
+
+/* ---- device ---------------------------------------------------------------- */
+int zs3_device_count(int* count);
+int zs3_set_device(int device);        /* hipSetDevice for the calling OS thread */
+int zs3_dev_alloc(void** d_ptr, size_t bytes);
+int zs3_dev_free(void* d_ptr);
+int zs3_host_alloc(void** h_ptr, size_t bytes);   /* pinned; backing for internal/bpool */
+int zs3_host_free(void* h_ptr);
+int zs3_memcpy_h2d(void* d_dst, const void* h_src, size_t bytes, void* stream);
+int zs3_memcpy_d2h(void* h_dst, const void* d_src, size_t bytes, void* stream);
+int zs3_stream_sync(void* stream);
+
+/* ---- codec: the Erasure value (erasure-coding.go:35-73) -------------------- */
+typedef struct zs3_codec zs3_codec;
+
+/* NewErasure (erasure-coding.go:42): k = dataBlocks, m = parityBlocks.
+ * k <= 0 || m <= 0 -> ZS3_ERR_INV_SHARD_NUM; k + m > 256 -> ZS3_ERR_MAX_SHARD_NUM.
+ * Builds (once) the klauspost systematic Vandermonde matrix for (k, m). */
+int zs3_codec_new(int k, int m, int64_t block_size, zs3_codec** out);
+void zs3_codec_free(zs3_codec* c);
+int zs3_codec_matrix(const zs3_codec* c, uint8_t* h_out /* (k+m)*k bytes */);
+
+/* Size arithmetic, exact Go semantics (int64, -1 = unknown length). */
+int64_t zs3_shard_size(const zs3_codec* c);                       /* Erasure.ShardSize      :122 */
+int64_t zs3_shard_file_size(const zs3_codec* c, int64_t total);   /* Erasure.ShardFileSize  :127 */
+int64_t zs3_shard_file_offset(const zs3_codec* c, int64_t start, int64_t length,
+                              int64_t total);                     /* Erasure.ShardFileOffset :141 */
+int64_t zs3_bitrot_shard_file_size(int64_t size, int64_t shard_size); /* bitrotShardFileSize bitrot.go:150 (HH256S) */
+
+/* ---- device-resident batches ----------------------------------------------
+ * A batch is n_blocks independent blocks of block_len bytes each (one 1 MiB
+ * erasure block per object stripe, erasure-encode.go:83-111).  S = ceil(block_len/k).
+ *
+ * zs3_encode_batch: Split + Encode (+ HighwayHash-256 of every shard chunk) —
+ *   EncodeData (erasure-coding.go:77) fused with streamingBitrotWriter.Write's
+ *   h.Reset/h.Write/h.Sum (bitrot-streaming.go:47-49) for all k+m shards.
+ *   data   : block b at d_data + b*data_stride, bytes [0, block_len); bytes up to
+ *            k*S read as zero (Split padding) — they are not written.
+ *   parity : block b parity row r at d_parity + b*parity_stride + r*S.  For the
+ *            reference's in-place layout pass d_parity = d_data + k*S and
+ *            parity_stride = data_stride.
+ *   sums   : optional (NULL = encode only); block b shard i digest at
+ *            d_sums + (b*(k+m) + i)*32, using the magic HH-256 key (bitrot.go:37).
+ *   block_len == 0 is EncodeData's empty case: nothing is written (no shards, no
+ *   sums, matching streamingBitrotWriter.Write's len(p)==0 no-op). */
+int zs3_encode_batch(const zs3_codec* c, const uint8_t* d_data, int64_t data_stride,
+                     int64_t block_len, int64_t n_blocks, uint8_t* d_parity,
+                     int64_t parity_stride, uint8_t* d_sums, void* stream);
+
+/* zs3_reconstruct_batch: ReconstructData (data_only != 0, DecodeDataBlocks
+ *   erasure-coding.go:96) or Reconstruct (DecodeDataAndParityBlocks :113) on every
+ *   block of a batch sharing one erasure pattern.  Block b shard i at
+ *   d_shards + b*block_stride + i*shard_len.  present[i] != 0 marks shard i present
+ *   (len != 0 in the Go [][]byte); missing rows are written in place.  Errors as
+ *   reedsolomon: fewer than k present -> ZS3_ERR_TOO_FEW_SHARDS; nothing present ->
+ *   ZS3_ERR_SHARD_NO_DATA; all needed present -> ZS3_OK with no work. */
+int zs3_reconstruct_batch(const zs3_codec* c, uint8_t* d_shards, int64_t block_stride,
+                          int64_t shard_len, int64_t n_blocks, const uint8_t* h_present,
+                          int data_only, void* stream);
+
+/* HighwayHash-256 of n_msgs messages of msg_len bytes at d_msgs + i*msg_stride
+ * (key = 32 bytes, NULL = the bitrot magic key).  Digest i at d_sums + 32*i. */
+int zs3_hh256_batch(const uint8_t* h_key, const uint8_t* d_msgs, int64_t msg_stride,
+                    int64_t msg_len, int64_t n_msgs, uint8_t* d_sums, void* stream);
+
+/* Bitrot verify (streamingBitrotReader.ReadAt, bitrot-streaming.go:171-186): hash
+ * each chunk and compare against d_want + 32*i; d_bad[i] = 1 where it differs
+ * (the per-shard errFileCorrupt, never a whole-batch failure). */
+int zs3_hh256_verify_batch(const uint8_t* h_key, const uint8_t* d_msgs, int64_t msg_stride,
+                           int64_t msg_len, int64_t n_msgs, const uint8_t* d_want,
+                           int32_t* d_bad, void* stream);
+
+/* Deterministic synthetic blocks (splitmix64 counter stream; identical to the
+ * oracle's fill): block b gets object id obj0 + b. */
+int zs3_fill_batch(uint8_t* d_out, int64_t stride, int64_t len, int64_t n_blocks,
+                   uint64_t seed, uint64_t obj0, void* stream);
+
+/* ---- host-pointer calls (synchronous; staged through pinned memory) ------- */
+
+/* Erasure.EncodeData in place (erasure-coding.go:77-91 with the bpool buffer):
+ * h_buf holds len data bytes and has capacity cap >= (k+m)*S.  On return bytes
+ * [len, k*S) are zero (Split), parity row r is at h_buf + (k+r)*S, and if h_sums
+ * is not NULL it receives the (k+m) HH-256 shard digests.  Returns S (>= 0) or an
+ * error (cap too small -> ZS3_ERR_INVALID_ARG).  len == 0 returns 0. */
+int64_t zs3_encode_data(const zs3_codec* c, uint8_t* h_buf, int64_t len, int64_t cap,
+                        uint8_t* h_sums);
+
+/* DecodeDataBlocks / DecodeDataAndParityBlocks on one host stripe of k+m rows of
+ * shard_len bytes (missing rows may hold garbage; they are overwritten). */
+int zs3_decode_data_blocks(const zs3_codec* c, uint8_t* h_shards, int64_t shard_len,
+                           const uint8_t* h_present, int data_only);
+
+/* HighwayHash-256 of one host message (key NULL = bitrot magic key). */
+int zs3_hh256(const uint8_t* h_key, const uint8_t* h_msg, int64_t len, uint8_t* h_out32);
+
+/* Startup self-tests through the device path: erasureSelfTest
+ * (erasure-coding.go:158-216, 60 (k, m) xxhash64 KATs + shard-0 rebuild) and
+ * bitrotSelfTest (bitrot.go:218-249).  Returns ZS3_OK or ZS3_ERR_FILE_CORRUPT. */
+int zs3_selftest(void);
+
+/* Which kernel served the last batch call on this thread: 1 = specialised
+ * (k, m) kernel, 0 = generic byte kernel. */
+int zs3_last_path(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ZS3GPU_H */

@@ -1,0 +1,100 @@
+"""CPU-only checks of the C-ABI library: it loads, exports every symbol
+include/zs3gpu.h declares, and the host-only entry points (NewErasure checks,
+size arithmetic, coding matrix) match the reference.  No compute calls."""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import zs3server_amd as z
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "zs3gpu.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(zs3_[a-z0-9_]+)\s*\(", src)))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def built():
+    import __graft_entry__ as g
+    g.build_lib()
+    z.lib()
+
+
+def test_header_matches_python_export_list():
+    assert header_functions() == sorted(z.EXPORTS)
+
+
+def test_library_exports_every_header_symbol():
+    out = subprocess.check_output(["nm", "-D", "--defined-only", z.LIB_PATH]).decode()
+    syms = {line.split()[-1] for line in out.splitlines() if line.strip()}
+    missing = [f for f in header_functions() if f not in syms]
+    assert not missing, missing
+
+
+def test_version_and_strerror():
+    L = z.lib()
+    assert L.zs3_version() == (0 << 16) | (1 << 8)
+    assert L.zs3_strerror(-3) == b"too few shards given"
+    assert L.zs3_strerror(-7) == b"file is corrupted"
+
+
+@pytest.mark.parametrize("k,m,code", [(0, 2, -1), (2, 0, -1), (-1, 4, -1), (200, 57, -2), (255, 2, -2)])
+def test_new_erasure_errors(k, m, code):
+    # cmd/erasure-coding.go:44-50
+    with pytest.raises(z.ZS3Error) as ei:
+        z.Codec(k, m, 1 << 20)
+    assert ei.value.code == code
+
+
+def test_new_erasure_max_shards_ok():
+    c = z.Codec(128, 128, 1 << 20)  # k+m == 256 is allowed
+    assert c.shard_size() == 8192
+
+
+def test_codec_matrix_matches_oracle(oracle):
+    for k, m in [(4, 2), (8, 4), (16, 4), (5, 3), (12, 4), (1, 1), (20, 12)]:
+        assert np.array_equal(z.Codec(k, m).matrix(), oracle.build_matrix(k, m))
+
+
+def ceil_frac(a, b):
+    # cmd/utils.go:691
+    if b == 0:
+        return 0
+    c = a // b if a >= 0 else -((-a) // b)
+    if a > 0 and a % b:
+        c = a // b + 1
+    return c
+
+
+@pytest.mark.parametrize("k,m,bs", [(4, 2, 1 << 20), (8, 4, 1 << 20), (16, 4, 1 << 20), (5, 3, 1 << 20),
+                                    (6, 2, 10 << 20), (12, 4, 1 << 20)])
+def test_shard_size_arithmetic(k, m, bs):
+    # Erasure.ShardSize / ShardFileSize / ShardFileOffset, cmd/erasure-coding.go:122-150
+    c = z.Codec(k, m, bs)
+    ss = ceil_frac(bs, k)
+    assert c.shard_size() == ss
+    assert c.shard_file_size(0) == 0
+    assert c.shard_file_size(-1) == -1
+    rng = np.random.default_rng(k * 100 + m)
+    for total in [1, 17, bs - 1, bs, bs + 1, 3 * bs + 5, 64 * bs] + list(rng.integers(1, 10 * bs, 20)):
+        total = int(total)
+        want = (total // bs) * ss + ceil_frac(total % bs, k)
+        assert c.shard_file_size(total) == want
+        for start, length in [(0, total), (total // 3, total - total // 3), (0, 0), (total - 1, 1)]:
+            till = ((start + length) // bs) * ss + ss
+            assert c.shard_file_offset(start, length, total) == min(till, want)
+
+
+def test_bitrot_shard_file_size():
+    # cmd/bitrot.go:150-155 (HighwayHash256S: 32-byte sum per shard chunk)
+    assert z.bitrot_shard_file_size(35, 10) == 4 * 32 + 35
+    assert z.bitrot_shard_file_size(131072, 131072) == 131072 + 32
+    assert z.bitrot_shard_file_size(0, 10) == 0
+    assert z.bitrot_shard_file_size(4 * 131072 + 1, 131072) == 5 * 32 + 4 * 131072 + 1

@@ -1,0 +1,88 @@
+"""Mirror of the streaming bitrot format (HighwayHash256S) over the zs3gpu C ABI.
+
+cmd/bitrot-streaming.go: every Write(p) of one shard chunk emits
+[32-byte HH256(p)][p]; ReadAt re-hashes each chunk and returns errFileCorrupt on
+mismatch.  cmd/bitrot.go:150-210: bitrotShardFileSize and bitrotVerify.
+Hashes are computed by the device kernel (zs3_hh256 / zs3_hh256_batch).
+"""
+from __future__ import annotations
+
+import io
+
+from . import MAGIC_HH256_KEY, ZS3Error, bitrot_shard_file_size, hh256
+
+HASH_SIZE = 32
+ERR_FILE_CORRUPT = -7
+ERR_UNEXPECTED = -8
+
+
+class StreamingBitrotWriter:
+    """newStreamingBitrotWriterBuffer (bitrot-streaming.go:84) — in-memory sink."""
+
+    def __init__(self, shard_size: int, sink=None):
+        self.shard_size = shard_size
+        self.iow = sink if sink is not None else io.BytesIO()
+
+    def Write(self, p: bytes) -> int:
+        # bitrot-streaming.go:43-65
+        if len(p) == 0:
+            return 0
+        self.iow.write(hh256(bytes(p), MAGIC_HH256_KEY))
+        self.iow.write(bytes(p))
+        return len(p)
+
+    def Close(self) -> None:
+        pass
+
+    def getvalue(self) -> bytes:
+        return self.iow.getvalue()
+
+
+class StreamingBitrotReader:
+    """newStreamingBitrotReader over an in-memory shard file (bitrot-streaming.go:192)."""
+
+    def __init__(self, data: bytes, till_offset: int, shard_size: int):
+        self.data = data
+        self.shard_size = shard_size
+        self.till_offset = -(-till_offset // shard_size) * HASH_SIZE + till_offset
+        self.rc = None
+        self.curr_offset = 0
+
+    def ReadAt(self, n: int, offset: int) -> bytes:
+        # bitrot-streaming.go:142-189
+        if offset % self.shard_size != 0:
+            raise ZS3Error(ERR_UNEXPECTED, "ReadAt: unaligned offset")
+        if self.rc is None:
+            self.curr_offset = offset
+            stream_offset = (offset // self.shard_size) * HASH_SIZE + offset
+            self.rc = io.BytesIO(self.data[stream_offset:self.till_offset])
+        if offset != self.curr_offset:
+            raise ZS3Error(ERR_UNEXPECTED, "ReadAt: non-sequential offset")
+        want = self.rc.read(HASH_SIZE)
+        buf = self.rc.read(n)
+        if len(want) != HASH_SIZE or len(buf) != n:
+            raise ZS3Error(ERR_UNEXPECTED, "ReadAt: short read (io.ErrUnexpectedEOF)")
+        if hh256(buf, MAGIC_HH256_KEY) != want:
+            raise ZS3Error(ERR_FILE_CORRUPT, "ReadAt: content hash does not match")
+        self.curr_offset += n
+        return buf
+
+
+def bitrot_verify(stream: bytes, want_size: int, part_size: int, shard_size: int) -> None:
+    """bitrotVerify for HighwayHash256S (cmd/bitrot.go:158-210): raises errFileCorrupt."""
+    if want_size != bitrot_shard_file_size(part_size, shard_size):
+        raise ZS3Error(ERR_FILE_CORRUPT, "bitrotVerify: size")
+    r = io.BytesIO(stream)
+    left = want_size
+    while left > 0:
+        h = r.read(HASH_SIZE)
+        if len(h) != HASH_SIZE:
+            raise ZS3Error(ERR_FILE_CORRUPT, "bitrotVerify: short hash")
+        left -= HASH_SIZE
+        if left < shard_size:
+            shard_size = left
+        chunk = r.read(shard_size)
+        left -= len(chunk)
+        if hh256(chunk, MAGIC_HH256_KEY) != h:
+            raise ZS3Error(ERR_FILE_CORRUPT, "bitrotVerify: hash mismatch")
+    return None

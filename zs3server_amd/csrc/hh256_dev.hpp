@@ -1,0 +1,141 @@
+// hh256_dev.hpp — HighwayHash-256 on CDNA4 (gfx950), one chain per quad.
+//
+// Restates minio/highwayhash v1.0.2 (== Google's C reference) as used by the
+// streaming bitrot writer/reader: cmd/bitrot.go:47-64 (hash factory, magic key
+// cmd/bitrot.go:37) and cmd/bitrot-streaming.go:47-49 / :171-182.
+//
+// Mapping: HighwayHash keeps 4 independent 64-bit lanes (v0, v1, mul0, mul1)
+// that only interact in ZipperMergeAndAdd, which mixes lane pairs (0,1) and
+// (2,3).  Each thread of a quad owns ONE HH lane; the zipper needs only the
+// partner's high dword, fetched with one DPP quad_perm [1,0,3,2] move.  A
+// 64-lane wavefront therefore advances 16 independent hash chains in lockstep.
+// Per packet and thread: 2 x v_lshl_add_u64, 2 x v_mad_u64_u32, 4 x xor,
+// 2 x DPP, 6 x v_perm_b32, 2 x 64-bit add.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace zs3dev {
+
+struct HHLane {
+    uint64_t v0, v1, mul0, mul1;
+};
+
+__device__ __forceinline__ uint32_t dpp_xor1(uint32_t v) {  // lane ^ 1 within the quad
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint32_t dpp_xor2(uint32_t v) {  // lane ^ 2 within the quad
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);
+}
+
+// Zipper-merge term for this thread's lane from its own 64-bit value and the
+// partner lane's high dword.  Byte maps (C reference ZipperMergeAndAdd):
+//   even lane: [o3 p4 o2 o5 | p6 o1 p7 o0]   odd lane: [o3 p4 o2 o5 | o1 p6 o0 p7]
+// (oN = own byte N, pN = partner byte N); v_perm_b32 selects byte i of {S0:S1}.
+__device__ __forceinline__ uint64_t zipper(uint64_t own, uint32_t partner_hi, uint32_t sel_hi) {
+    const uint32_t olo = (uint32_t)own, ohi = (uint32_t)(own >> 32);
+    const uint32_t t = __builtin_amdgcn_perm(partner_hi, olo, 0x0c020403u);
+    const uint32_t lo = __builtin_amdgcn_perm(t, ohi, 0x01060504u);
+    const uint32_t hi = __builtin_amdgcn_perm(partner_hi, olo, sel_hi);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint32_t zipper_sel(int lane) {
+    return (lane & 1) ? 0x07000601u : 0x00070106u;
+}
+
+// One HighwayHash Update() step for this thread's lane (C reference Update).
+__device__ __forceinline__ void hh_update(HHLane& s, uint64_t w, uint32_t sel_hi) {
+    s.v1 += s.mul0 + w;
+    s.mul0 ^= (uint64_t)(uint32_t)s.v1 * (s.v0 >> 32);
+    s.v0 += s.mul1;
+    s.mul1 ^= (uint64_t)(uint32_t)s.v0 * (s.v1 >> 32);
+    s.v0 += zipper(s.v1, dpp_xor1((uint32_t)(s.v1 >> 32)), sel_hi);
+    s.v1 += zipper(s.v0, dpp_xor1((uint32_t)(s.v0 >> 32)), sel_hi);
+}
+
+// Initial state for lane `lane` under key words key[0..3] (C reference Reset).
+__device__ __forceinline__ HHLane hh_init(int lane, uint64_t k0, uint64_t k1, uint64_t k2, uint64_t k3) {
+    const uint64_t key = lane == 0 ? k0 : lane == 1 ? k1 : lane == 2 ? k2 : k3;
+    const uint64_t i0 = lane == 0 ? 0xdbe6d5d5fe4cce2fULL
+                      : lane == 1 ? 0xa4093822299f31d0ULL
+                      : lane == 2 ? 0x13198a2e03707344ULL
+                                  : 0x243f6a8885a308d3ULL;
+    const uint64_t i1 = lane == 0 ? 0x3bd39e10cb0ef593ULL
+                      : lane == 1 ? 0xc0acf169b5f18a8cULL
+                      : lane == 2 ? 0xbe5466cf34e90c6cULL
+                                  : 0x452821e638d01377ULL;
+    HHLane s;
+    s.mul0 = i0;
+    s.mul1 = i1;
+    s.v0 = i0 ^ key;
+    s.v1 = i1 ^ ((key >> 32) | (key << 32));
+    return s;
+}
+
+// Hash `npk` full 32-byte packets of a row staged in LDS (8-byte aligned).
+__device__ __forceinline__ void hh_packets(HHLane& s, const uint8_t* row, int npk, int lane,
+                                           uint32_t sel_hi) {
+    const uint64_t* p = reinterpret_cast<const uint64_t*>(row) + lane;
+#pragma unroll 4
+    for (int i = 0; i < npk; ++i) hh_update(s, p[4 * i], sel_hi);
+}
+
+__device__ __forceinline__ uint32_t rotl32(uint32_t x, uint32_t n) {
+    return __builtin_amdgcn_alignbit(x, x, 32u - n);  // n in 1..31
+}
+
+// HighwayHashUpdateRemainder for the final size_mod32 = n (1..31) bytes at `tail`
+// (LDS).  The packet is zero-filled, holds tail[0 .. n&~3), and then either
+// packet[28..31] = last 4 bytes (n & 16) or packet[16..18] = the 1-3 trailing bytes.
+__device__ __forceinline__ void hh_remainder(HHLane& s, const uint8_t* tail, uint32_t n, int lane,
+                                             uint32_t sel_hi) {
+    s.v0 += ((uint64_t)n << 32) + n;
+    s.v1 = ((uint64_t)rotl32((uint32_t)(s.v1 >> 32), n) << 32) | rotl32((uint32_t)s.v1, n);
+    const uint32_t remain = n & ~3u, mod4 = n & 3u;
+    uint8_t b[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint32_t idx = 8u * lane + i;
+        b[i] = idx < remain ? tail[idx] : 0;
+    }
+    if (n & 16u) {
+        if (lane == 3) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) b[4 + i] = tail[n - 4 + i];
+        }
+    } else if (mod4) {
+        if (lane == 2) {
+            b[0] = tail[remain];
+            b[1] = tail[remain + (mod4 >> 1)];
+            b[2] = tail[n - 1];
+        }
+    }
+    uint64_t w = 0;
+#pragma unroll
+    for (int i = 7; i >= 0; --i) w = (w << 8) | b[i];
+    hh_update(s, w, sel_hi);
+}
+
+// 10 PermuteAndUpdate rounds + ModularReduction.  Returns this lane's 64-bit
+// digest word h[lane] (digest = h0||h1||h2||h3 little-endian).
+__device__ __forceinline__ uint64_t hh_finalize256(HHLane& s, int lane, uint32_t sel_hi) {
+    for (int r = 0; r < 10; ++r) {
+        // permuted[l] = rot32(v0[(l + 2) & 3])
+        const uint32_t plo = dpp_xor2((uint32_t)s.v0);
+        const uint32_t phi = dpp_xor2((uint32_t)(s.v0 >> 32));
+        hh_update(s, ((uint64_t)plo << 32) | phi, sel_hi);
+    }
+    const uint64_t a_hi = s.v1 + s.mul1;  // a3 (odd lane) / a2 (even lane)
+    const uint64_t a_lo = s.v0 + s.mul0;  // a1 (odd lane) / a0 (even lane)
+    const uint32_t q_lo = dpp_xor1((uint32_t)a_hi);
+    const uint32_t q_hi = dpp_xor1((uint32_t)(a_hi >> 32));
+    if (lane & 1) {
+        const uint64_t a2 = ((uint64_t)q_hi << 32) | q_lo;
+        const uint64_t a3 = a_hi & 0x3FFFFFFFFFFFFFFFULL;
+        return a_lo ^ ((a3 << 1) | (a2 >> 63)) ^ ((a3 << 2) | (a2 >> 62));
+    }
+    return a_lo ^ (a_hi << 1) ^ (a_hi << 2);
+}
+
+}  // namespace zs3dev

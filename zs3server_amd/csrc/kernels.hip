@@ -1,0 +1,582 @@
+// kernels.hip — gfx950 kernels for the erasure-shard + bitrot-hash data path.
+//
+// Replaces the arithmetic behind:
+//   Erasure.EncodeData                cmd/erasure-coding.go:77-91  (Split + Encode)
+//   Erasure.DecodeDataBlocks          cmd/erasure-coding.go:96-109 (ReconstructData)
+//   Erasure.DecodeDataAndParityBlocks cmd/erasure-coding.go:113-119 (Reconstruct)
+//   streamingBitrotWriter.Write       cmd/bitrot-streaming.go:43-65 (HH256 per shard chunk)
+//   streamingBitrotReader.ReadAt      cmd/bitrot-streaming.go:142-189 (HH256 verify)
+//
+// Design: the fused kernel owns G whole (object, block) stripes per
+// workgroup and walks them in tiles of T bytes per shard row.  Each tile:
+//   1. data columns (16 B per thread per shard) are loaded with coalesced
+//      global_load_dwordx4 one tile AHEAD into registers,
+//   2. the m parity columns are computed in registers (v_perm nibble tables +
+//      v_bitop3 XOR3), data+parity are written to an LDS tile, parity is stored,
+//   3. each quad hashes one shard row of the tile from LDS (HighwayHash lane per
+//      thread), so every stripe byte is read from HBM once and parity is hashed
+//      without being re-read.
+// HBM traffic per block = B (data) + B*m/k (parity) + 32*(k+m) (sums).
+#include "kernels.hpp"
+#include "gf_dev.hpp"
+#include "hh256_dev.hpp"
+
+using namespace zs3dev;
+
+namespace zs3k {
+
+static int g_variant = 0;
+void set_variant(int v) { g_variant = v; }
+int get_variant() { return g_variant; }
+
+// Barrier that only drains LDS traffic: __syncthreads() would also wait for the
+// tile prefetch (vmcnt(0)) and serialise HBM latency with the hash phase.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+__device__ __forceinline__ uint4 ld16(const uint8_t* p) {
+    uint4 v;
+    __builtin_memcpy(&v, p, 16);  // global_load_dwordx4 (unaligned-access mode)
+    return v;
+}
+__device__ __forceinline__ void st16(uint8_t* p, const uint4& v) { __builtin_memcpy(p, &v, 16); }
+
+// An SGPR zero the compiler cannot see through: indexing the LDS coefficient
+// tables with it keeps their loads inside the loop instead of hoisting all
+// m*k*5 dwords into VGPRs (which would cap occupancy at one wave per SIMD).
+__device__ __forceinline__ int opaque_zero() {
+    int z = 0;
+    asm volatile("" : "+s"(z));
+    return z;
+}
+
+constexpr int gcd_c(int a, int b) { return b ? gcd_c(b, a % b) : a; }
+
+// Stripes per workgroup: smallest G making 4*G*(k+m) a multiple of 64 (so every
+// hash lane of every wavefront is used), capped at 512 hash threads.
+template <int R>
+constexpr int pick_G() {
+    int g = 16 / gcd_c(R, 16);
+    while (g > 1 && 4 * g * R > 512) g /= 2;
+    while (4 * g * R < 192) g *= 2;  // at least three wavefronts per workgroup
+    return g;
+}
+constexpr int round64(int x) { return (x + 63) / 64 * 64; }
+
+// Tile bytes per shard row so that NBUF LDS tiles stay under ~40 KiB (3-4
+// workgroups resident per CU).
+template <int ROWS, int NBUF>
+constexpr int pick_T() {
+    return (NBUF * ROWS * (1024 + 32) <= 40960) ? 1024
+         : (NBUF * ROWS * (512 + 32) <= 40960)  ? 512
+                                                 : 256;
+}
+
+// ---------------------------------------------------------------------------
+// Fused Split + Encode + HighwayHash-256 over G stripes per workgroup.
+template <int K, int M, int G, int T, int NBUF, int NT>
+__global__ void __launch_bounds__(NT) k_encode_hash(EncArgs a) {
+    constexpr int R = K + M;
+    constexpr int TS = T + 32;  // LDS row stride: +8 banks per row, conflict-free b64 reads
+    constexpr int CPB = T / 16;  // 16-byte columns per stripe per tile
+    constexpr int NCOL = G * CPB;
+    constexpr int CPT = (NCOL + NT - 1) / NT;
+
+    __shared__ __attribute__((aligned(16))) uint8_t tile[NBUF][G * R * TS];
+    __shared__ __attribute__((aligned(16))) uint32_t tabs[M * K * 8];
+
+    const int tid = threadIdx.x;
+    const int64_t blk0 = (int64_t)blockIdx.x * G;
+    const int64_t S = a.S, n = a.n;
+
+    for (int i = tid; i < M * K * 8; i += NT) tabs[i] = a.tables[i];
+
+    // ---- hash-chain role: quad = one shard row of one stripe
+    const int chain = tid >> 2, lane = tid & 3;
+    const bool chain_live = chain < G * R && (blk0 + chain / R) < a.n_blocks;
+    const int crow = chain < G * R ? chain : 0;
+    const uint32_t sel = zipper_sel(lane);
+    HHLane st = hh_init(lane, a.key[0], a.key[1], a.key[2], a.key[3]);
+
+    // ---- encode role: CPT columns per thread
+    uint4 x[CPT][K] = {};
+    auto prefetch = [&](int64_t t0) {
+#pragma unroll
+        for (int c = 0; c < CPT; ++c) {
+            const int col = tid + c * NT;
+            const int g = col / CPB;
+            const int o = (col % CPB) * 16;
+            // Dead stripes of the last workgroup alias the last live block: they
+            // recompute and store byte-identical parity (benign), so the encode has
+            // no data-dependent branches (which make hipcc split the parity rows and
+            // keep every shard's nibbles live).
+            const int64_t b = (blk0 + g) < a.n_blocks ? (blk0 + g) : (a.n_blocks - 1);
+            const bool live = col < NCOL && t0 + o < S;
+            const uint8_t* blk = a.data + b * a.data_stride;
+#pragma unroll
+            for (int j = 0; j < K; ++j)
+                if (live) x[c][j] = ld16(blk + (int64_t)j * S + t0 + o);
+        }
+    };
+
+    auto encode_store = [&](int64_t t0, int L, uint8_t* tl) {
+#pragma unroll
+        for (int c = 0; c < CPT; ++c) {
+            const int col = tid + c * NT;
+            if (col >= NCOL) continue;
+            const int g = col / CPB;
+            const int o = (col % CPB) * 16;
+            const int64_t b = (blk0 + g) < a.n_blocks ? (blk0 + g) : (a.n_blocks - 1);
+            if (o >= L) continue;
+            const uint32_t* tb = tabs + opaque_zero();
+            GfAcc acc[M][4];
+#pragma unroll
+            for (int r = 0; r < M; ++r)
+#pragma unroll
+                for (int w = 0; w < 4; ++w) acc_init(acc[r][w]);
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                __builtin_amdgcn_sched_barrier(0);  // keep each shard's table reads local
+                const Nib n0 = split_nibbles(x[c][j].x), n1 = split_nibbles(x[c][j].y);
+                const Nib n2 = split_nibbles(x[c][j].z), n3 = split_nibbles(x[c][j].w);
+#pragma unroll
+                for (int r = 0; r < M; ++r) {
+                    const CoefTab t = load_coef(tb, r * K + j);
+                    acc_add(acc[r][0], gf_lookup(n0, t));
+                    acc_add(acc[r][1], gf_lookup(n1, t));
+                    acc_add(acc[r][2], gf_lookup(n2, t));
+                    acc_add(acc[r][3], gf_lookup(n3, t));
+                }
+                *reinterpret_cast<uint4*>(tl + (g * R + j) * TS + o) = x[c][j];
+            }
+            uint8_t* pbase = a.parity + b * a.parity_stride + t0 + o;
+#pragma unroll
+            for (int r = 0; r < M; ++r) {
+                const uint4 p = make_uint4(acc_done(acc[r][0]), acc_done(acc[r][1]),
+                                           acc_done(acc[r][2]), acc_done(acc[r][3]));
+                *reinterpret_cast<uint4*>(tl + (g * R + K + r) * TS + o) = p;
+                st16(pbase + (int64_t)r * S, p);
+            }
+        }
+    };
+
+    lds_barrier();  // tables visible
+    prefetch(0);
+    int it = 0;
+    for (int64_t t0 = 0; t0 < S; t0 += T, ++it) {
+        const int L = (int)((S - t0) < T ? (S - t0) : T);
+        uint8_t* tl = tile[NBUF == 1 ? 0 : (it & 1)];
+        encode_store(t0, L, tl);
+        if (t0 + T < S) prefetch(t0 + T);
+        lds_barrier();
+        const uint8_t* row = tl + crow * TS;
+        hh_packets(st, row, L >> 5, lane, sel);
+        if (t0 + L >= S && (L & 31)) hh_remainder(st, row + (L & ~31), (uint32_t)(L & 31), lane, sel);
+        if (NBUF == 1) lds_barrier();
+    }
+    const uint64_t h = hh_finalize256(st, lane, sel);
+    if (chain_live) {
+        const int64_t b = blk0 + chain / R;
+        const int s = chain % R;
+        uint8_t* out = a.sums + (b * R + s) * 32 + 8 * lane;
+        *reinterpret_cast<uint64_t*>(out) = h;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Encode only (no hash): one thread per 16-byte column, K loads -> M stores.
+template <int K, int M>
+__global__ void __launch_bounds__(256) k_encode_only(EncArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t tabs[M * K * 8];
+    for (int i = threadIdx.x; i < M * K * 8; i += 256) tabs[i] = a.tables[i];
+    __syncthreads();
+    const int64_t S = a.S, n = a.n;
+    const int64_t cols = (S + 15) >> 4;
+    for (int64_t b = blockIdx.y; b < a.n_blocks; b += gridDim.y) {
+        const uint8_t* blk = a.data + b * a.data_stride;
+        uint8_t* pb = a.parity + b * a.parity_stride;
+        for (int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x; c < cols; c += (int64_t)gridDim.x * 256) {
+            const int64_t o = c * 16;
+            const uint32_t* tb = tabs + opaque_zero();
+            uint4 x[K];
+#pragma unroll
+            for (int j = 0; j < K; ++j) x[j] = ld16(blk + (int64_t)j * S + o);
+            GfAcc acc[M][4];
+#pragma unroll
+            for (int r = 0; r < M; ++r)
+#pragma unroll
+                for (int w = 0; w < 4; ++w) acc_init(acc[r][w]);
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                __builtin_amdgcn_sched_barrier(0);  // keep each shard's table reads local
+                const Nib n0 = split_nibbles(x[j].x), n1 = split_nibbles(x[j].y);
+                const Nib n2 = split_nibbles(x[j].z), n3 = split_nibbles(x[j].w);
+#pragma unroll
+                for (int r = 0; r < M; ++r) {
+                    const CoefTab t = load_coef(tb, r * K + j);
+                    acc_add(acc[r][0], gf_lookup(n0, t));
+                    acc_add(acc[r][1], gf_lookup(n1, t));
+                    acc_add(acc[r][2], gf_lookup(n2, t));
+                    acc_add(acc[r][3], gf_lookup(n3, t));
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < M; ++r) {
+                const uint4 p = make_uint4(acc_done(acc[r][0]), acc_done(acc[r][1]),
+                                           acc_done(acc[r][2]), acc_done(acc[r][3]));
+                st16(pb + (int64_t)r * S + o, p);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Reconstruct: E_MAX output rows, each a GF combination of the K valid rows.
+template <int K, int EMAX>
+__global__ void __launch_bounds__(256) k_reconstruct(RecArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t tabs[EMAX * K * 8];
+    __shared__ int32_t rows[K + EMAX];
+    for (int i = threadIdx.x; i < a.e * K * 8; i += 256) tabs[i] = a.tables[i];
+    for (int i = threadIdx.x; i < K + a.e; i += 256) rows[i] = a.rows[i];
+    __syncthreads();
+    const int64_t S = a.S;
+    const int64_t cols = (S + 15) >> 4;
+    const int E = a.e;
+    for (int64_t b = blockIdx.y; b < a.n_blocks; b += gridDim.y) {
+        uint8_t* blk = a.shards + b * a.block_stride;
+        for (int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x; c < cols; c += (int64_t)gridDim.x * 256) {
+            const int64_t o = c * 16;
+            const uint32_t* tbl = tabs + opaque_zero();
+            uint4 x[K];
+#pragma unroll
+            for (int t = 0; t < K; ++t) x[t] = ld16(blk + (int64_t)rows[t] * S + o);
+            GfAcc acc[EMAX][4];
+#pragma unroll
+            for (int r = 0; r < EMAX; ++r)
+#pragma unroll
+                for (int w = 0; w < 4; ++w) acc_init(acc[r][w]);
+#pragma unroll
+            for (int t = 0; t < K; ++t) {
+                const Nib n0 = split_nibbles(x[t].x), n1 = split_nibbles(x[t].y);
+                const Nib n2 = split_nibbles(x[t].z), n3 = split_nibbles(x[t].w);
+#pragma unroll
+                for (int r = 0; r < EMAX; ++r) {
+                    if (r < E) {
+                        const CoefTab tb = load_coef(tbl, r * K + t);
+                        acc_add(acc[r][0], gf_lookup(n0, tb));
+                        acc_add(acc[r][1], gf_lookup(n1, tb));
+                        acc_add(acc[r][2], gf_lookup(n2, tb));
+                        acc_add(acc[r][3], gf_lookup(n3, tb));
+                    }
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < EMAX; ++r) {
+                if (r < E) {
+                    const uint4 p = make_uint4(acc_done(acc[r][0]), acc_done(acc[r][1]),
+                                               acc_done(acc[r][2]), acc_done(acc[r][3]));
+                    st16(blk + (int64_t)rows[K + r] * S + o, p);
+                }
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Generic byte path: any k, m (k+m <= 256), any shard size and alignment.
+// One stripe per workgroup; tile rows staged in LDS; log/exp GF tables in LDS.
+constexpr int GEN_T = 256;
+constexpr int GEN_TS = GEN_T + 32;
+
+__global__ void __launch_bounds__(1024) k_encode_hash_generic(EncArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int k = a.k, m = a.m, R = k + m;
+    uint8_t* tile = smem;                           // R * GEN_TS
+    uint8_t* lg = smem + (size_t)R * GEN_TS;        // 256
+    uint8_t* ex = lg + 256;                         // 512
+    uint8_t* mat = ex + 512;                        // m * k parity rows
+    const int tid = threadIdx.x, NT = blockDim.x;
+    // build GF tables
+    if (tid == 0) {
+        unsigned v = 1;
+        for (int i = 0; i < 255; ++i) {
+            ex[i] = (uint8_t)v;
+            lg[v] = (uint8_t)i;
+            v <<= 1;
+            if (v & 0x100) v ^= 0x11D;
+        }
+        for (int i = 255; i < 512; ++i) ex[i] = ex[i - 255];
+        lg[0] = 0;
+    }
+    for (int i = tid; i < m * k; i += NT) mat[i] = a.matrix[(size_t)k * k + i];
+    __syncthreads();
+
+    const int64_t S = a.S, n = a.n;
+    const bool hash = a.sums != nullptr;
+    const int chain = tid >> 2, lane = tid & 3;
+    const int crow = chain < R ? chain : 0;
+    const uint32_t sel = zipper_sel(lane);
+    for (int64_t b = blockIdx.x; b < a.n_blocks; b += gridDim.x) {
+        const uint8_t* blk = a.data + b * a.data_stride;
+        uint8_t* pb = a.parity + b * a.parity_stride;
+        HHLane st = hh_init(lane, a.key[0], a.key[1], a.key[2], a.key[3]);
+        for (int64_t t0 = 0; t0 < S; t0 += GEN_T) {
+            const int L = (int)((S - t0) < GEN_T ? (S - t0) : GEN_T);
+            for (int i = tid; i < k * L; i += NT) {
+                const int j = i / L, o = i - j * L;
+                const int64_t pos = (int64_t)j * S + t0 + o;
+                tile[j * GEN_TS + o] = pos < n ? blk[pos] : (uint8_t)0;
+            }
+            __syncthreads();
+            for (int i = tid; i < m * L; i += NT) {
+                const int r = i / L, o = i - r * L;
+                uint8_t acc = 0;
+                for (int j = 0; j < k; ++j) acc ^= gf_mul_log(lg, ex, mat[r * k + j], tile[j * GEN_TS + o]);
+                tile[(k + r) * GEN_TS + o] = acc;
+                pb[(int64_t)r * S + t0 + o] = acc;
+            }
+            __syncthreads();
+            if (hash && chain < R) {
+                const uint8_t* row = tile + crow * GEN_TS;
+                hh_packets(st, row, L >> 5, lane, sel);
+                if (t0 + L >= S && (L & 31)) hh_remainder(st, row + (L & ~31), (uint32_t)(L & 31), lane, sel);
+            }
+            __syncthreads();
+        }
+        if (hash && chain < R) {
+            const uint64_t h = hh_finalize256(st, lane, sel);
+            *reinterpret_cast<uint64_t*>(a.sums + (b * R + chain) * 32 + 8 * lane) = h;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_reconstruct_generic(RecArgs a) {
+    __shared__ uint8_t lg[256], ex[512];
+    extern __shared__ uint8_t coef[];  // e*k coefficients then rows
+    const int k = a.k, E = a.e;
+    if (threadIdx.x == 0) {
+        unsigned v = 1;
+        for (int i = 0; i < 255; ++i) {
+            ex[i] = (uint8_t)v;
+            lg[v] = (uint8_t)i;
+            v <<= 1;
+            if (v & 0x100) v ^= 0x11D;
+        }
+        for (int i = 255; i < 512; ++i) ex[i] = ex[i - 255];
+        lg[0] = 0;
+    }
+    int32_t* rows = reinterpret_cast<int32_t*>(coef + ((E * k + 3) & ~3));
+    for (int i = threadIdx.x; i < E * k; i += blockDim.x) coef[i] = a.coef[i];
+    for (int i = threadIdx.x; i < k + E; i += blockDim.x) rows[i] = a.rows[i];
+    __syncthreads();
+    const int64_t S = a.S;
+    for (int64_t b = blockIdx.y; b < a.n_blocks; b += gridDim.y) {
+        uint8_t* blk = a.shards + b * a.block_stride;
+        for (int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; o < S; o += (int64_t)gridDim.x * blockDim.x) {
+            for (int r = 0; r < E; ++r) {
+                uint8_t acc = 0;
+                for (int t = 0; t < k; ++t)
+                    acc ^= gf_mul_log(lg, ex, coef[r * k + t], blk[(int64_t)rows[t] * S + o]);
+                blk[(int64_t)rows[k + r] * S + o] = acc;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// HighwayHash-256 of n messages (64 chains = 256 threads per workgroup), with
+// optional compare against expected digests (streamingBitrotReader.ReadAt,
+// cmd/bitrot-streaming.go:180-186: per-shard errFileCorrupt, not whole-batch).
+constexpr int HB_CH = 64;
+constexpr int HB_T = 256;
+constexpr int HB_TS = HB_T + 32;
+
+__global__ void __launch_bounds__(256) k_hash_batch(HashArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t tile[HB_CH * HB_TS];
+    const int tid = threadIdx.x;
+    const int64_t m0 = (int64_t)blockIdx.x * HB_CH;
+    const int chain = tid >> 2, lane = tid & 3;
+    const uint32_t sel = zipper_sel(lane);
+    HHLane st = hh_init(lane, a.key[0], a.key[1], a.key[2], a.key[3]);
+    const int64_t len = a.len;
+    for (int64_t t0 = 0; t0 < len; t0 += HB_T) {
+        const int L = (int)((len - t0) < HB_T ? (len - t0) : HB_T);
+        // coalesced staging: 16-byte pieces, row-major
+        for (int i = tid; i < HB_CH * (HB_T / 16); i += 256) {
+            const int r = i / (HB_T / 16), o = (i % (HB_T / 16)) * 16;
+            const int64_t msg = m0 + r;
+            if (msg < a.n && o < L) {
+                const uint8_t* src = a.msgs + msg * a.stride + t0 + o;
+                uint4 v;
+                if (o + 16 <= L) {
+                    v = ld16(src);
+                } else {
+                    uint8_t tb[16] = {0};
+                    for (int q = 0; q < L - o; ++q) tb[q] = src[q];
+                    __builtin_memcpy(&v, tb, 16);
+                }
+                *reinterpret_cast<uint4*>(tile + r * HB_TS + o) = v;
+            }
+        }
+        lds_barrier();
+        const uint8_t* row = tile + chain * HB_TS;
+        hh_packets(st, row, L >> 5, lane, sel);
+        if (t0 + L >= len && (L & 31)) hh_remainder(st, row + (L & ~31), (uint32_t)(L & 31), lane, sel);
+        lds_barrier();
+    }
+    const uint64_t h = hh_finalize256(st, lane, sel);
+    const int64_t msg = m0 + chain;
+    if (msg < a.n) {
+        if (a.sums) *reinterpret_cast<uint64_t*>(a.sums + msg * 32 + 8 * lane) = h;
+        if (a.expect && a.bad) {
+            uint64_t want;
+            __builtin_memcpy(&want, a.expect + msg * 32 + 8 * lane, 8);
+            const unsigned long long mism = __ballot(want != h);
+            const unsigned q = (unsigned)((mism >> (tid & 60)) & 0xFull);
+            if (lane == 0) a.bad[msg] = q ? 1 : 0;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Synthetic input: counter-based splitmix64 (== oracle_fill in oracle/zs3_oracle.c).
+__device__ __forceinline__ uint64_t sm_mix(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+    return z ^ (z >> 31);
+}
+
+__global__ void __launch_bounds__(256) k_fill(uint8_t* out, int64_t stride, int64_t len, int64_t n,
+                                              uint64_t seed, uint64_t obj0) {
+    const int64_t nw = (len + 7) >> 3;
+    for (int64_t b = blockIdx.y; b < n; b += gridDim.y) {
+        const uint64_t s0 = seed + ((obj0 + (uint64_t)b) << 40);
+        uint8_t* o = out + b * stride;
+        const bool al = (((uintptr_t)o) & 7) == 0;
+        for (int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x; w < nw; w += (int64_t)gridDim.x * 256) {
+            const uint64_t v = sm_mix(s0 + (uint64_t)(w + 1) * 0x9e3779b97f4a7c15ULL);
+            if (al && w * 8 + 8 <= len) {
+                *reinterpret_cast<uint64_t*>(o + w * 8) = v;
+            } else {
+                for (int i = 0; i < 8 && w * 8 + i < len; ++i) o[w * 8 + i] = (uint8_t)(v >> (8 * i));
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Dispatch
+template <int K, int M>
+static hipError_t run_encode_fast(const EncArgs& a, hipStream_t s) {
+    if (a.sums) {
+        constexpr int R = K + M;
+        constexpr int G = pick_G<R>();
+        constexpr int NBUF = 2;
+        constexpr int T = pick_T<G * R, NBUF>();
+        constexpr int NT = round64(4 * G * R);
+        const int64_t grid = (a.n_blocks + G - 1) / G;
+        hipLaunchKernelGGL((k_encode_hash<K, M, G, T, NBUF, NT>), dim3((unsigned)grid), dim3(NT), 0, s, a);
+    } else {
+        const int64_t cols = (a.S + 15) >> 4;
+        const unsigned gx = (unsigned)((cols + 255) / 256);
+        const unsigned gy = (unsigned)(a.n_blocks < 65535 ? a.n_blocks : 65535);
+        hipLaunchKernelGGL((k_encode_only<K, M>), dim3(gx, gy), dim3(256), 0, s, a);
+    }
+    return hipGetLastError();
+}
+
+#define ZS3_FAST_KM(X) \
+    X(2, 1) X(2, 2) X(3, 2) X(3, 3) X(4, 2) X(4, 3) X(4, 4) X(5, 3) X(6, 2) X(6, 3) X(6, 4) \
+    X(8, 2) X(8, 3) X(8, 4) X(10, 4) X(12, 4) X(16, 4)
+
+bool has_fast_encode(int k, int m) {
+#define X(K, M) if (k == K && m == M) return true;
+    ZS3_FAST_KM(X)
+#undef X
+    return false;
+}
+
+hipError_t launch_encode(const EncArgs& a, hipStream_t s, bool* used_fast) {
+    if (a.n_blocks <= 0 || a.S <= 0) return hipSuccess;
+    // Vectorised kernels: 16-byte shard columns and no Split padding.
+    const bool vec_ok = (a.S % 16) == 0 && a.n == (int64_t)a.k * a.S;
+#define X(K, M)                                  \
+    if (vec_ok && a.k == K && a.m == M) {        \
+        if (used_fast) *used_fast = true;        \
+        return run_encode_fast<K, M>(a, s);      \
+    }
+    ZS3_FAST_KM(X)
+#undef X
+    if (used_fast) *used_fast = false;
+    const int R = a.k + a.m;
+    int nt = round64(4 * R);
+    if (nt < 256) nt = 256;
+    if (nt > 1024) nt = 1024;
+    const size_t lds = (size_t)R * GEN_TS + 256 + 512 + (size_t)a.m * a.k;
+    hipError_t e = hipFuncSetAttribute((const void*)k_encode_hash_generic,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    const unsigned grid = (unsigned)(a.n_blocks < 65535 ? a.n_blocks : 65535);
+    hipLaunchKernelGGL(k_encode_hash_generic, dim3(grid), dim3(nt), lds, s, a);
+    return hipGetLastError();
+}
+
+template <int K>
+static hipError_t run_rec_fast(const RecArgs& a, hipStream_t s) {
+    const int64_t cols = (a.S + 15) >> 4;
+    const unsigned gx = (unsigned)((cols + 255) / 256);
+    const unsigned gy = (unsigned)(a.n_blocks < 65535 ? a.n_blocks : 65535);
+    if (a.e <= 2)
+        hipLaunchKernelGGL((k_reconstruct<K, 2>), dim3(gx, gy), dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL((k_reconstruct<K, 4>), dim3(gx, gy), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_reconstruct(const RecArgs& a, hipStream_t s, bool* used_fast) {
+    if (a.n_blocks <= 0 || a.S <= 0 || a.e <= 0) return hipSuccess;
+    if (a.e <= 4 && (a.S % 16) == 0) {
+        if (used_fast) *used_fast = true;
+        switch (a.k) {
+            case 2: return run_rec_fast<2>(a, s);
+            case 3: return run_rec_fast<3>(a, s);
+            case 4: return run_rec_fast<4>(a, s);
+            case 5: return run_rec_fast<5>(a, s);
+            case 6: return run_rec_fast<6>(a, s);
+            case 8: return run_rec_fast<8>(a, s);
+            case 10: return run_rec_fast<10>(a, s);
+            case 12: return run_rec_fast<12>(a, s);
+            case 16: return run_rec_fast<16>(a, s);
+            default: break;
+        }
+    }
+    if (used_fast) *used_fast = false;
+    const size_t lds = (size_t)((a.e * a.k + 3) & ~3) + 4 * (size_t)(a.k + a.e);
+    hipError_t e = hipFuncSetAttribute((const void*)k_reconstruct_generic,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    const unsigned gx = (unsigned)((a.S + 255) / 256);
+    const unsigned gy = (unsigned)(a.n_blocks < 65535 ? a.n_blocks : 65535);
+    hipLaunchKernelGGL(k_reconstruct_generic, dim3(gx < 1024 ? gx : 1024, gy), dim3(256), lds, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_hash(const HashArgs& a, hipStream_t s) {
+    if (a.n <= 0) return hipSuccess;
+    const int64_t grid = (a.n + HB_CH - 1) / HB_CH;
+    hipLaunchKernelGGL(k_hash_batch, dim3((unsigned)grid), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_fill(uint8_t* out, int64_t stride, int64_t len, int64_t n, uint64_t seed,
+                       uint64_t obj0, hipStream_t s) {
+    if (n <= 0 || len <= 0) return hipSuccess;
+    const int64_t nw = (len + 7) >> 3;
+    const unsigned gx = (unsigned)((nw + 255) / 256 < 256 ? (nw + 255) / 256 : 256);
+    const unsigned gy = (unsigned)(n < 65535 ? n : 65535);
+    hipLaunchKernelGGL(k_fill, dim3(gx, gy), dim3(256), 0, s, out, stride, len, n, seed, obj0);
+    return hipGetLastError();
+}
+
+}  // namespace zs3k

@@ -1,0 +1,67 @@
+// kernels.hpp — launch interface between the C-ABI layer (zs3gpu.hip) and the
+// HIP kernels (kernels.hip).  Internal; not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace zs3k {
+
+// Batched Split+Encode(+HH256) over n_blocks independent blocks.
+// Block b: data bytes at data + b*data_stride, length n (<= k*S; bytes beyond n are
+// implicit zero padding, as reedsolomon.Split), parity row r at
+// parity + b*parity_stride + r*S, sums (optional) at sums + (b*(k+m) + i)*32.
+struct EncArgs {
+    const uint8_t* data;
+    int64_t data_stride;
+    uint8_t* parity;
+    int64_t parity_stride;
+    uint8_t* sums;            // nullptr: encode only
+    const uint32_t* tables;   // perm tables, 8 dwords per coefficient (r*k + j)
+    const uint8_t* matrix;    // (k+m) x k coding matrix (generic path)
+    int64_t S;                // shard size
+    int64_t n;                // block length
+    int64_t n_blocks;
+    uint64_t key[4];          // HighwayHash key words (little-endian)
+    int k, m;
+};
+
+// Reconstruct: out rows = coef x valid rows, per block.  Block b shard i at
+// shards + b*block_stride + i*S.
+struct RecArgs {
+    uint8_t* shards;
+    int64_t block_stride;
+    int64_t S;
+    int64_t n_blocks;
+    const uint32_t* tables;   // perm tables, 8 dwords per (e*k + t)
+    const uint8_t* coef;      // e x k coefficients (generic path)
+    const int32_t* rows;      // k valid row indices then e output row indices
+    int k, e;
+};
+
+// HighwayHash-256 of n equal-length messages (bitrot verify / reader path).
+struct HashArgs {
+    const uint8_t* msgs;
+    int64_t stride;
+    int64_t len;
+    int64_t n;
+    uint8_t* sums;            // n x 32
+    const uint8_t* expect;    // optional n x 32; mismatch flags -> bad
+    int32_t* bad;             // optional n flags (1 = errFileCorrupt)
+    uint64_t key[4];
+};
+
+// Returns hipSuccess or an error from the launch.
+hipError_t launch_encode(const EncArgs& a, hipStream_t s, bool* used_fast);
+hipError_t launch_reconstruct(const RecArgs& a, hipStream_t s, bool* used_fast);
+hipError_t launch_hash(const HashArgs& a, hipStream_t s);
+hipError_t launch_fill(uint8_t* out, int64_t stride, int64_t len, int64_t n, uint64_t seed,
+                       uint64_t obj0, hipStream_t s);
+
+// Number of (k, m) pairs with a specialised fused kernel, and whether (k, m) has one.
+bool has_fast_encode(int k, int m);
+
+// Tuning knob for experiments: 0 = default variant.
+void set_variant(int v);
+int get_variant();
+
+}  // namespace zs3k

@@ -1,0 +1,645 @@
+// zs3gpu.hip — C-ABI layer (include/zs3gpu.h) over the gfx950 kernels.
+//
+// Host-side counterpart of the reference's Erasure value (cmd/erasure-coding.go)
+// and bitrot hash factory (cmd/bitrot.go): codec construction with NewErasure's
+// checks, size arithmetic, decode-matrix inversion cached per erasure pattern (as
+// klauspost's inversion tree does), per-thread pinned staging for host-pointer
+// calls, and the startup self-tests.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/zs3gpu.h"
+#include "gf256.hpp"
+#include "kernels.hpp"
+
+namespace {
+
+constexpr int kMajor = 0, kMinor = 1, kPatch = 0;
+
+// cmd/bitrot.go:37 — HH-256 of the first 100 decimals of pi under a zero key.
+const uint8_t kMagicKey[32] = {0x4b, 0xe7, 0x34, 0xfa, 0x8e, 0x23, 0x8a, 0xcd, 0x26, 0x3e, 0x83,
+                               0xe6, 0xbb, 0x96, 0x85, 0x52, 0x04, 0x0f, 0x93, 0x5d, 0xa3, 0x9f,
+                               0x44, 0x14, 0x97, 0xe0, 0x9d, 0x13, 0x22, 0xde, 0x36, 0xa0};
+
+thread_local int t_last_path = -1;
+
+void key_words(const uint8_t* key, uint64_t out[4]) {
+    const uint8_t* k = key ? key : kMagicKey;
+    for (int i = 0; i < 4; ++i) {
+        uint64_t v = 0;
+        for (int b = 7; b >= 0; --b) v = (v << 8) | k[8 * i + b];
+        out[i] = v;
+    }
+}
+
+int64_t ceil_frac(int64_t num, int64_t den) {  // cmd/utils.go:691
+    if (den == 0) return 0;
+    if (den < 0) {
+        num = -num;
+        den = -den;
+    }
+    int64_t c = num / den;
+    if (num > 0 && num % den != 0) ++c;
+    return c;
+}
+
+int current_device() {
+    int d = 0;
+    if (hipGetDevice(&d) != hipSuccess) return -1;
+    return d;
+}
+
+struct DevBuf {
+    void* p = nullptr;
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+};
+
+// Cached reconstruct plan for one erasure pattern.
+struct RecPlan {
+    int status = ZS3_OK;          // error for this pattern, or OK
+    bool noop = false;
+    int e = 0;
+    std::vector<int32_t> rows;    // k valid rows, then e output rows
+    std::vector<uint8_t> coef;    // e x k
+    std::vector<uint32_t> tables; // e x k x 8
+    std::map<int, std::shared_ptr<DevBuf>> dev;  // device -> [tables | coef | rows]
+};
+
+}  // namespace
+
+struct zs3_codec {
+    int k, m;
+    int64_t block_size;
+    std::vector<uint8_t> matrix;   // (k+m) x k
+    std::vector<uint32_t> tables;  // m x k x 8 (parity rows)
+    std::mutex mu;
+    std::map<int, std::shared_ptr<DevBuf>> dev;  // device -> [tables | matrix]
+    std::map<std::string, std::shared_ptr<RecPlan>> plans;
+};
+
+namespace {
+
+int map_hip(hipError_t e) { return e == hipSuccess ? ZS3_OK : (e == hipErrorOutOfMemory ? ZS3_ERR_NOMEM : ZS3_ERR_DEVICE); }
+
+// Device copy of the codec's tables + matrix on the current device.
+int codec_device(zs3_codec* c, const uint32_t** tabs, const uint8_t** mat) {
+    const int d = current_device();
+    if (d < 0) return ZS3_ERR_DEVICE;
+    std::lock_guard<std::mutex> g(c->mu);
+    auto it = c->dev.find(d);
+    if (it == c->dev.end()) {
+        auto b = std::make_shared<DevBuf>();
+        const size_t tb = c->tables.size() * 4, mb = c->matrix.size();
+        if (hipMalloc(&b->p, tb + mb) != hipSuccess) return ZS3_ERR_NOMEM;
+        if (hipMemcpy(b->p, c->tables.data(), tb, hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy((uint8_t*)b->p + tb, c->matrix.data(), mb, hipMemcpyHostToDevice) != hipSuccess)
+            return ZS3_ERR_DEVICE;
+        it = c->dev.emplace(d, b).first;
+    }
+    *tabs = (const uint32_t*)it->second->p;
+    *mat = (const uint8_t*)it->second->p + c->tables.size() * 4;
+    return ZS3_OK;
+}
+
+// reedsolomon reconstruct() argument checks + inversion for one pattern.
+std::shared_ptr<RecPlan> make_plan(const zs3_codec* c, const uint8_t* present, int data_only) {
+    auto p = std::make_shared<RecPlan>();
+    const int k = c->k, n = c->k + c->m;
+    int np = 0, dp = 0;
+    for (int i = 0; i < n; ++i)
+        if (present[i]) {
+            ++np;
+            if (i < k) ++dp;
+        }
+    if (np == 0) {
+        p->status = ZS3_ERR_SHARD_NO_DATA;
+        return p;
+    }
+    if (np == n || (data_only && dp == k)) {
+        p->noop = true;
+        return p;
+    }
+    if (np < k) {
+        p->status = ZS3_ERR_TOO_FEW_SHARDS;
+        return p;
+    }
+    std::vector<int32_t> valid;
+    for (int i = 0; i < n && (int)valid.size() < k; ++i)
+        if (present[i]) valid.push_back(i);
+    std::vector<uint8_t> sub((size_t)k * k), dec((size_t)k * k);
+    for (int r = 0; r < k; ++r) std::memcpy(&sub[(size_t)r * k], &c->matrix[(size_t)valid[r] * k], k);
+    if (!zs3::gf_invert(sub.data(), k, dec.data())) {
+        p->status = ZS3_ERR_SINGULAR;
+        return p;
+    }
+    const zs3::GF& g = zs3::gf();
+    p->rows = valid;
+    for (int d = 0; d < k; ++d) {
+        if (present[d]) continue;
+        p->rows.push_back(d);
+        p->coef.insert(p->coef.end(), &dec[(size_t)d * k], &dec[(size_t)d * k] + k);
+    }
+    if (!data_only) {
+        // missing parity row p = M[p] * data = (M[p] * dec) * valid rows
+        for (int r = k; r < n; ++r) {
+            if (present[r]) continue;
+            p->rows.push_back(r);
+            for (int t = 0; t < k; ++t) {
+                uint8_t acc = 0;
+                for (int j = 0; j < k; ++j) acc ^= g.mul(c->matrix[(size_t)r * k + j], dec[(size_t)j * k + t]);
+                p->coef.push_back(acc);
+            }
+        }
+    }
+    p->e = (int)p->rows.size() - k;
+    p->tables.assign((size_t)p->e * k * 8, 0);
+    for (int i = 0; i < p->e * k; ++i) zs3::perm_tables(p->coef[i], &p->tables[(size_t)i * 8]);
+    return p;
+}
+
+std::shared_ptr<RecPlan> get_plan(zs3_codec* c, const uint8_t* present, int data_only) {
+    std::string key((const char*)present, c->k + c->m);
+    for (auto& ch : key) ch = ch ? 1 : 0;
+    key.push_back(data_only ? 1 : 0);
+    std::lock_guard<std::mutex> g(c->mu);
+    auto it = c->plans.find(key);
+    if (it != c->plans.end()) return it->second;
+    auto p = make_plan(c, (const uint8_t*)key.data(), data_only);
+    c->plans.emplace(key, p);
+    return p;
+}
+
+int plan_device(zs3_codec* c, RecPlan* p, const uint32_t** tabs, const uint8_t** coef, const int32_t** rows) {
+    const int d = current_device();
+    if (d < 0) return ZS3_ERR_DEVICE;
+    std::lock_guard<std::mutex> g(c->mu);
+    auto it = p->dev.find(d);
+    const size_t tb = p->tables.size() * 4, cb = (p->coef.size() + 15) & ~(size_t)15, rb = p->rows.size() * 4;
+    if (it == p->dev.end()) {
+        auto b = std::make_shared<DevBuf>();
+        if (hipMalloc(&b->p, tb + cb + rb) != hipSuccess) return ZS3_ERR_NOMEM;
+        uint8_t* base = (uint8_t*)b->p;
+        if (hipMemcpy(base, p->tables.data(), tb, hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(base + tb, p->coef.data(), p->coef.size(), hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(base + tb + cb, p->rows.data(), rb, hipMemcpyHostToDevice) != hipSuccess)
+            return ZS3_ERR_DEVICE;
+        it = p->dev.emplace(d, b).first;
+    }
+    uint8_t* base = (uint8_t*)it->second->p;
+    *tabs = (const uint32_t*)base;
+    *coef = base + tb;
+    *rows = (const int32_t*)(base + tb + cb);
+    return ZS3_OK;
+}
+
+// Per-OS-thread staging for host-pointer calls.
+struct Staging {
+    int dev = -1;
+    hipStream_t stream = nullptr;
+    uint8_t* d = nullptr;
+    size_t dcap = 0;
+    uint8_t* h = nullptr;
+    size_t hcap = 0;
+    ~Staging() {
+        if (d) (void)hipFree(d);
+        if (h) (void)hipHostFree(h);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+thread_local std::map<int, std::unique_ptr<Staging>> t_staging;
+
+Staging* staging(size_t dbytes, size_t hbytes) {
+    const int d = current_device();
+    if (d < 0) return nullptr;
+    auto& sp = t_staging[d];
+    if (!sp) {
+        sp.reset(new Staging());
+        sp->dev = d;
+        if (hipStreamCreateWithFlags(&sp->stream, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    }
+    Staging* s = sp.get();
+    if (s->dcap < dbytes) {
+        if (s->d) (void)hipFree(s->d);
+        s->d = nullptr;
+        s->dcap = 0;
+        if (hipMalloc(&s->d, dbytes) != hipSuccess) return nullptr;
+        s->dcap = dbytes;
+    }
+    if (s->hcap < hbytes) {
+        if (s->h) (void)hipHostFree(s->h);
+        s->h = nullptr;
+        s->hcap = 0;
+        if (hipHostMalloc(&s->h, hbytes, hipHostMallocDefault) != hipSuccess) return nullptr;
+        s->hcap = hbytes;
+    }
+    return s;
+}
+
+size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+// ---- XXH64 (for erasureSelfTest, which hashes with cespare/xxhash/v2) -------
+constexpr uint64_t P1 = 11400714785074694791ULL, P2 = 14029467366897019727ULL,
+                   P3 = 1609587929392839161ULL, P4 = 9650029242287828579ULL,
+                   P5 = 2870177450012600261ULL;
+inline uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+inline uint64_t rd64(const uint8_t* p) {
+    uint64_t v;
+    std::memcpy(&v, p, 8);
+    return v;
+}
+inline uint32_t rd32(const uint8_t* p) {
+    uint32_t v;
+    std::memcpy(&v, p, 4);
+    return v;
+}
+inline uint64_t xround(uint64_t acc, uint64_t in) { return rotl64(acc + in * P2, 31) * P1; }
+inline uint64_t xmerge(uint64_t acc, uint64_t v) { return (acc ^ xround(0, v)) * P1 + P4; }
+
+uint64_t xxh64(const uint8_t* p, size_t len) {
+    const uint8_t* end = p + len;
+    uint64_t h;
+    if (len >= 32) {
+        uint64_t v1 = P1 + P2, v2 = P2, v3 = 0, v4 = 0 - P1;
+        const uint8_t* lim = end - 32;
+        do {
+            v1 = xround(v1, rd64(p));
+            v2 = xround(v2, rd64(p + 8));
+            v3 = xround(v3, rd64(p + 16));
+            v4 = xround(v4, rd64(p + 24));
+            p += 32;
+        } while (p <= lim);
+        h = rotl64(v1, 1) + rotl64(v2, 7) + rotl64(v3, 12) + rotl64(v4, 18);
+        h = xmerge(h, v1);
+        h = xmerge(h, v2);
+        h = xmerge(h, v3);
+        h = xmerge(h, v4);
+    } else {
+        h = P5;
+    }
+    h += (uint64_t)len;
+    while (p + 8 <= end) {
+        h ^= xround(0, rd64(p));
+        h = rotl64(h, 27) * P1 + P4;
+        p += 8;
+    }
+    if (p + 4 <= end) {
+        h ^= (uint64_t)rd32(p) * P1;
+        h = rotl64(h, 23) * P2 + P3;
+        p += 4;
+    }
+    while (p < end) {
+        h ^= (*p) * P5;
+        h = rotl64(h, 11) * P1;
+        ++p;
+    }
+    h ^= h >> 33;
+    h *= P2;
+    h ^= h >> 29;
+    h *= P3;
+    h ^= h >> 32;
+    return h;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* zs3_strerror(int code) {
+    switch (code) {
+        case ZS3_OK: return "ok";
+        case ZS3_ERR_INV_SHARD_NUM: return "cannot create Encoder with less than one data shard or less than zero parity shards";
+        case ZS3_ERR_MAX_SHARD_NUM: return "cannot create Encoder with more than 256 data+parity shards";
+        case ZS3_ERR_TOO_FEW_SHARDS: return "too few shards given";
+        case ZS3_ERR_SHARD_NO_DATA: return "no shard data";
+        case ZS3_ERR_SHARD_SIZE: return "shard sizes do not match";
+        case ZS3_ERR_SHORT_DATA: return "not enough data to fill the number of requested shards";
+        case ZS3_ERR_FILE_CORRUPT: return "file is corrupted";
+        case ZS3_ERR_INVALID_ARG: return "invalid arguments specified";
+        case ZS3_ERR_DEVICE: return "device error";
+        case ZS3_ERR_NOMEM: return "out of memory";
+        case ZS3_ERR_SINGULAR: return "matrix is singular";
+        default: return "unknown error";
+    }
+}
+
+int zs3_version(void) { return (kMajor << 16) | (kMinor << 8) | kPatch; }
+
+int zs3_device_count(int* count) {
+    if (!count) return ZS3_ERR_INVALID_ARG;
+    return map_hip(hipGetDeviceCount(count));
+}
+int zs3_set_device(int device) { return map_hip(hipSetDevice(device)); }
+int zs3_dev_alloc(void** d_ptr, size_t bytes) {
+    if (!d_ptr) return ZS3_ERR_INVALID_ARG;
+    return map_hip(hipMalloc(d_ptr, bytes));
+}
+int zs3_dev_free(void* d_ptr) { return map_hip(hipFree(d_ptr)); }
+int zs3_host_alloc(void** h_ptr, size_t bytes) {
+    if (!h_ptr) return ZS3_ERR_INVALID_ARG;
+    return map_hip(hipHostMalloc(h_ptr, bytes, hipHostMallocDefault));
+}
+int zs3_host_free(void* h_ptr) { return map_hip(hipHostFree(h_ptr)); }
+int zs3_memcpy_h2d(void* d, const void* h, size_t bytes, void* stream) {
+    return map_hip(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, (hipStream_t)stream));
+}
+int zs3_memcpy_d2h(void* h, const void* d, size_t bytes, void* stream) {
+    return map_hip(hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, (hipStream_t)stream));
+}
+int zs3_stream_sync(void* stream) { return map_hip(hipStreamSynchronize((hipStream_t)stream)); }
+
+int zs3_codec_new(int k, int m, int64_t block_size, zs3_codec** out) {
+    if (!out) return ZS3_ERR_INVALID_ARG;
+    *out = nullptr;
+    // NewErasure, cmd/erasure-coding.go:44-50
+    if (k <= 0 || m <= 0) return ZS3_ERR_INV_SHARD_NUM;
+    if (k + m > 256) return ZS3_ERR_MAX_SHARD_NUM;
+    std::unique_ptr<zs3_codec> c(new zs3_codec());
+    c->k = k;
+    c->m = m;
+    c->block_size = block_size;
+    if (!zs3::build_matrix(k, m, c->matrix)) return ZS3_ERR_SINGULAR;
+    c->tables.assign((size_t)m * k * 8, 0);
+    for (int r = 0; r < m; ++r)
+        for (int j = 0; j < k; ++j)
+            zs3::perm_tables(c->matrix[(size_t)(k + r) * k + j], &c->tables[((size_t)r * k + j) * 8]);
+    *out = c.release();
+    return ZS3_OK;
+}
+
+void zs3_codec_free(zs3_codec* c) { delete c; }
+
+int zs3_codec_matrix(const zs3_codec* c, uint8_t* out) {
+    if (!c || !out) return ZS3_ERR_INVALID_ARG;
+    std::memcpy(out, c->matrix.data(), c->matrix.size());
+    return ZS3_OK;
+}
+
+int64_t zs3_shard_size(const zs3_codec* c) { return c ? ceil_frac(c->block_size, c->k) : 0; }
+
+int64_t zs3_shard_file_size(const zs3_codec* c, int64_t total) {
+    if (!c) return 0;
+    if (total == 0) return 0;
+    if (total == -1) return -1;
+    const int64_t num = total / c->block_size;
+    const int64_t last = total % c->block_size;
+    return num * zs3_shard_size(c) + ceil_frac(last, c->k);
+}
+
+int64_t zs3_shard_file_offset(const zs3_codec* c, int64_t start, int64_t length, int64_t total) {
+    if (!c) return 0;
+    const int64_t ss = zs3_shard_size(c);
+    const int64_t sfs = zs3_shard_file_size(c, total);
+    const int64_t end_shard = (start + length) / c->block_size;
+    int64_t till = end_shard * ss + ss;
+    if (till > sfs) till = sfs;
+    return till;
+}
+
+int64_t zs3_bitrot_shard_file_size(int64_t size, int64_t shard_size) {
+    return ceil_frac(size, shard_size) * 32 + size;
+}
+
+int zs3_encode_batch(const zs3_codec* cc, const uint8_t* d_data, int64_t data_stride, int64_t block_len,
+                     int64_t n_blocks, uint8_t* d_parity, int64_t parity_stride, uint8_t* d_sums,
+                     void* stream) {
+    zs3_codec* c = const_cast<zs3_codec*>(cc);
+    if (!c || block_len < 0 || n_blocks < 0) return ZS3_ERR_INVALID_ARG;
+    if (block_len == 0 || n_blocks == 0) return ZS3_OK;  // EncodeData len 0: k+m empty shards
+    if (!d_data || !d_parity) return ZS3_ERR_INVALID_ARG;
+    const int64_t S = ceil_frac(block_len, c->k);
+    zs3k::EncArgs a{};
+    int rc = codec_device(c, &a.tables, &a.matrix);
+    if (rc) return rc;
+    a.data = d_data;
+    a.data_stride = data_stride;
+    a.parity = d_parity;
+    a.parity_stride = parity_stride;
+    a.sums = d_sums;
+    a.S = S;
+    a.n = block_len;
+    a.n_blocks = n_blocks;
+    a.k = c->k;
+    a.m = c->m;
+    key_words(nullptr, a.key);
+    bool fast = false;
+    rc = map_hip(zs3k::launch_encode(a, (hipStream_t)stream, &fast));
+    t_last_path = fast ? 1 : 0;
+    return rc;
+}
+
+int zs3_reconstruct_batch(const zs3_codec* cc, uint8_t* d_shards, int64_t block_stride, int64_t shard_len,
+                          int64_t n_blocks, const uint8_t* present, int data_only, void* stream) {
+    zs3_codec* c = const_cast<zs3_codec*>(cc);
+    if (!c || !present || shard_len < 0 || n_blocks < 0) return ZS3_ERR_INVALID_ARG;
+    auto plan = get_plan(c, present, data_only);
+    if (plan->status) return plan->status;
+    if (shard_len == 0) return ZS3_ERR_SHARD_NO_DATA;
+    if (plan->noop || n_blocks == 0) return ZS3_OK;
+    zs3k::RecArgs a{};
+    int rc = plan_device(c, plan.get(), &a.tables, &a.coef, &a.rows);
+    if (rc) return rc;
+    a.shards = d_shards;
+    a.block_stride = block_stride;
+    a.S = shard_len;
+    a.n_blocks = n_blocks;
+    a.k = c->k;
+    a.e = plan->e;
+    bool fast = false;
+    rc = map_hip(zs3k::launch_reconstruct(a, (hipStream_t)stream, &fast));
+    t_last_path = fast ? 1 : 0;
+    return rc;
+}
+
+int zs3_hh256_batch(const uint8_t* key, const uint8_t* d_msgs, int64_t stride, int64_t len, int64_t n,
+                    uint8_t* d_sums, void* stream) {
+    if (len < 0 || n < 0 || (n > 0 && !d_sums)) return ZS3_ERR_INVALID_ARG;
+    zs3k::HashArgs a{};
+    a.msgs = d_msgs;
+    a.stride = stride;
+    a.len = len;
+    a.n = n;
+    a.sums = d_sums;
+    key_words(key, a.key);
+    return map_hip(zs3k::launch_hash(a, (hipStream_t)stream));
+}
+
+int zs3_hh256_verify_batch(const uint8_t* key, const uint8_t* d_msgs, int64_t stride, int64_t len, int64_t n,
+                           const uint8_t* d_want, int32_t* d_bad, void* stream) {
+    if (len < 0 || n < 0 || (n > 0 && (!d_want || !d_bad))) return ZS3_ERR_INVALID_ARG;
+    zs3k::HashArgs a{};
+    a.msgs = d_msgs;
+    a.stride = stride;
+    a.len = len;
+    a.n = n;
+    a.expect = d_want;
+    a.bad = d_bad;
+    key_words(key, a.key);
+    return map_hip(zs3k::launch_hash(a, (hipStream_t)stream));
+}
+
+int zs3_fill_batch(uint8_t* d_out, int64_t stride, int64_t len, int64_t n, uint64_t seed, uint64_t obj0,
+                   void* stream) {
+    if (len < 0 || n < 0) return ZS3_ERR_INVALID_ARG;
+    return map_hip(zs3k::launch_fill(d_out, stride, len, n, seed, obj0, (hipStream_t)stream));
+}
+
+int64_t zs3_encode_data(const zs3_codec* c, uint8_t* buf, int64_t len, int64_t cap, uint8_t* h_sums) {
+    if (!c || len < 0) return ZS3_ERR_INVALID_ARG;
+    if (len == 0) return 0;
+    if (!buf) return ZS3_ERR_INVALID_ARG;
+    const int k = c->k, m = c->m, R = k + m;
+    const int64_t S = ceil_frac(len, k);
+    if (cap < (int64_t)R * S) return ZS3_ERR_INVALID_ARG;
+    std::memset(buf + len, 0, (size_t)(k * S - len));  // reedsolomon.Split zero-fill
+    const size_t dbytes = align16((size_t)R * S) + (size_t)R * 32;
+    Staging* st = staging(dbytes, dbytes);
+    if (!st) return ZS3_ERR_NOMEM;
+    std::memcpy(st->h, buf, (size_t)(k * S));
+    uint8_t* d_sums = st->d + align16((size_t)R * S);
+    int rc = map_hip(hipMemcpyAsync(st->d, st->h, (size_t)(k * S), hipMemcpyHostToDevice, st->stream));
+    if (rc) return rc;
+    rc = zs3_encode_batch(c, st->d, (int64_t)R * S, len, 1, st->d + (size_t)k * S, (int64_t)R * S,
+                          h_sums ? d_sums : nullptr, st->stream);
+    if (rc) return rc;
+    rc = map_hip(hipMemcpyAsync(st->h + (size_t)k * S, st->d + (size_t)k * S, (size_t)(m * S),
+                                hipMemcpyDeviceToHost, st->stream));
+    if (rc) return rc;
+    if (h_sums) {
+        rc = map_hip(hipMemcpyAsync(st->h + align16((size_t)R * S), d_sums, (size_t)R * 32,
+                                    hipMemcpyDeviceToHost, st->stream));
+        if (rc) return rc;
+    }
+    rc = map_hip(hipStreamSynchronize(st->stream));
+    if (rc) return rc;
+    std::memcpy(buf + (size_t)k * S, st->h + (size_t)k * S, (size_t)(m * S));
+    if (h_sums) std::memcpy(h_sums, st->h + align16((size_t)R * S), (size_t)R * 32);
+    return S;
+}
+
+int zs3_decode_data_blocks(const zs3_codec* cc, uint8_t* shards, int64_t S, const uint8_t* present, int data_only) {
+    zs3_codec* c = const_cast<zs3_codec*>(cc);
+    if (!c || !present || S < 0) return ZS3_ERR_INVALID_ARG;
+    auto plan = get_plan(c, present, data_only);
+    if (plan->status) return plan->status;
+    if (S == 0) return ZS3_ERR_SHARD_NO_DATA;
+    if (plan->noop) return ZS3_OK;
+    const int R = c->k + c->m;
+    const size_t bytes = (size_t)R * S;
+    Staging* st = staging(bytes, bytes);
+    if (!st) return ZS3_ERR_NOMEM;
+    std::memcpy(st->h, shards, bytes);
+    int rc = map_hip(hipMemcpyAsync(st->d, st->h, bytes, hipMemcpyHostToDevice, st->stream));
+    if (rc) return rc;
+    rc = zs3_reconstruct_batch(c, st->d, (int64_t)bytes, S, 1, present, data_only, st->stream);
+    if (rc) return rc;
+    rc = map_hip(hipMemcpyAsync(st->h, st->d, bytes, hipMemcpyDeviceToHost, st->stream));
+    if (rc) return rc;
+    rc = map_hip(hipStreamSynchronize(st->stream));
+    if (rc) return rc;
+    for (size_t i = plan->rows.size() - plan->e; i < plan->rows.size(); ++i) {
+        const int r = plan->rows[i];
+        std::memcpy(shards + (size_t)r * S, st->h + (size_t)r * S, (size_t)S);
+    }
+    return ZS3_OK;
+}
+
+int zs3_hh256(const uint8_t* key, const uint8_t* msg, int64_t len, uint8_t* out32) {
+    if (len < 0 || !out32 || (len > 0 && !msg)) return ZS3_ERR_INVALID_ARG;
+    const size_t mb = align16((size_t)len > 0 ? (size_t)len : 1);
+    Staging* st = staging(mb + 32, mb + 32);
+    if (!st) return ZS3_ERR_NOMEM;
+    if (len) std::memcpy(st->h, msg, (size_t)len);
+    int rc = map_hip(hipMemcpyAsync(st->d, st->h, mb, hipMemcpyHostToDevice, st->stream));
+    if (rc) return rc;
+    rc = zs3_hh256_batch(key, st->d, (int64_t)mb, len, 1, st->d + mb, st->stream);
+    if (rc) return rc;
+    rc = map_hip(hipMemcpyAsync(st->h + mb, st->d + mb, 32, hipMemcpyDeviceToHost, st->stream));
+    if (rc) return rc;
+    rc = map_hip(hipStreamSynchronize(st->stream));
+    if (rc) return rc;
+    std::memcpy(out32, st->h + mb, 32);
+    return ZS3_OK;
+}
+
+int zs3_selftest(void) {
+    // erasureSelfTest, cmd/erasure-coding.go:158-216 (want table from :169)
+    static const struct {
+        uint8_t k, m;
+        uint64_t want;
+    } kat[] = {
+        {2, 2, 0x23fb21be2496f5d3ULL}, {2, 3, 0xa5cd5600ba0d8e7cULL}, {3, 1, 0x60ab052148b010b4ULL},
+        {3, 2, 0xe64927daef76435aULL}, {3, 3, 0x672f6f242b227b21ULL}, {3, 4, 0x571e41ba23a6dc6ULL},
+        {4, 1, 0x524eaa814d5d86e2ULL}, {4, 2, 0x62b9552945504fefULL}, {4, 3, 0xcbf9065ee053e518ULL},
+        {4, 4, 0x9a07581dcd03da8ULL},  {4, 5, 0xbf2d27b55370113fULL}, {5, 1, 0xf71031a01d70dafULL},
+        {5, 2, 0x8e5845859939d0f4ULL}, {5, 3, 0x7ad9161acbb4c325ULL}, {5, 4, 0xc446b88830b4f800ULL},
+        {5, 5, 0xabf1573cc6f76165ULL}, {5, 6, 0x7b5598a85045bfb8ULL}, {6, 1, 0xe2fc1e677cc7d872ULL},
+        {6, 2, 0x7ed133de5ca6a58eULL}, {6, 3, 0x39ef92d0a74cc3c0ULL}, {6, 4, 0xcfc90052bc25d20ULL},
+        {6, 5, 0x71c96f6baeef9c58ULL}, {6, 6, 0x4b79056484883e4cULL}, {6, 7, 0xb1a0e2427ac2dc1aULL},
+        {7, 1, 0x937ba2b7af467a22ULL}, {7, 2, 0x5fd13a734d27d37aULL}, {7, 3, 0x3be2722d9b66912fULL},
+        {7, 4, 0x14c628e59011be3dULL}, {7, 5, 0xcc3b39ad4c083b9fULL}, {7, 6, 0x45af361b7de7a4ffULL},
+        {7, 7, 0x456cc320cec8a6e6ULL}, {7, 8, 0x1867a9f4db315b5cULL}, {8, 1, 0xbc5756b9a9ade030ULL},
+        {8, 2, 0xdfd7d9d0b3e36503ULL}, {8, 3, 0x72bb72c2cdbcf99dULL}, {8, 4, 0x3ba5e9b41bf07f0ULL},
+        {8, 5, 0xd7dabc15800f9d41ULL}, {8, 6, 0xb482a6169fd270fULL},  {8, 7, 0x50748e0099d657e8ULL},
+        {9, 1, 0xc77ae0144fcaeb6eULL}, {9, 2, 0x8a86c7dbebf27b68ULL}, {9, 3, 0xa64e3be6d6fe7e92ULL},
+        {9, 4, 0x239b71c41745d207ULL}, {9, 5, 0x2d0803094c5a86ceULL}, {9, 6, 0xa3c2539b3af84874ULL},
+        {10, 1, 0x7d30d91b89fcec21ULL}, {10, 2, 0xfa5af9aa9f1857a3ULL}, {10, 3, 0x84bc4bda8af81f90ULL},
+        {10, 4, 0x6c1cba8631de994aULL}, {10, 5, 0x4383e58a086cc1acULL}, {11, 1, 0x4ed2929a2df690bULL},
+        {11, 2, 0xecd6f1b1399775c0ULL}, {11, 3, 0xc78cfbfc0dc64d01ULL}, {11, 4, 0xb2643390973702d6ULL},
+        {12, 1, 0x3b2a88686122d082ULL}, {12, 2, 0xfd2f30a48a8e2e9ULL}, {12, 3, 0xd5ce58368ae90b13ULL},
+        {13, 1, 0x9c88e2a9d1b8fff8ULL}, {13, 2, 0xcb8460aa4cf6613ULL}, {14, 1, 0x78a28bbaec57996eULL},
+    };
+    int ok = 1;
+    for (const auto& t : kat) {
+        zs3_codec* c = nullptr;
+        if (zs3_codec_new(t.k, t.m, 1 << 20, &c)) return ZS3_ERR_FILE_CORRUPT;
+        const int R = t.k + t.m;
+        std::vector<uint8_t> buf(512 * 2, 0);
+        for (int i = 0; i < 256; ++i) buf[i] = (uint8_t)i;
+        const int64_t S = zs3_encode_data(c, buf.data(), 256, (int64_t)buf.size(), nullptr);
+        if (S <= 0) {
+            zs3_codec_free(c);
+            return S < 0 ? (int)S : ZS3_ERR_FILE_CORRUPT;
+        }
+        std::vector<uint8_t> stream;
+        for (int i = 0; i < R; ++i) {
+            stream.push_back((uint8_t)i);
+            stream.insert(stream.end(), buf.begin() + (size_t)i * S, buf.begin() + (size_t)(i + 1) * S);
+        }
+        if (xxh64(stream.data(), stream.size()) != t.want) ok = 0;
+        // delete first shard, DecodeDataBlocks (:201-209)
+        std::vector<uint8_t> first(buf.begin(), buf.begin() + S);
+        std::vector<uint8_t> pres(R, 1);
+        pres[0] = 0;
+        std::memset(buf.data(), 0, (size_t)S);
+        if (zs3_decode_data_blocks(c, buf.data(), S, pres.data(), 1) != ZS3_OK) ok = 0;
+        if (std::memcmp(first.data(), buf.data(), (size_t)S) != 0) ok = 0;
+        zs3_codec_free(c);
+    }
+    // bitrotSelfTest, cmd/bitrot.go:218-249 (HighwayHash256S)
+    static const uint8_t want_hh[32] = {0x39, 0xc0, 0x40, 0x7e, 0xd3, 0xf0, 0x1b, 0x18, 0xd2, 0x2c, 0x85,
+                                        0xdb, 0x4a, 0xef, 0xf1, 0x1e, 0x06, 0x0c, 0xa5, 0xf4, 0x31, 0x31,
+                                        0xb0, 0x12, 0x67, 0x31, 0xca, 0x19, 0x7c, 0xd4, 0x23, 0x13};
+    std::vector<uint8_t> msg;
+    uint8_t sum[32] = {0};
+    for (int i = 0; i < 32 * 32; i += 32) {
+        if (zs3_hh256(nullptr, msg.data(), (int64_t)msg.size(), sum) != ZS3_OK) return ZS3_ERR_DEVICE;
+        msg.insert(msg.end(), sum, sum + 32);
+    }
+    if (std::memcmp(sum, want_hh, 32) != 0) ok = 0;
+    return ok ? ZS3_OK : ZS3_ERR_FILE_CORRUPT;
+}
+
+int zs3_last_path(void) { return t_last_path; }
+
+}  // extern "C"

@@ -40,6 +40,13 @@ class Erasure:
         n = len(arr) if length is None else length
         if n == 0:
             return [np.zeros(0, dtype=np.uint8) for _ in range(k + m)]
+        S = -(-n // k)
+        if len(arr) < (k + m) * S:
+            # reedsolomon.Split allocates the padding shards when cap(data) is short;
+            # the shard values are identical, only their backing differs.
+            big = np.zeros((k + m) * S, dtype=np.uint8)
+            big[:n] = arr[:n]
+            arr = big
         S, _ = self._codec.encode_data(arr, n)
         return [arr[i * S:(i + 1) * S] for i in range(k + m)]
 

@@ -157,6 +157,10 @@ int zs3_selftest(void);
  * (k, m) kernel, 0 = generic byte kernel. */
 int zs3_last_path(void);
 
+/* Diagnostics: select an experimental tile/column variant of the fused encode
+ * kernel for the headline shapes (0 = tuned default).  Not for production use. */
+int zs3_debug_set_variant(int variant);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,50 @@
+"""Time every experimental variant of the fused encode+hash kernel on the
+headline shapes and cross-check outputs against the default variant."""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import zs3server_amd as z  # noqa: E402
+
+SHAPES = [(8, 4, 4096), (4, 2, 1024), (16, 4, 2048)]
+VARIANTS = [0, 1, 2, 3, 4, 5, 6, 7, 8]
+steps = int(os.environ.get("SWEEP_STEPS", "10"))
+res = []
+for k, m, nobj in SHAPES:
+    blen = 1 << 20
+    S = blen // k
+    stride = (k + m) * S
+    codec = z.Codec(k, m)
+    buf = torch.empty(nobj * stride, dtype=torch.uint8, device="cuda")
+    sums = torch.empty(nobj * (k + m) * 32, dtype=torch.uint8, device="cuda")
+    z.fill_batch(buf, stride, blen, nobj, seed=5)
+    ref = None
+    for v in VARIANTS:
+        z.set_variant(v)
+        buf.view(nobj, k + m, S)[:, k:, :] = 0
+        sums.zero_()
+        codec.encode_batch(buf, stride, blen, nobj, parity=buf, parity_offset=k * S, parity_stride=stride, sums=sums)
+        torch.cuda.synchronize()
+        sig = (int(buf.view(torch.int64).sum()), int(sums.view(torch.int64).sum()))
+        if ref is None:
+            ref = sig
+        ok = sig == ref
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(steps):
+            codec.encode_batch(buf, stride, blen, nobj, parity=buf, parity_offset=k * S, parity_stride=stride, sums=sums)
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / steps
+        ab = nobj * (blen + m * S + 32 * (k + m))
+        r = {"k": k, "m": m, "objects": nobj, "variant": v, "ms": round(ms, 4),
+             "GiBps": round(nobj * blen / ms / 1e-3 / 2**30, 1), "hbm_GBps": round(ab / ms / 1e6, 1), "match": ok}
+        print(json.dumps(r), flush=True)
+        res.append(r)
+    del buf, sums
+    torch.cuda.empty_cache()
+z.set_variant(0)

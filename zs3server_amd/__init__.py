@@ -40,7 +40,7 @@ EXPORTS = [
     "zs3_shard_file_size", "zs3_shard_file_offset", "zs3_bitrot_shard_file_size",
     "zs3_encode_batch", "zs3_reconstruct_batch", "zs3_hh256_batch", "zs3_hh256_verify_batch",
     "zs3_fill_batch", "zs3_encode_data", "zs3_decode_data_blocks", "zs3_hh256", "zs3_selftest",
-    "zs3_last_path",
+    "zs3_last_path", "zs3_debug_set_variant",
 ]
 
 
@@ -231,6 +231,11 @@ def selftest() -> None:
 
 def last_path() -> int:
     return lib().zs3_last_path()
+
+
+def set_variant(v: int) -> None:
+    """Diagnostics: experimental fused-kernel variant (0 = tuned default)."""
+    lib().zs3_debug_set_variant(v)
 
 
 def device_count() -> int:

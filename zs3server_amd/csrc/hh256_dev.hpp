@@ -44,14 +44,31 @@ __device__ __forceinline__ uint32_t zipper_sel(int lane) {
     return (lane & 1) ? 0x07000601u : 0x00070106u;
 }
 
+// 64-bit add as ONE v_lshl_add_u64.  Written in asm because hipcc otherwise
+// splits `x + ((hi << 32) | lo)` into two adds plus two v_mov (disjoint-or -> add).
+__device__ __forceinline__ uint64_t add64(uint64_t a, uint64_t b) {
+    uint64_t r;
+    asm("v_lshl_add_u64 %0, %1, 0, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
+__device__ __forceinline__ uint64_t zipper_add(uint64_t acc, uint64_t own, uint32_t partner_hi,
+                                               uint32_t sel_hi) {
+    const uint32_t olo = (uint32_t)own, ohi = (uint32_t)(own >> 32);
+    const uint32_t t = __builtin_amdgcn_perm(partner_hi, olo, 0x0c020403u);
+    const uint32_t lo = __builtin_amdgcn_perm(t, ohi, 0x01060504u);
+    const uint32_t hi = __builtin_amdgcn_perm(partner_hi, olo, sel_hi);
+    return add64(acc, ((uint64_t)hi << 32) | lo);
+}
+
 // One HighwayHash Update() step for this thread's lane (C reference Update).
 __device__ __forceinline__ void hh_update(HHLane& s, uint64_t w, uint32_t sel_hi) {
-    s.v1 += s.mul0 + w;
+    s.v1 = add64(s.v1, add64(s.mul0, w));
     s.mul0 ^= (uint64_t)(uint32_t)s.v1 * (s.v0 >> 32);
-    s.v0 += s.mul1;
+    s.v0 = add64(s.v0, s.mul1);
     s.mul1 ^= (uint64_t)(uint32_t)s.v0 * (s.v1 >> 32);
-    s.v0 += zipper(s.v1, dpp_xor1((uint32_t)(s.v1 >> 32)), sel_hi);
-    s.v1 += zipper(s.v0, dpp_xor1((uint32_t)(s.v0 >> 32)), sel_hi);
+    s.v0 = zipper_add(s.v0, s.v1, dpp_xor1((uint32_t)(s.v1 >> 32)), sel_hi);
+    s.v1 = zipper_add(s.v1, s.v0, dpp_xor1((uint32_t)(s.v0 >> 32)), sel_hi);
 }
 
 // Initial state for lane `lane` under key words key[0..3] (C reference Reset).
@@ -77,8 +94,16 @@ __device__ __forceinline__ HHLane hh_init(int lane, uint64_t k0, uint64_t k1, ui
 __device__ __forceinline__ void hh_packets(HHLane& s, const uint8_t* row, int npk, int lane,
                                            uint32_t sel_hi) {
     const uint64_t* p = reinterpret_cast<const uint64_t*>(row) + lane;
-#pragma unroll 4
-    for (int i = 0; i < npk; ++i) hh_update(s, p[4 * i], sel_hi);
+    if (npk <= 0) return;
+    // Software-pipelined: the next packet's ds_read_b64 is in flight while the
+    // current packet runs the serial HighwayHash chain.
+    uint64_t w = p[0];
+    for (int i = 1; i < npk; ++i) {
+        const uint64_t nxt = p[4 * i];
+        hh_update(s, w, sel_hi);
+        w = nxt;
+    }
+    hh_update(s, w, sel_hi);
 }
 
 __device__ __forceinline__ uint32_t rotl32(uint32_t x, uint32_t n) {

@@ -21,6 +21,8 @@
 #include "gf_dev.hpp"
 #include "hh256_dev.hpp"
 
+#include <stdlib.h>
+
 using namespace zs3dev;
 
 namespace zs3k {
@@ -75,11 +77,29 @@ constexpr int pick_T() {
 
 // ---------------------------------------------------------------------------
 // Fused Split + Encode + HighwayHash-256 over G stripes per workgroup.
-template <int K, int M, int G, int T, int NBUF, int NT>
+// CW = bytes per encode column per thread (16 -> dwordx4 loads, 8 -> dwordx2, 4 -> dword).
+template <int NWd>
+struct Col {
+    uint32_t w[NWd];
+};
+
+template <int NWd>
+__device__ __forceinline__ Col<NWd> ldcol(const uint8_t* p) {
+    Col<NWd> v;
+    __builtin_memcpy(&v, p, 4 * NWd);
+    return v;
+}
+template <int NWd>
+__device__ __forceinline__ void stcol(uint8_t* p, const Col<NWd>& v) {
+    __builtin_memcpy(p, &v, 4 * NWd);
+}
+
+template <int K, int M, int G, int T, int NBUF, int NT, int CW>
 __global__ void __launch_bounds__(NT) k_encode_hash(EncArgs a) {
     constexpr int R = K + M;
+    constexpr int NWd = CW / 4;
     constexpr int TS = T + 32;  // LDS row stride: +8 banks per row, conflict-free b64 reads
-    constexpr int CPB = T / 16;  // 16-byte columns per stripe per tile
+    constexpr int CPB = T / CW;  // columns per stripe per tile
     constexpr int NCOL = G * CPB;
     constexpr int CPT = (NCOL + NT - 1) / NT;
 
@@ -88,7 +108,7 @@ __global__ void __launch_bounds__(NT) k_encode_hash(EncArgs a) {
 
     const int tid = threadIdx.x;
     const int64_t blk0 = (int64_t)blockIdx.x * G;
-    const int64_t S = a.S, n = a.n;
+    const int64_t S = a.S;
 
     for (int i = tid; i < M * K * 8; i += NT) tabs[i] = a.tables[i];
 
@@ -99,24 +119,23 @@ __global__ void __launch_bounds__(NT) k_encode_hash(EncArgs a) {
     const uint32_t sel = zipper_sel(lane);
     HHLane st = hh_init(lane, a.key[0], a.key[1], a.key[2], a.key[3]);
 
-    // ---- encode role: CPT columns per thread
-    uint4 x[CPT][K] = {};
+    // ---- encode role: CPT columns per thread.  Dead stripes of the last workgroup
+    // alias the last live block and store byte-identical parity (benign), so the
+    // encode has no data-dependent branches (those make hipcc split the parity rows
+    // and keep every shard's nibbles live).
+    Col<NWd> x[CPT][K] = {};
     auto prefetch = [&](int64_t t0) {
 #pragma unroll
         for (int c = 0; c < CPT; ++c) {
             const int col = tid + c * NT;
             const int g = col / CPB;
-            const int o = (col % CPB) * 16;
-            // Dead stripes of the last workgroup alias the last live block: they
-            // recompute and store byte-identical parity (benign), so the encode has
-            // no data-dependent branches (which make hipcc split the parity rows and
-            // keep every shard's nibbles live).
+            const int o = (col % CPB) * CW;
             const int64_t b = (blk0 + g) < a.n_blocks ? (blk0 + g) : (a.n_blocks - 1);
             const bool live = col < NCOL && t0 + o < S;
             const uint8_t* blk = a.data + b * a.data_stride;
 #pragma unroll
             for (int j = 0; j < K; ++j)
-                if (live) x[c][j] = ld16(blk + (int64_t)j * S + t0 + o);
+                if (live) x[c][j] = ldcol<NWd>(blk + (int64_t)j * S + t0 + o);
         }
     };
 
@@ -126,37 +145,37 @@ __global__ void __launch_bounds__(NT) k_encode_hash(EncArgs a) {
             const int col = tid + c * NT;
             if (col >= NCOL) continue;
             const int g = col / CPB;
-            const int o = (col % CPB) * 16;
+            const int o = (col % CPB) * CW;
             const int64_t b = (blk0 + g) < a.n_blocks ? (blk0 + g) : (a.n_blocks - 1);
             if (o >= L) continue;
             const uint32_t* tb = tabs + opaque_zero();
-            GfAcc acc[M][4];
+            GfAcc acc[M][NWd];
 #pragma unroll
             for (int r = 0; r < M; ++r)
 #pragma unroll
-                for (int w = 0; w < 4; ++w) acc_init(acc[r][w]);
+                for (int w = 0; w < NWd; ++w) acc_init(acc[r][w]);
 #pragma unroll
             for (int j = 0; j < K; ++j) {
                 __builtin_amdgcn_sched_barrier(0);  // keep each shard's table reads local
-                const Nib n0 = split_nibbles(x[c][j].x), n1 = split_nibbles(x[c][j].y);
-                const Nib n2 = split_nibbles(x[c][j].z), n3 = split_nibbles(x[c][j].w);
+                Nib nb[NWd];
+#pragma unroll
+                for (int w = 0; w < NWd; ++w) nb[w] = split_nibbles(x[c][j].w[w]);
 #pragma unroll
                 for (int r = 0; r < M; ++r) {
                     const CoefTab t = load_coef(tb, r * K + j);
-                    acc_add(acc[r][0], gf_lookup(n0, t));
-                    acc_add(acc[r][1], gf_lookup(n1, t));
-                    acc_add(acc[r][2], gf_lookup(n2, t));
-                    acc_add(acc[r][3], gf_lookup(n3, t));
+#pragma unroll
+                    for (int w = 0; w < NWd; ++w) acc_add(acc[r][w], gf_lookup(nb[w], t));
                 }
-                *reinterpret_cast<uint4*>(tl + (g * R + j) * TS + o) = x[c][j];
+                stcol<NWd>(tl + (g * R + j) * TS + o, x[c][j]);
             }
             uint8_t* pbase = a.parity + b * a.parity_stride + t0 + o;
 #pragma unroll
             for (int r = 0; r < M; ++r) {
-                const uint4 p = make_uint4(acc_done(acc[r][0]), acc_done(acc[r][1]),
-                                           acc_done(acc[r][2]), acc_done(acc[r][3]));
-                *reinterpret_cast<uint4*>(tl + (g * R + K + r) * TS + o) = p;
-                st16(pbase + (int64_t)r * S, p);
+                Col<NWd> p;
+#pragma unroll
+                for (int w = 0; w < NWd; ++w) p.w[w] = acc_done(acc[r][w]);
+                stcol<NWd>(tl + (g * R + K + r) * TS + o, p);
+                stcol<NWd>(pbase + (int64_t)r * S, p);
             }
         }
     };
@@ -467,6 +486,42 @@ __global__ void __launch_bounds__(256) k_fill(uint8_t* out, int64_t stride, int6
 
 // ---------------------------------------------------------------------------
 // Dispatch
+template <int K, int M, int G, int T, int NBUF, int CW>
+static void launch_fused(const EncArgs& a, hipStream_t s) {
+    constexpr int R = K + M;
+    constexpr int NT = round64(4 * G * R);
+    static_assert(T % CW == 0 && T % 32 == 0, "tile");
+    const int64_t grid = (a.n_blocks + G - 1) / G;
+    hipLaunchKernelGGL((k_encode_hash<K, M, G, T, NBUF, NT, CW>), dim3((unsigned)grid), dim3(NT), 0, s, a);
+}
+
+static int env_variant() {
+    static int v = -2;
+    if (v == -2) {
+        const char* e = getenv("ZS3_VARIANT");
+        v = e ? atoi(e) : -1;
+    }
+    return g_variant > 0 ? g_variant : v;
+}
+
+// Experimental variants for the headline shapes (ZS3_VARIANT=n); -1/0 = default.
+template <int K, int M>
+static bool launch_variant(int v, const EncArgs& a, hipStream_t s) {
+    constexpr int R = K + M;
+    constexpr int G = pick_G<R>();
+    switch (v) {
+        case 1: launch_fused<K, M, G, 256, 2, 16>(a, s); return true;
+        case 2: launch_fused<K, M, G, 768, 1, 16>(a, s); return true;
+        case 3: launch_fused<K, M, G, 384, 2, 8>(a, s); return true;
+        case 4: launch_fused<K, M, G, 192, 2, 4>(a, s); return true;
+        case 5: launch_fused<K, M, G, 384, 1, 8>(a, s); return true;
+        case 6: launch_fused<K, M, G, 768, 2, 16>(a, s); return true;
+        case 7: launch_fused<K, M, G, 512, 2, 16>(a, s); return true;
+        case 8: launch_fused<K, M, G, 192, 1, 4>(a, s); return true;
+        default: return false;
+    }
+}
+
 template <int K, int M>
 static hipError_t run_encode_fast(const EncArgs& a, hipStream_t s) {
     if (a.sums) {
@@ -474,9 +529,12 @@ static hipError_t run_encode_fast(const EncArgs& a, hipStream_t s) {
         constexpr int G = pick_G<R>();
         constexpr int NBUF = 2;
         constexpr int T = pick_T<G * R, NBUF>();
-        constexpr int NT = round64(4 * G * R);
-        const int64_t grid = (a.n_blocks + G - 1) / G;
-        hipLaunchKernelGGL((k_encode_hash<K, M, G, T, NBUF, NT>), dim3((unsigned)grid), dim3(NT), 0, s, a);
+        bool done = false;
+        if constexpr ((K == 8 && M == 4) || (K == 4 && M == 2) || (K == 16 && M == 4)) {
+            const int v = env_variant();
+            if (v > 0) done = launch_variant<K, M>(v, a, s);
+        }
+        if (!done) launch_fused<K, M, G, T, NBUF, 16>(a, s);
     } else {
         const int64_t cols = (a.S + 15) >> 4;
         const unsigned gx = (unsigned)((cols + 255) / 256);

@@ -642,4 +642,9 @@ int zs3_selftest(void) {
 
 int zs3_last_path(void) { return t_last_path; }
 
+int zs3_debug_set_variant(int variant) {
+    zs3k::set_variant(variant);
+    return ZS3_OK;
+}
+
 }  // extern "C"

@@ -10,8 +10,9 @@ import torch  # noqa: E402
 
 import zs3server_amd as z  # noqa: E402
 
-SHAPES = [(8, 4, 4096), (4, 2, 1024), (16, 4, 2048)]
-VARIANTS = [0, 1, 2, 3, 4, 5, 6, 7, 8]
+SHAPES = [tuple(int(x) for x in t.split(":")) for t in os.environ.get("SWEEP_SHAPES", "8:4:4096,4:2:1024,16:4:2048").split(",")]
+REPEAT = int(os.environ.get("SWEEP_REPEAT", "2"))
+VARIANTS = [int(v) for v in os.environ.get("SWEEP_VARIANTS", "0,1,2,3,4,5,6,7,8").split(",")]
 steps = int(os.environ.get("SWEEP_STEPS", "10"))
 res = []
 for k, m, nobj in SHAPES:
@@ -23,7 +24,7 @@ for k, m, nobj in SHAPES:
     sums = torch.empty(nobj * (k + m) * 32, dtype=torch.uint8, device="cuda")
     z.fill_batch(buf, stride, blen, nobj, seed=5)
     ref = None
-    for v in VARIANTS:
+    for v in VARIANTS * REPEAT:
         z.set_variant(v)
         buf.view(nobj, k + m, S)[:, k:, :] = 0
         sums.zero_()

@@ -89,12 +89,44 @@ __device__ __forceinline__ Col<NWd> ldcol(const uint8_t* p) {
     __builtin_memcpy(&v, p, 4 * NWd);
     return v;
 }
+// Non-temporal variants: data blocks are read exactly once and parity is not
+// re-read by this kernel, so keep both out of the caches' replacement state.
+template <int NWd>
+__device__ __forceinline__ Col<NWd> ldcol_nt(const uint8_t* p) {
+    Col<NWd> v;
+    if constexpr (NWd == 4) {
+        typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+        const u4 t = __builtin_nontemporal_load(reinterpret_cast<const u4*>(p));
+        v.w[0] = t.x; v.w[1] = t.y; v.w[2] = t.z; v.w[3] = t.w;
+    } else if constexpr (NWd == 2) {
+        typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+        const u2 t = __builtin_nontemporal_load(reinterpret_cast<const u2*>(p));
+        v.w[0] = t.x; v.w[1] = t.y;
+    } else {
+        v.w[0] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(p));
+    }
+    return v;
+}
+template <int NWd>
+__device__ __forceinline__ void stcol_nt(uint8_t* p, const Col<NWd>& v) {
+    if constexpr (NWd == 4) {
+        typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+        u4 t = {v.w[0], v.w[1], v.w[2], v.w[3]};
+        __builtin_nontemporal_store(t, reinterpret_cast<u4*>(p));
+    } else if constexpr (NWd == 2) {
+        typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+        u2 t = {v.w[0], v.w[1]};
+        __builtin_nontemporal_store(t, reinterpret_cast<u2*>(p));
+    } else {
+        __builtin_nontemporal_store(v.w[0], reinterpret_cast<uint32_t*>(p));
+    }
+}
 template <int NWd>
 __device__ __forceinline__ void stcol(uint8_t* p, const Col<NWd>& v) {
     __builtin_memcpy(p, &v, 4 * NWd);
 }
 
-template <int K, int M, int G, int T, int NBUF, int NT, int CW>
+template <int K, int M, int G, int T, int NBUF, int NT, int CW, int PF, bool NTL>
 __global__ void __launch_bounds__(NT) k_encode_hash(EncArgs a) {
     constexpr int R = K + M;
     constexpr int NWd = CW / 4;
@@ -123,8 +155,8 @@ __global__ void __launch_bounds__(NT) k_encode_hash(EncArgs a) {
     // alias the last live block and store byte-identical parity (benign), so the
     // encode has no data-dependent branches (those make hipcc split the parity rows
     // and keep every shard's nibbles live).
-    Col<NWd> x[CPT][K] = {};
-    auto prefetch = [&](int64_t t0) {
+    Col<NWd> xs[PF][CPT][K] = {};
+    auto prefetch = [&](Col<NWd> (&x)[CPT][K], int64_t t0) {
 #pragma unroll
         for (int c = 0; c < CPT; ++c) {
             const int col = tid + c * NT;
@@ -135,11 +167,12 @@ __global__ void __launch_bounds__(NT) k_encode_hash(EncArgs a) {
             const uint8_t* blk = a.data + b * a.data_stride;
 #pragma unroll
             for (int j = 0; j < K; ++j)
-                if (live) x[c][j] = ldcol<NWd>(blk + (int64_t)j * S + t0 + o);
+                if (live) x[c][j] = NTL ? ldcol_nt<NWd>(blk + (int64_t)j * S + t0 + o)
+                                        : ldcol<NWd>(blk + (int64_t)j * S + t0 + o);
         }
     };
 
-    auto encode_store = [&](int64_t t0, int L, uint8_t* tl) {
+    auto encode_store = [&](Col<NWd> (&x)[CPT][K], int64_t t0, int L, uint8_t* tl) {
 #pragma unroll
         for (int c = 0; c < CPT; ++c) {
             const int col = tid + c * NT;
@@ -175,24 +208,38 @@ __global__ void __launch_bounds__(NT) k_encode_hash(EncArgs a) {
 #pragma unroll
                 for (int w = 0; w < NWd; ++w) p.w[w] = acc_done(acc[r][w]);
                 stcol<NWd>(tl + (g * R + K + r) * TS + o, p);
-                stcol<NWd>(pbase + (int64_t)r * S, p);
+                if (NTL)
+                    stcol_nt<NWd>(pbase + (int64_t)r * S, p);
+                else
+                    stcol<NWd>(pbase + (int64_t)r * S, p);
             }
         }
     };
 
     lds_barrier();  // tables visible
-    prefetch(0);
-    int it = 0;
-    for (int64_t t0 = 0; t0 < S; t0 += T, ++it) {
+    // Register prefetch PF tiles deep: tile i lives in xs[i % PF]; the loop is
+    // unrolled by PF so the slot index is a compile-time constant.
+#pragma unroll
+    for (int p = 0; p < PF; ++p)
+        if ((int64_t)p * T < S) prefetch(xs[p], (int64_t)p * T);
+    auto step = [&](Col<NWd> (&x)[CPT][K], int64_t t0, int it) {
         const int L = (int)((S - t0) < T ? (S - t0) : T);
         uint8_t* tl = tile[NBUF == 1 ? 0 : (it & 1)];
-        encode_store(t0, L, tl);
-        if (t0 + T < S) prefetch(t0 + T);
+        encode_store(x, t0, L, tl);
+        if (t0 + (int64_t)PF * T < S) prefetch(x, t0 + (int64_t)PF * T);
         lds_barrier();
         const uint8_t* row = tl + crow * TS;
         hh_packets(st, row, L >> 5, lane, sel);
         if (t0 + L >= S && (L & 31)) hh_remainder(st, row + (L & ~31), (uint32_t)(L & 31), lane, sel);
         if (NBUF == 1) lds_barrier();
+    };
+    int it = 0;
+    for (int64_t t0 = 0; t0 < S; t0 += (int64_t)PF * T) {
+#pragma unroll
+        for (int p = 0; p < PF; ++p) {
+            const int64_t tp = t0 + (int64_t)p * T;
+            if (tp < S) step(xs[p], tp, it++);
+        }
     }
     const uint64_t h = hh_finalize256(st, lane, sel);
     if (chain_live) {
@@ -486,13 +533,13 @@ __global__ void __launch_bounds__(256) k_fill(uint8_t* out, int64_t stride, int6
 
 // ---------------------------------------------------------------------------
 // Dispatch
-template <int K, int M, int G, int T, int NBUF, int CW>
+template <int K, int M, int G, int T, int NBUF, int CW, int PF = 1, bool NTL = false>
 static void launch_fused(const EncArgs& a, hipStream_t s) {
     constexpr int R = K + M;
     constexpr int NT = round64(4 * G * R);
     static_assert(T % CW == 0 && T % 32 == 0, "tile");
     const int64_t grid = (a.n_blocks + G - 1) / G;
-    hipLaunchKernelGGL((k_encode_hash<K, M, G, T, NBUF, NT, CW>), dim3((unsigned)grid), dim3(NT), 0, s, a);
+    hipLaunchKernelGGL((k_encode_hash<K, M, G, T, NBUF, NT, CW, PF, NTL>), dim3((unsigned)grid), dim3(NT), 0, s, a);
 }
 
 static int env_variant() {
@@ -518,6 +565,14 @@ static bool launch_variant(int v, const EncArgs& a, hipStream_t s) {
         case 6: launch_fused<K, M, G, 768, 2, 16>(a, s); return true;
         case 7: launch_fused<K, M, G, 512, 2, 16>(a, s); return true;
         case 8: launch_fused<K, M, G, 192, 1, 4>(a, s); return true;
+        case 9: launch_fused<K, M, G, 384, 1, 8, 2>(a, s); return true;
+        case 10: launch_fused<K, M, G, 384, 1, 8, 2, true>(a, s); return true;
+        case 11: launch_fused<K, M, G, 256, 2, 16, 2>(a, s); return true;
+        case 12: launch_fused<K, M, G, 192, 2, 4, 2>(a, s); return true;
+        case 13: launch_fused<K, M, G, 768, 1, 16, 2>(a, s); return true;
+        case 14: launch_fused<K, M, G, 384, 1, 8, 1, true>(a, s); return true;
+        case 15: launch_fused<K, M, G, 384, 1, 8, 3>(a, s); return true;
+        case 16: launch_fused<K, M, G, 192, 1, 4, 3>(a, s); return true;
         default: return false;
     }
 }

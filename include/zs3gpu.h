@@ -160,6 +160,9 @@ int zs3_last_path(void);
 /* Diagnostics: select an experimental tile/column variant of the fused encode
  * kernel for the headline shapes (0 = tuned default).  Not for production use. */
 int zs3_debug_set_variant(int variant);
+/* Diagnostics: device buffer receiving per-wave phase cycle sums from the
+ * stamped variants (NULL = off). */
+int zs3_debug_set_buffer(void* d_dbg);
 
 #ifdef __cplusplus
 }

@@ -40,7 +40,7 @@ EXPORTS = [
     "zs3_shard_file_size", "zs3_shard_file_offset", "zs3_bitrot_shard_file_size",
     "zs3_encode_batch", "zs3_reconstruct_batch", "zs3_hh256_batch", "zs3_hh256_verify_batch",
     "zs3_fill_batch", "zs3_encode_data", "zs3_decode_data_blocks", "zs3_hh256", "zs3_selftest",
-    "zs3_last_path", "zs3_debug_set_variant",
+    "zs3_last_path", "zs3_debug_set_variant", "zs3_debug_set_buffer",
 ]
 
 
@@ -236,6 +236,12 @@ def last_path() -> int:
 def set_variant(v: int) -> None:
     """Diagnostics: experimental fused-kernel variant (0 = tuned default)."""
     lib().zs3_debug_set_variant(v)
+
+
+def set_debug_buffer(t) -> None:
+    L = lib()
+    L.zs3_debug_set_buffer.argtypes = [C.c_void_p]
+    L.zs3_debug_set_buffer(_ptr(t))
 
 
 def device_count() -> int:

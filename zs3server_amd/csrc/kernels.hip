@@ -126,7 +126,7 @@ __device__ __forceinline__ void stcol(uint8_t* p, const Col<NWd>& v) {
     __builtin_memcpy(p, &v, 4 * NWd);
 }
 
-template <int K, int M, int G, int T, int NBUF, int NT, int CW, int PF, bool NTL>
+template <int K, int M, int G, int T, int NBUF, int NT, int CW, int PF, bool NTL, bool STAMP = false>
 __global__ void __launch_bounds__(NT) k_encode_hash(EncArgs a) {
     constexpr int R = K + M;
     constexpr int NWd = CW / 4;
@@ -222,16 +222,40 @@ __global__ void __launch_bounds__(NT) k_encode_hash(EncArgs a) {
 #pragma unroll
     for (int p = 0; p < PF; ++p)
         if ((int64_t)p * T < S) prefetch(xs[p], (int64_t)p * T);
+    // Diagnostics build (STAMP): s_memtime around each phase, summed per wave.
+    uint64_t ph[5] = {0, 0, 0, 0, 0};
+    auto stamp = [&]() -> uint64_t {
+        uint64_t t = 0;
+        if constexpr (STAMP) {
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        return t;
+    };
     auto step = [&](Col<NWd> (&x)[CPT][K], int64_t t0, int it) {
         const int L = (int)((S - t0) < T ? (S - t0) : T);
         uint8_t* tl = tile[NBUF == 1 ? 0 : (it & 1)];
+        const uint64_t s0 = stamp();
         encode_store(x, t0, L, tl);
+        const uint64_t s1 = stamp();
         if (t0 + (int64_t)PF * T < S) prefetch(x, t0 + (int64_t)PF * T);
+        const uint64_t s2 = stamp();
         lds_barrier();
+        const uint64_t s3 = stamp();
         const uint8_t* row = tl + crow * TS;
         hh_packets(st, row, L >> 5, lane, sel);
         if (t0 + L >= S && (L & 31)) hh_remainder(st, row + (L & ~31), (uint32_t)(L & 31), lane, sel);
+        const uint64_t s4 = stamp();
         if (NBUF == 1) lds_barrier();
+        const uint64_t s5 = stamp();
+        if constexpr (STAMP) {
+            ph[0] += s1 - s0;
+            ph[1] += s2 - s1;
+            ph[2] += s3 - s2;
+            ph[3] += s4 - s3;
+            ph[4] += s5 - s4;
+        }
     };
     int it = 0;
     for (int64_t t0 = 0; t0 < S; t0 += (int64_t)PF * T) {
@@ -247,6 +271,12 @@ __global__ void __launch_bounds__(NT) k_encode_hash(EncArgs a) {
         const int s = chain % R;
         uint8_t* out = a.sums + (b * R + s) * 32 + 8 * lane;
         *reinterpret_cast<uint64_t*>(out) = h;
+    }
+    if constexpr (STAMP) {
+        if ((tid & 63) == 0 && a.dbg) {
+            uint64_t* d = a.dbg + ((int64_t)blockIdx.x * (NT / 64) + (tid >> 6)) * 5;
+            for (int i = 0; i < 5; ++i) d[i] = ph[i];
+        }
     }
 }
 
@@ -533,13 +563,13 @@ __global__ void __launch_bounds__(256) k_fill(uint8_t* out, int64_t stride, int6
 
 // ---------------------------------------------------------------------------
 // Dispatch
-template <int K, int M, int G, int T, int NBUF, int CW, int PF = 1, bool NTL = false>
+template <int K, int M, int G, int T, int NBUF, int CW, int PF = 1, bool NTL = false, bool STAMP = false>
 static void launch_fused(const EncArgs& a, hipStream_t s) {
     constexpr int R = K + M;
     constexpr int NT = round64(4 * G * R);
     static_assert(T % CW == 0 && T % 32 == 0, "tile");
     const int64_t grid = (a.n_blocks + G - 1) / G;
-    hipLaunchKernelGGL((k_encode_hash<K, M, G, T, NBUF, NT, CW, PF, NTL>), dim3((unsigned)grid), dim3(NT), 0, s, a);
+    hipLaunchKernelGGL((k_encode_hash<K, M, G, T, NBUF, NT, CW, PF, NTL, STAMP>), dim3((unsigned)grid), dim3(NT), 0, s, a);
 }
 
 static int env_variant() {
@@ -573,6 +603,8 @@ static bool launch_variant(int v, const EncArgs& a, hipStream_t s) {
         case 14: launch_fused<K, M, G, 384, 1, 8, 1, true>(a, s); return true;
         case 15: launch_fused<K, M, G, 384, 1, 8, 3>(a, s); return true;
         case 16: launch_fused<K, M, G, 192, 1, 4, 3>(a, s); return true;
+        case 101: launch_fused<K, M, G, 384, 1, 8, 1, false, true>(a, s); return true;
+        case 102: launch_fused<K, M, G, 256, 2, 16, 1, false, true>(a, s); return true;
         default: return false;
     }
 }

@@ -23,6 +23,7 @@ struct EncArgs {
     int64_t n_blocks;
     uint64_t key[4];          // HighwayHash key words (little-endian)
     int k, m;
+    uint64_t* dbg;            // diagnostics build only: per-wave phase cycle sums
 };
 
 // Reconstruct: out rows = coef x valid rows, per block.  Block b shard i at

@@ -30,6 +30,7 @@ const uint8_t kMagicKey[32] = {0x4b, 0xe7, 0x34, 0xfa, 0x8e, 0x23, 0x8a, 0xcd, 0
                                0x44, 0x14, 0x97, 0xe0, 0x9d, 0x13, 0x22, 0xde, 0x36, 0xa0};
 
 thread_local int t_last_path = -1;
+uint64_t* g_dbg = nullptr;  // diagnostics: stamped-variant output buffer
 
 void key_words(const uint8_t* key, uint64_t out[4]) {
     const uint8_t* k = key ? key : kMagicKey;
@@ -432,6 +433,7 @@ int zs3_encode_batch(const zs3_codec* cc, const uint8_t* d_data, int64_t data_st
     a.k = c->k;
     a.m = c->m;
     key_words(nullptr, a.key);
+    a.dbg = g_dbg;
     bool fast = false;
     rc = map_hip(zs3k::launch_encode(a, (hipStream_t)stream, &fast));
     t_last_path = fast ? 1 : 0;
@@ -644,6 +646,11 @@ int zs3_last_path(void) { return t_last_path; }
 
 int zs3_debug_set_variant(int variant) {
     zs3k::set_variant(variant);
+    return ZS3_OK;
+}
+
+int zs3_debug_set_buffer(void* d_dbg) {
+    g_dbg = (uint64_t*)d_dbg;
     return ZS3_OK;
 }
 

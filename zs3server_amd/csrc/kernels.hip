@@ -281,6 +281,155 @@ __global__ void __launch_bounds__(NT) k_encode_hash(EncArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Software-pipelined fused kernel: in step i every wave hashes tile i (LDS buffer
+// i%2) AND encodes tile i+1 (into buffer (i+1)%2) in ONE basic block, so the
+// serial HighwayHash chain (~200 cycles of dependent latency per packet) is
+// filled with the independent GF(2^8) encode work instead of being serialised
+// with it behind a barrier.  One barrier per step.  Full tiles hash NPK = T/32
+// packets fully unrolled; a trailing partial tile uses the looped path.
+template <int K, int M, int G, int T, int NT, int CW, bool STAMP = false>
+__global__ void __launch_bounds__(NT) k_encode_hash_pipe(EncArgs a) {
+    constexpr int R = K + M;
+    constexpr int NWd = CW / 4;
+    constexpr int TS = T + 32;
+    constexpr int CPB = T / CW;
+    constexpr int NCOL = G * CPB;
+    constexpr int NPK = T / 32;
+    static_assert(NCOL <= NT, "one column per thread");
+
+    __shared__ __attribute__((aligned(16))) uint8_t tile[2][G * R * TS];
+    __shared__ __attribute__((aligned(16))) uint32_t tabs[M * K * 8];
+
+    const int tid = threadIdx.x;
+    const int64_t blk0 = (int64_t)blockIdx.x * G;
+    const int64_t S = a.S;
+    const int64_t ntile = (S + T - 1) / T;
+
+    for (int i = tid; i < M * K * 8; i += NT) tabs[i] = a.tables[i];
+
+    const int chain = tid >> 2, lane = tid & 3;
+    const bool chain_live = chain < G * R && (blk0 + chain / R) < a.n_blocks;
+    const int crow = chain < G * R ? chain : 0;
+    const uint32_t sel = zipper_sel(lane);
+    HHLane st = hh_init(lane, a.key[0], a.key[1], a.key[2], a.key[3]);
+
+    // encode column of this thread (dead stripes alias the last live block)
+    const bool col_live = tid < NCOL;
+    const int g = col_live ? tid / CPB : 0;
+    const int o = (tid % CPB) * CW;
+    const int64_t b = (blk0 + g) < a.n_blocks ? (blk0 + g) : (a.n_blocks - 1);
+    const uint8_t* blk = a.data + b * a.data_stride + o;
+    uint8_t* pbase = a.parity + b * a.parity_stride + o;
+
+    Col<NWd> x[K] = {};
+    auto load_tile = [&](int64_t t0) {
+        if (col_live && t0 + o < S) {
+#pragma unroll
+            for (int j = 0; j < K; ++j) x[j] = ldcol<NWd>(blk + (int64_t)j * S + t0);
+        }
+    };
+    auto encode_tile = [&](int64_t t0, uint8_t* tl) {
+        if (!(col_live && t0 + o < S)) return;
+        const uint32_t* tb = tabs + opaque_zero();
+        GfAcc acc[M][NWd];
+#pragma unroll
+        for (int r = 0; r < M; ++r)
+#pragma unroll
+            for (int w = 0; w < NWd; ++w) acc_init(acc[r][w]);
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            Nib nb[NWd];
+#pragma unroll
+            for (int w = 0; w < NWd; ++w) nb[w] = split_nibbles(x[j].w[w]);
+#pragma unroll
+            for (int r = 0; r < M; ++r) {
+                const CoefTab t = load_coef(tb, r * K + j);
+#pragma unroll
+                for (int w = 0; w < NWd; ++w) acc_add(acc[r][w], gf_lookup(nb[w], t));
+            }
+            stcol<NWd>(tl + (g * R + j) * TS + o, x[j]);
+        }
+#pragma unroll
+        for (int r = 0; r < M; ++r) {
+            Col<NWd> p;
+#pragma unroll
+            for (int w = 0; w < NWd; ++w) p.w[w] = acc_done(acc[r][w]);
+            stcol<NWd>(tl + (g * R + K + r) * TS + o, p);
+            stcol<NWd>(pbase + (int64_t)r * S + t0, p);
+        }
+    };
+    auto hash_full = [&](const uint8_t* tl) {
+        const uint64_t* p = reinterpret_cast<const uint64_t*>(tl + crow * TS) + lane;
+        uint64_t w[NPK];
+#pragma unroll
+        for (int i = 0; i < NPK; ++i) w[i] = p[4 * i];
+#pragma unroll
+        for (int i = 0; i < NPK; ++i) hh_update(st, w[i], sel);
+    };
+    auto hash_part = [&](const uint8_t* tl, int L) {
+        const uint8_t* row = tl + crow * TS;
+        hh_packets(st, row, L >> 5, lane, sel);
+        if (L & 31) hh_remainder(st, row + (L & ~31), (uint32_t)(L & 31), lane, sel);
+    };
+
+    uint64_t ph[3] = {0, 0, 0};
+    auto stamp = [&]() -> uint64_t {
+        uint64_t t = 0;
+        if constexpr (STAMP) {
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        return t;
+    };
+
+    lds_barrier();  // tables visible
+    load_tile(0);
+    encode_tile(0, tile[0]);
+    if (ntile > 1) load_tile(T);
+    lds_barrier();
+    for (int64_t i = 0; i < ntile; ++i) {
+        uint8_t* cur = tile[i & 1];
+        uint8_t* nxt = tile[(i + 1) & 1];
+        const int64_t t_next = (i + 1) * T;
+        const int Lcur = (int)((S - i * T) < T ? (S - i * T) : T);
+        const uint64_t s0 = stamp();
+        if (Lcur == T) {
+            // one basic block: encode(i+1) || hash(i)
+            encode_tile(t_next, nxt);
+            hash_full(cur);
+        } else {
+            encode_tile(t_next, nxt);
+            hash_part(cur, Lcur);
+        }
+        const uint64_t s1 = stamp();
+        if (t_next + T < S) load_tile(t_next + T);
+        lds_barrier();
+        const uint64_t s2 = stamp();
+        if constexpr (STAMP) {
+            ph[0] += s1 - s0;
+            ph[1] += s2 - s1;
+        }
+    }
+    const uint64_t h = hh_finalize256(st, lane, sel);
+    if (chain_live) {
+        const int64_t bb = blk0 + chain / R;
+        const int s = chain % R;
+        *reinterpret_cast<uint64_t*>(a.sums + (bb * R + s) * 32 + 8 * lane) = h;
+    }
+    if constexpr (STAMP) {
+        if ((tid & 63) == 0 && a.dbg) {
+            uint64_t* d = a.dbg + ((int64_t)blockIdx.x * (NT / 64) + (tid >> 6)) * 5;
+            d[0] = ph[0];
+            d[1] = 0;
+            d[2] = ph[1];
+            d[3] = 0;
+            d[4] = 0;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Encode only (no hash): one thread per 16-byte column, K loads -> M stores.
 template <int K, int M>
 __global__ void __launch_bounds__(256) k_encode_only(EncArgs a) {
@@ -572,6 +721,19 @@ static void launch_fused(const EncArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((k_encode_hash<K, M, G, T, NBUF, NT, CW, PF, NTL, STAMP>), dim3((unsigned)grid), dim3(NT), 0, s, a);
 }
 
+template <int K, int M, int G, int T, int CW, bool STAMP = false>
+static void launch_pipe(const EncArgs& a, hipStream_t s) {
+    constexpr int R = K + M;
+    constexpr int NT = round64(4 * G * R);
+    static_assert(T % CW == 0 && T % 32 == 0, "tile");
+    if constexpr (G * T / CW <= NT) {
+        const int64_t grid = (a.n_blocks + G - 1) / G;
+        hipLaunchKernelGGL((k_encode_hash_pipe<K, M, G, T, NT, CW, STAMP>), dim3((unsigned)grid), dim3(NT), 0, s, a);
+    } else {
+        launch_fused<K, M, G, T, 1, CW>(a, s);
+    }
+}
+
 static int env_variant() {
     static int v = -2;
     if (v == -2) {
@@ -603,6 +765,11 @@ static bool launch_variant(int v, const EncArgs& a, hipStream_t s) {
         case 14: launch_fused<K, M, G, 384, 1, 8, 1, true>(a, s); return true;
         case 15: launch_fused<K, M, G, 384, 1, 8, 3>(a, s); return true;
         case 16: launch_fused<K, M, G, 192, 1, 4, 3>(a, s); return true;
+        case 20: launch_pipe<K, M, G, 384, 8>(a, s); return true;
+        case 21: launch_pipe<K, M, G, 192, 4>(a, s); return true;
+        case 22: launch_pipe<K, M, G, 256, 8>(a, s); return true;
+        case 23: launch_pipe<K, M, G, 320, 8>(a, s); return true;
+        case 120: launch_pipe<K, M, G, 384, 8, true>(a, s); return true;
         case 101: launch_fused<K, M, G, 384, 1, 8, 1, false, true>(a, s); return true;
         case 102: launch_fused<K, M, G, 256, 2, 16, 1, false, true>(a, s); return true;
         default: return false;

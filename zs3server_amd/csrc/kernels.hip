@@ -383,6 +383,11 @@ __global__ void __launch_bounds__(NT) k_encode_hash_pipe(EncArgs a) {
         return t;
     };
 
+    uint64_t rt0 = 0, ct0 = 0;
+    if constexpr (STAMP) {
+        rt0 = __builtin_amdgcn_s_memrealtime();
+        ct0 = __builtin_amdgcn_s_memtime();
+    }
     lds_barrier();  // tables visible
     load_tile(0);
     encode_tile(0, tile[0]);
@@ -420,11 +425,13 @@ __global__ void __launch_bounds__(NT) k_encode_hash_pipe(EncArgs a) {
     if constexpr (STAMP) {
         if ((tid & 63) == 0 && a.dbg) {
             uint64_t* d = a.dbg + ((int64_t)blockIdx.x * (NT / 64) + (tid >> 6)) * 5;
+            const uint64_t rt1 = __builtin_amdgcn_s_memrealtime();
+            const uint64_t ct1 = __builtin_amdgcn_s_memtime();
             d[0] = ph[0];
-            d[1] = 0;
+            d[1] = rt0;
             d[2] = ph[1];
-            d[3] = 0;
-            d[4] = 0;
+            d[3] = rt1;
+            d[4] = ct1 - ct0;
         }
     }
 }

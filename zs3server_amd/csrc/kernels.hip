@@ -44,14 +44,6 @@ __device__ __forceinline__ uint4 ld16(const uint8_t* p) {
 }
 __device__ __forceinline__ void st16(uint8_t* p, const uint4& v) { __builtin_memcpy(p, &v, 16); }
 
-// An SGPR zero the compiler cannot see through: indexing the LDS coefficient
-// tables with it keeps their loads inside the loop instead of hoisting all
-// m*k*5 dwords into VGPRs (which would cap occupancy at one wave per SIMD).
-__device__ __forceinline__ int opaque_zero() {
-    int z = 0;
-    asm volatile("" : "+s"(z));
-    return z;
-}
 
 constexpr int gcd_c(int a, int b) { return b ? gcd_c(b, a % b) : a; }
 
@@ -78,11 +70,6 @@ constexpr int pick_T() {
 // ---------------------------------------------------------------------------
 // Fused Split + Encode + HighwayHash-256 over G stripes per workgroup.
 // CW = bytes per encode column per thread (16 -> dwordx4 loads, 8 -> dwordx2, 4 -> dword).
-template <int NWd>
-struct Col {
-    uint32_t w[NWd];
-};
-
 template <int NWd>
 __device__ __forceinline__ Col<NWd> ldcol(const uint8_t* p) {
     Col<NWd> v;
@@ -126,7 +113,7 @@ __device__ __forceinline__ void stcol(uint8_t* p, const Col<NWd>& v) {
     __builtin_memcpy(p, &v, 4 * NWd);
 }
 
-template <int K, int M, int G, int T, int NBUF, int NT, int CW, int PF, bool NTL, bool STAMP = false>
+template <int K, int M, int G, int T, int NBUF, int NT, int CW, int PF, bool NTL, bool STAMP = false, int DYB = 0>
 __global__ void __launch_bounds__(NT) k_encode_hash(EncArgs a) {
     constexpr int R = K + M;
     constexpr int NWd = CW / 4;
@@ -135,14 +122,16 @@ __global__ void __launch_bounds__(NT) k_encode_hash(EncArgs a) {
     constexpr int NCOL = G * CPB;
     constexpr int CPT = (NCOL + NT - 1) / NT;
 
+    constexpr int NTAB = DYB ? (K / M) * (M == 4 ? 9 : 3) * 8 : M * K * 8;
     __shared__ __attribute__((aligned(16))) uint8_t tile[NBUF][G * R * TS];
-    __shared__ __attribute__((aligned(16))) uint32_t tabs[M * K * 8];
+    __shared__ __attribute__((aligned(16))) uint32_t tabs[NTAB];
+    const uint32_t* dtabs = tabs;
 
     const int tid = threadIdx.x;
     const int64_t blk0 = (int64_t)blockIdx.x * G;
     const int64_t S = a.S;
 
-    for (int i = tid; i < M * K * 8; i += NT) tabs[i] = a.tables[i];
+    for (int i = tid; i < NTAB; i += NT) tabs[i] = DYB ? a.dtables[i] : a.tables[i];
 
     // ---- hash-chain role: quad = one shard row of one stripe
     const int chain = tid >> 2, lane = tid & 3;
@@ -181,32 +170,14 @@ __global__ void __launch_bounds__(NT) k_encode_hash(EncArgs a) {
             const int o = (col % CPB) * CW;
             const int64_t b = (blk0 + g) < a.n_blocks ? (blk0 + g) : (a.n_blocks - 1);
             if (o >= L) continue;
-            const uint32_t* tb = tabs + opaque_zero();
-            GfAcc acc[M][NWd];
+            Col<NWd> par[M];
+            encode_column<NWd, K, M, DYB>(x[c], par, tabs, dtabs);
 #pragma unroll
-            for (int r = 0; r < M; ++r)
-#pragma unroll
-                for (int w = 0; w < NWd; ++w) acc_init(acc[r][w]);
-#pragma unroll
-            for (int j = 0; j < K; ++j) {
-                __builtin_amdgcn_sched_barrier(0);  // keep each shard's table reads local
-                Nib nb[NWd];
-#pragma unroll
-                for (int w = 0; w < NWd; ++w) nb[w] = split_nibbles(x[c][j].w[w]);
-#pragma unroll
-                for (int r = 0; r < M; ++r) {
-                    const CoefTab t = load_coef(tb, r * K + j);
-#pragma unroll
-                    for (int w = 0; w < NWd; ++w) acc_add(acc[r][w], gf_lookup(nb[w], t));
-                }
-                stcol<NWd>(tl + (g * R + j) * TS + o, x[c][j]);
-            }
+            for (int j = 0; j < K; ++j) stcol<NWd>(tl + (g * R + j) * TS + o, x[c][j]);
             uint8_t* pbase = a.parity + b * a.parity_stride + t0 + o;
 #pragma unroll
             for (int r = 0; r < M; ++r) {
-                Col<NWd> p;
-#pragma unroll
-                for (int w = 0; w < NWd; ++w) p.w[w] = acc_done(acc[r][w]);
+                const Col<NWd>& p = par[r];
                 stcol<NWd>(tl + (g * R + K + r) * TS + o, p);
                 if (NTL)
                     stcol_nt<NWd>(pbase + (int64_t)r * S, p);
@@ -287,7 +258,7 @@ __global__ void __launch_bounds__(NT) k_encode_hash(EncArgs a) {
 // filled with the independent GF(2^8) encode work instead of being serialised
 // with it behind a barrier.  One barrier per step.  Full tiles hash NPK = T/32
 // packets fully unrolled; a trailing partial tile uses the looped path.
-template <int K, int M, int G, int T, int NT, int CW, bool STAMP = false>
+template <int K, int M, int G, int T, int NT, int CW, bool STAMP = false, int DYB = 0>
 __global__ void __launch_bounds__(NT) k_encode_hash_pipe(EncArgs a) {
     constexpr int R = K + M;
     constexpr int NWd = CW / 4;
@@ -297,15 +268,17 @@ __global__ void __launch_bounds__(NT) k_encode_hash_pipe(EncArgs a) {
     constexpr int NPK = T / 32;
     static_assert(NCOL <= NT, "one column per thread");
 
+    constexpr int NTAB = DYB ? (K / M) * (M == 4 ? 9 : 3) * 8 : M * K * 8;
     __shared__ __attribute__((aligned(16))) uint8_t tile[2][G * R * TS];
-    __shared__ __attribute__((aligned(16))) uint32_t tabs[M * K * 8];
+    __shared__ __attribute__((aligned(16))) uint32_t tabs[NTAB];
+    const uint32_t* dtabs = tabs;
 
     const int tid = threadIdx.x;
     const int64_t blk0 = (int64_t)blockIdx.x * G;
     const int64_t S = a.S;
     const int64_t ntile = (S + T - 1) / T;
 
-    for (int i = tid; i < M * K * 8; i += NT) tabs[i] = a.tables[i];
+    for (int i = tid; i < NTAB; i += NT) tabs[i] = DYB ? a.dtables[i] : a.tables[i];
 
     const int chain = tid >> 2, lane = tid & 3;
     const bool chain_live = chain < G * R && (blk0 + chain / R) < a.n_blocks;
@@ -330,30 +303,13 @@ __global__ void __launch_bounds__(NT) k_encode_hash_pipe(EncArgs a) {
     };
     auto encode_tile = [&](int64_t t0, uint8_t* tl) {
         if (!(col_live && t0 + o < S)) return;
-        const uint32_t* tb = tabs + opaque_zero();
-        GfAcc acc[M][NWd];
+        Col<NWd> par[M];
+        encode_column<NWd, K, M, DYB>(x, par, tabs, dtabs);
 #pragma unroll
-        for (int r = 0; r < M; ++r)
-#pragma unroll
-            for (int w = 0; w < NWd; ++w) acc_init(acc[r][w]);
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-            Nib nb[NWd];
-#pragma unroll
-            for (int w = 0; w < NWd; ++w) nb[w] = split_nibbles(x[j].w[w]);
-#pragma unroll
-            for (int r = 0; r < M; ++r) {
-                const CoefTab t = load_coef(tb, r * K + j);
-#pragma unroll
-                for (int w = 0; w < NWd; ++w) acc_add(acc[r][w], gf_lookup(nb[w], t));
-            }
-            stcol<NWd>(tl + (g * R + j) * TS + o, x[j]);
-        }
+        for (int j = 0; j < K; ++j) stcol<NWd>(tl + (g * R + j) * TS + o, x[j]);
 #pragma unroll
         for (int r = 0; r < M; ++r) {
-            Col<NWd> p;
-#pragma unroll
-            for (int w = 0; w < NWd; ++w) p.w[w] = acc_done(acc[r][w]);
+            const Col<NWd>& p = par[r];
             stcol<NWd>(tl + (g * R + K + r) * TS + o, p);
             stcol<NWd>(pbase + (int64_t)r * S + t0, p);
         }
@@ -721,10 +677,18 @@ __global__ void __launch_bounds__(256) k_fill(uint8_t* out, int64_t stride, int6
 // Dispatch
 template <int K, int M, int G, int T, int NBUF, int CW, int PF = 1, bool NTL = false, bool STAMP = false>
 static void launch_fused(const EncArgs& a, hipStream_t s) {
+    constexpr bool CAN_DY = (M == 2 || M == 4) && K % M == 0;
     constexpr int R = K + M;
     constexpr int NT = round64(4 * G * R);
     static_assert(T % CW == 0 && T % 32 == 0, "tile");
     const int64_t grid = (a.n_blocks + G - 1) / G;
+    if constexpr (CAN_DY) {
+        if (a.dyb == M) {
+            hipLaunchKernelGGL((k_encode_hash<K, M, G, T, NBUF, NT, CW, PF, NTL, STAMP, M>), dim3((unsigned)grid),
+                               dim3(NT), 0, s, a);
+            return;
+        }
+    }
     hipLaunchKernelGGL((k_encode_hash<K, M, G, T, NBUF, NT, CW, PF, NTL, STAMP>), dim3((unsigned)grid), dim3(NT), 0, s, a);
 }
 
@@ -735,6 +699,14 @@ static void launch_pipe(const EncArgs& a, hipStream_t s) {
     static_assert(T % CW == 0 && T % 32 == 0, "tile");
     if constexpr (G * T / CW <= NT) {
         const int64_t grid = (a.n_blocks + G - 1) / G;
+        constexpr bool CAN_DY = (M == 2 || M == 4) && K % M == 0;
+        if constexpr (CAN_DY) {
+            if (a.dyb == M) {
+                hipLaunchKernelGGL((k_encode_hash_pipe<K, M, G, T, NT, CW, STAMP, M>), dim3((unsigned)grid), dim3(NT),
+                                   0, s, a);
+                return;
+            }
+        }
         hipLaunchKernelGGL((k_encode_hash_pipe<K, M, G, T, NT, CW, STAMP>), dim3((unsigned)grid), dim3(NT), 0, s, a);
     } else {
         launch_fused<K, M, G, T, 1, CW>(a, s);
@@ -795,7 +767,17 @@ static hipError_t run_encode_fast(const EncArgs& a, hipStream_t s) {
             const int v = env_variant();
             if (v > 0) done = launch_variant<K, M>(v, a, s);
         }
-        if (!done) launch_fused<K, M, G, T, NBUF, 16>(a, s);
+        if (!done) {
+            // Tuned defaults (scripts/sweep_variants.py on MI355X, profiles/r01):
+            // 8-byte columns so every thread encodes, one 384-byte tile per step;
+            // the software-pipelined kernel where two LDS tiles fit 4 workgroups/CU.
+            if constexpr (2 * G * R * (384 + 32) + M * K * 32 <= 40960)
+                launch_pipe<K, M, G, 384, 8>(a, s);
+            else if constexpr (G * R * (384 + 32) + M * K * 32 <= 40960)
+                launch_fused<K, M, G, 384, 1, 8>(a, s);
+            else
+                launch_fused<K, M, G, T, NBUF, 16>(a, s);
+        }
     } else {
         const int64_t cols = (a.S + 15) >> 4;
         const unsigned gx = (unsigned)((cols + 255) / 256);

@@ -24,6 +24,8 @@ struct EncArgs {
     uint64_t key[4];          // HighwayHash key words (little-endian)
     int k, m;
     uint64_t* dbg;            // diagnostics build only: per-wave phase cycle sums
+    int dyb;                  // 0, or 2/4: parity block is dyadic in dyb x dyb blocks
+    const uint32_t* dtables;  // dyadic Karatsuba tables (3 or 9 coefficients per block)
 };
 
 // Reconstruct: out rows = coef x valid rows, per block.  Block b shard i at

@@ -31,6 +31,7 @@ const uint8_t kMagicKey[32] = {0x4b, 0xe7, 0x34, 0xfa, 0x8e, 0x23, 0x8a, 0xcd, 0
 
 thread_local int t_last_path = -1;
 uint64_t* g_dbg = nullptr;  // diagnostics: stamped-variant output buffer
+int g_no_dyadic = 0;        // diagnostics: force the plain (m*k multiply) encode
 
 void key_words(const uint8_t* key, uint64_t out[4]) {
     const uint8_t* k = key ? key : kMagicKey;
@@ -82,7 +83,9 @@ struct zs3_codec {
     int k, m;
     int64_t block_size;
     std::vector<uint8_t> matrix;   // (k+m) x k
-    std::vector<uint32_t> tables;  // m x k x 8 (parity rows)
+    std::vector<uint32_t> tables;  // m x k x 8 (parity rows), then dyadic tables if dyb
+    int dyb = 0;                   // 2 or 4 when the parity block is dyadic (see below)
+    size_t dyadic_off = 0;         // dword offset of the dyadic tables in `tables`
     std::mutex mu;
     std::map<int, std::shared_ptr<DevBuf>> dev;  // device -> [tables | matrix]
     std::map<std::string, std::shared_ptr<RecPlan>> plans;
@@ -374,6 +377,38 @@ int zs3_codec_new(int k, int m, int64_t block_size, zs3_codec** out) {
     for (int r = 0; r < m; ++r)
         for (int j = 0; j < k; ++j)
             zs3::perm_tables(c->matrix[(size_t)(k + r) * k + j], &c->tables[((size_t)r * k + j) * 8]);
+    // Dyadic structure: the Vandermonde points 0..k+m-1 make the parity block of the
+    // power-of-two shapes (4+2, 8+4, 16+4, ...) dyadic in m x m blocks,
+    // P[r][q*m + t] = D_q[r ^ t], so each block is [[A,B],[B,A]] and a Karatsuba
+    // split needs 3 (m = 2) or 9 (m = 4) GF multiplies instead of m*m.
+    if ((m == 2 || m == 4) && k % m == 0) {
+        bool dy = true;
+        for (int r = 0; r < m && dy; ++r)
+            for (int j = 0; j < k && dy; ++j) {
+                const int q = j / m, t = j % m;
+                dy = c->matrix[(size_t)(k + r) * k + j] == c->matrix[(size_t)k * k + q * m + (r ^ t)];
+            }
+        if (dy) {
+            c->dyb = m;
+            c->dyadic_off = c->tables.size();
+            const int per = m == 4 ? 9 : 3;
+            c->tables.resize(c->tables.size() + (size_t)(k / m) * per * 8, 0);
+            for (int q = 0; q < k / m; ++q) {
+                const uint8_t* D = &c->matrix[(size_t)k * k + q * m];
+                uint8_t co[9];
+                if (m == 2) {
+                    co[0] = D[0]; co[1] = D[1]; co[2] = D[0] ^ D[1];
+                } else {
+                    const uint8_t a = D[0], b = D[1], cc = D[2], d = D[3];
+                    co[0] = a; co[1] = b; co[2] = a ^ b;
+                    co[3] = cc; co[4] = d; co[5] = cc ^ d;
+                    co[6] = a ^ cc; co[7] = b ^ d; co[8] = a ^ b ^ cc ^ d;
+                }
+                for (int i = 0; i < per; ++i)
+                    zs3::perm_tables(co[i], &c->tables[c->dyadic_off + ((size_t)q * per + i) * 8]);
+            }
+        }
+    }
     *out = c.release();
     return ZS3_OK;
 }
@@ -432,6 +467,8 @@ int zs3_encode_batch(const zs3_codec* cc, const uint8_t* d_data, int64_t data_st
     a.n_blocks = n_blocks;
     a.k = c->k;
     a.m = c->m;
+    a.dyb = g_no_dyadic ? 0 : c->dyb;
+    a.dtables = a.tables + c->dyadic_off;
     key_words(nullptr, a.key);
     a.dbg = g_dbg;
     bool fast = false;
@@ -645,7 +682,9 @@ int zs3_selftest(void) {
 int zs3_last_path(void) { return t_last_path; }
 
 int zs3_debug_set_variant(int variant) {
-    zs3k::set_variant(variant);
+    // variant >= 1000: same variant with the plain (non-dyadic) GF encode
+    g_no_dyadic = variant >= 1000;
+    zs3k::set_variant(variant % 1000);
     return ZS3_OK;
 }
 

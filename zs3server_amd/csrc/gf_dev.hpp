@@ -115,34 +115,6 @@ __device__ __forceinline__ int opaque_zero() {
     return z;
 }
 
-// Plain encode of one column: out[r] = XOR_j M[k+r][j] * x[j]  (K*M multiplies).
-template <int NWd, int K, int M>
-__device__ __forceinline__ void encode_plain(const Col<NWd> (&x)[K], Col<NWd> (&out)[M], const uint32_t* tabs) {
-    const uint32_t* tb = tabs + opaque_zero();
-    GfAcc acc[M][NWd];
-#pragma unroll
-    for (int r = 0; r < M; ++r)
-#pragma unroll
-        for (int w = 0; w < NWd; ++w) acc_init(acc[r][w]);
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-        __builtin_amdgcn_sched_barrier(0);  // keep each shard's table reads local
-        Nib nb[NWd];
-#pragma unroll
-        for (int w = 0; w < NWd; ++w) nb[w] = split_nibbles(x[j].w[w]);
-#pragma unroll
-        for (int r = 0; r < M; ++r) {
-            const CoefTab t = load_coef(tb, r * K + j);
-#pragma unroll
-            for (int w = 0; w < NWd; ++w) acc_add(acc[r][w], gf_lookup(nb[w], t));
-        }
-    }
-#pragma unroll
-    for (int r = 0; r < M; ++r)
-#pragma unroll
-        for (int w = 0; w < NWd; ++w) out[r].w[w] = acc_done(acc[r][w]);
-}
-
 // Dyadic encode (parity block = K/M blocks [[A,B],[B,A]]; see zs3gpu.hip).
 // M = 4, per block with generator (a,b,c,d) and inputs x0..x3:
 //   T = a.x0 + b.x1 + c.x2 + d.x3,  R = (a+b)(x0+x1) + (c+d)(x2+x3)
@@ -205,15 +177,6 @@ __device__ __forceinline__ void encode_dyadic(const Col<NWd> (&x)[K], Col<NWd> (
     for (int r = 0; r < M; ++r)
 #pragma unroll
         for (int w = 0; w < NWd; ++w) out[r].w[w] = acc[r][w];
-}
-
-template <int NWd, int K, int M, int DYB>
-__device__ __forceinline__ void encode_column(const Col<NWd> (&x)[K], Col<NWd> (&out)[M], const uint32_t* tabs,
-                                              const uint32_t* dtabs) {
-    if constexpr (DYB == M && (M == 2 || M == 4) && K % M == 0)
-        encode_dyadic<NWd, K, M>(x, out, dtabs);
-    else
-        encode_plain<NWd, K, M>(x, out, tabs);
 }
 
 // Scalar GF multiply with log/exp tables (generic byte path).

@@ -23,6 +23,8 @@
 
 #include <stdlib.h>
 
+#include <type_traits>
+
 using namespace zs3dev;
 
 namespace zs3k {
@@ -171,9 +173,36 @@ __global__ void __launch_bounds__(NT) k_encode_hash(EncArgs a) {
             const int64_t b = (blk0 + g) < a.n_blocks ? (blk0 + g) : (a.n_blocks - 1);
             if (o >= L) continue;
             Col<NWd> par[M];
-            encode_column<NWd, K, M, DYB>(x[c], par, tabs, dtabs);
+            if constexpr (DYB != 0) {
+                encode_dyadic<NWd, K, M>(x[c], par, dtabs);
 #pragma unroll
-            for (int j = 0; j < K; ++j) stcol<NWd>(tl + (g * R + j) * TS + o, x[c][j]);
+                for (int j = 0; j < K; ++j) stcol<NWd>(tl + (g * R + j) * TS + o, x[c][j]);
+            } else {
+                const uint32_t* tb = tabs + opaque_zero();
+                GfAcc acc[M][NWd];
+#pragma unroll
+                for (int r = 0; r < M; ++r)
+#pragma unroll
+                    for (int w = 0; w < NWd; ++w) acc_init(acc[r][w]);
+#pragma unroll
+                for (int j = 0; j < K; ++j) {
+                    __builtin_amdgcn_sched_barrier(0);  // keep each shard's table reads local
+                    Nib nb[NWd];
+#pragma unroll
+                    for (int w = 0; w < NWd; ++w) nb[w] = split_nibbles(x[c][j].w[w]);
+#pragma unroll
+                    for (int r = 0; r < M; ++r) {
+                        const CoefTab t = load_coef(tb, r * K + j);
+#pragma unroll
+                        for (int w = 0; w < NWd; ++w) acc_add(acc[r][w], gf_lookup(nb[w], t));
+                    }
+                    stcol<NWd>(tl + (g * R + j) * TS + o, x[c][j]);
+                }
+#pragma unroll
+                for (int r = 0; r < M; ++r)
+#pragma unroll
+                    for (int w = 0; w < NWd; ++w) par[r].w[w] = acc_done(acc[r][w]);
+            }
             uint8_t* pbase = a.parity + b * a.parity_stride + t0 + o;
 #pragma unroll
             for (int r = 0; r < M; ++r) {
@@ -301,12 +330,44 @@ __global__ void __launch_bounds__(NT) k_encode_hash_pipe(EncArgs a) {
             for (int j = 0; j < K; ++j) x[j] = ldcol<NWd>(blk + (int64_t)j * S + t0);
         }
     };
-    auto encode_tile = [&](int64_t t0, uint8_t* tl) {
-        if (!(col_live && t0 + o < S)) return;
+    // FULL: the caller guarantees tile t0 is a full tile and every thread owns a
+    // column, so the body has no branch and shares a basic block with the hash.
+    auto encode_tile = [&](int64_t t0, uint8_t* tl, auto full) {
+        if constexpr (!decltype(full)::value) {
+            if (!(col_live && t0 + o < S)) return;
+        }
         Col<NWd> par[M];
-        encode_column<NWd, K, M, DYB>(x, par, tabs, dtabs);
+        if constexpr (DYB != 0) {
+            encode_dyadic<NWd, K, M>(x, par, dtabs);
 #pragma unroll
-        for (int j = 0; j < K; ++j) stcol<NWd>(tl + (g * R + j) * TS + o, x[j]);
+            for (int j = 0; j < K; ++j) stcol<NWd>(tl + (g * R + j) * TS + o, x[j]);
+        } else {
+            // plain form kept inline: wrapped in a helper, hipcc's scheduling of
+            // this loop doubles the VGPR count (255 vs 120).
+            const uint32_t* tb = tabs + opaque_zero();
+            GfAcc acc[M][NWd];
+#pragma unroll
+            for (int r = 0; r < M; ++r)
+#pragma unroll
+                for (int w = 0; w < NWd; ++w) acc_init(acc[r][w]);
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                Nib nb[NWd];
+#pragma unroll
+                for (int w = 0; w < NWd; ++w) nb[w] = split_nibbles(x[j].w[w]);
+#pragma unroll
+                for (int r = 0; r < M; ++r) {
+                    const CoefTab t = load_coef(tb, r * K + j);
+#pragma unroll
+                    for (int w = 0; w < NWd; ++w) acc_add(acc[r][w], gf_lookup(nb[w], t));
+                }
+                stcol<NWd>(tl + (g * R + j) * TS + o, x[j]);
+            }
+#pragma unroll
+            for (int r = 0; r < M; ++r)
+#pragma unroll
+                for (int w = 0; w < NWd; ++w) par[r].w[w] = acc_done(acc[r][w]);
+        }
 #pragma unroll
         for (int r = 0; r < M; ++r) {
             const Col<NWd>& p = par[r];
@@ -344,9 +405,11 @@ __global__ void __launch_bounds__(NT) k_encode_hash_pipe(EncArgs a) {
         rt0 = __builtin_amdgcn_s_memrealtime();
         ct0 = __builtin_amdgcn_s_memtime();
     }
+    using Full = std::integral_constant<bool, true>;
+    using Part = std::integral_constant<bool, false>;
     lds_barrier();  // tables visible
     load_tile(0);
-    encode_tile(0, tile[0]);
+    encode_tile(0, tile[0], Part{});
     if (ntile > 1) load_tile(T);
     lds_barrier();
     for (int64_t i = 0; i < ntile; ++i) {
@@ -355,12 +418,15 @@ __global__ void __launch_bounds__(NT) k_encode_hash_pipe(EncArgs a) {
         const int64_t t_next = (i + 1) * T;
         const int Lcur = (int)((S - i * T) < T ? (S - i * T) : T);
         const uint64_t s0 = stamp();
-        if (Lcur == T) {
+        if (NCOL == NT && Lcur == T && t_next + T <= S) {
             // one basic block: encode(i+1) || hash(i)
-            encode_tile(t_next, nxt);
+            encode_tile(t_next, nxt, Full{});
+            hash_full(cur);
+        } else if (Lcur == T) {
+            encode_tile(t_next, nxt, Part{});
             hash_full(cur);
         } else {
-            encode_tile(t_next, nxt);
+            encode_tile(t_next, nxt, Part{});
             hash_part(cur, Lcur);
         }
         const uint64_t s1 = stamp();

@@ -835,14 +835,20 @@ static hipError_t run_encode_fast(const EncArgs& a, hipStream_t s) {
         }
         if (!done) {
             // Tuned defaults (scripts/sweep_variants.py on MI355X, profiles/r01):
-            // 8-byte columns so every thread encodes, one 384-byte tile per step;
-            // the software-pipelined kernel where two LDS tiles fit 4 workgroups/CU.
-            if constexpr (2 * G * R * (384 + 32) + M * K * 32 <= 40960)
-                launch_pipe<K, M, G, 384, 8>(a, s);
-            else if constexpr (G * R * (384 + 32) + M * K * 32 <= 40960)
-                launch_fused<K, M, G, 384, 1, 8>(a, s);
-            else
+            // 8-byte columns so every thread encodes, one 384-byte tile per step,
+            // one LDS tile.  The dyadic (Karatsuba) encode wins for k <= 8; at
+            // k = 16 its extra live tables cost more occupancy than it saves.
+            if constexpr (G * R * (384 + 32) + M * K * 32 <= 40960) {
+                if constexpr (K > 8) {
+                    EncArgs b = a;
+                    b.dyb = 0;
+                    launch_fused<K, M, G, 384, 1, 8>(b, s);
+                } else {
+                    launch_fused<K, M, G, 384, 1, 8>(a, s);
+                }
+            } else {
                 launch_fused<K, M, G, T, NBUF, 16>(a, s);
+            }
         }
     } else {
         const int64_t cols = (a.S + 15) >> 4;

@@ -81,6 +81,23 @@ def cpu_baseline(k: int, m: int, blen: int, seconds: float, threads: int) -> dic
     }
 
 
+def committed_traffic(k: int, m: int, nobj: int, blen: int):
+    """Per-launch HBM bytes measured by scripts/profile_round.sh (two rocprofv3 PMC
+    passes, FETCH_SIZE doubled per the gfx950 correction) for this workload, if the
+    committed profile was taken on the same shape."""
+    import glob
+    best = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json"))):
+        try:
+            d = json.load(open(path))
+        except Exception:
+            continue
+        for name, v in d.items():
+            if f"<{k}, {m}," in name and v.get("workload", {}).get("objects", nobj) == nobj:
+                best = (v["hbm_bytes_per_launch"], os.path.relpath(path, ROOT))
+    return best if best else (None, None)
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -94,7 +111,8 @@ def main() -> None:
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic", type=float, default=None,
-                    help="HBM bytes per launch from a rocprofv3 PMC pass (profiles/), if measured")
+                    help="HBM bytes per launch from a rocprofv3 PMC pass; default: the committed "
+                         "profiles/*/pmc_traffic.json entry for the kernel that runs, if any")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -145,6 +163,10 @@ def main() -> None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, kern_ms = float(t[0]), float(t[1])
 
+    traffic, traffic_src = args.traffic, None
+    if traffic is None:
+        traffic, traffic_src = committed_traffic(k, m, nobj, blen)
+
     total_bytes = world * nobj * blen * args.steps
     value = total_bytes / elapsed / 2 ** 30
     abytes = nobj * algo_bytes_per_block(k, m, blen)
@@ -170,7 +192,8 @@ def main() -> None:
                        "kernel_path": "specialised" if fast == 1 else "generic"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": args.traffic,
+                         "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "kernel_ms": round(kern_ms, 4),
                          "algo_bytes_per_launch": abytes},
         }

@@ -115,9 +115,9 @@ def main() -> None:
                          "profiles/*/pmc_traffic.json entry for the kernel that runs, if any")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from zs3server_amd.dist import max_over_ranks, object_range, rank_env
+
+    world, rank, local = rank_env()
     if world > 1:
         dist.init_process_group("gloo")  # control only: barrier + max of timings
     torch.cuda.set_device(local)
@@ -131,7 +131,8 @@ def main() -> None:
     codec = z.Codec(k, m, blen)
     buf = torch.empty(nobj * stride, dtype=torch.uint8, device=dev)
     sums = torch.empty(nobj * (k + m) * 32, dtype=torch.uint8, device=dev)
-    z.fill_batch(buf, stride, blen, nobj, seed=1234, obj0=rank * nobj)
+    obj_lo, _ = object_range(rank, nobj)  # disjoint object ids per rank
+    z.fill_batch(buf, stride, blen, nobj, seed=1234, obj0=obj_lo)
     torch.cuda.synchronize()
 
     def step():
@@ -158,10 +159,7 @@ def main() -> None:
     kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
     fast = z.last_path()
 
-    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, kern_ms = float(t[0]), float(t[1])
+    elapsed, kern_ms = max_over_ranks([elapsed, kern_ms], world)
 
     traffic, traffic_src = args.traffic, None
     if traffic is None:

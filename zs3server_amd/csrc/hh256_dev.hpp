@@ -163,4 +163,122 @@ __device__ __forceinline__ uint64_t hh_finalize256(HHLane& s, int lane, uint32_t
     return a_lo ^ (a_hi << 1) ^ (a_hi << 2);
 }
 
+// ---------------------------------------------------------------------------
+// Pair form: one chain per PAIR of threads, each thread owning the HH lane pair
+// (2h, 2h+1) that ZipperMergeAndAdd mixes, so an Update needs no cross-lane move.
+// With A = lane 2h+1 and B = lane 2h (C reference ZipperMergeAndAdd(v1=A, v0=B)):
+//   addB = [B3 A4 B2 B5 | A6 B1 A7 B0],  addA = [A3 B4 A2 A5 | A1 B6 A0 B7]
+// X = [A4 B5 B4 A5] (one v_perm of A.hi, B.hi) feeds both low dwords: 5 v_perm per
+// zipper for two lanes instead of 6.
+struct HHPair {
+    uint64_t v0[2], v1[2], mul0[2], mul1[2];  // [0] = lane 2h (B), [1] = lane 2h+1 (A)
+};
+
+__device__ __forceinline__ void zipper_pair(uint64_t A, uint64_t B, uint64_t& addA, uint64_t& addB) {
+    const uint32_t alo = (uint32_t)A, ahi = (uint32_t)(A >> 32);
+    const uint32_t blo = (uint32_t)B, bhi = (uint32_t)(B >> 32);
+    const uint32_t X = __builtin_amdgcn_perm(ahi, bhi, 0x05000104u);
+    const uint32_t b_lo = __builtin_amdgcn_perm(X, blo, 0x05020403u);
+    const uint32_t a_lo = __builtin_amdgcn_perm(X, alo, 0x07020603u);
+    const uint32_t b_hi = __builtin_amdgcn_perm(ahi, blo, 0x00070106u);
+    const uint32_t a_hi = __builtin_amdgcn_perm(bhi, alo, 0x07000601u);
+    addA = ((uint64_t)a_hi << 32) | a_lo;
+    addB = ((uint64_t)b_hi << 32) | b_lo;
+}
+
+__device__ __forceinline__ void hh2_update(HHPair& s, uint64_t w0, uint64_t w1) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const uint64_t w = i ? w1 : w0;
+        s.v1[i] = add64(s.v1[i], add64(s.mul0[i], w));
+        s.mul0[i] ^= (uint64_t)(uint32_t)s.v1[i] * (s.v0[i] >> 32);
+        s.v0[i] = add64(s.v0[i], s.mul1[i]);
+        s.mul1[i] ^= (uint64_t)(uint32_t)s.v0[i] * (s.v1[i] >> 32);
+    }
+    uint64_t aA, aB;
+    zipper_pair(s.v1[1], s.v1[0], aA, aB);
+    s.v0[1] = add64(s.v0[1], aA);
+    s.v0[0] = add64(s.v0[0], aB);
+    zipper_pair(s.v0[1], s.v0[0], aA, aB);
+    s.v1[1] = add64(s.v1[1], aA);
+    s.v1[0] = add64(s.v1[0], aB);
+}
+
+__device__ __forceinline__ HHPair hh2_init(int h, uint64_t k0, uint64_t k1, uint64_t k2, uint64_t k3) {
+    HHPair s;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const HHLane l = hh_init(2 * h + i, k0, k1, k2, k3);
+        s.v0[i] = l.v0;
+        s.v1[i] = l.v1;
+        s.mul0[i] = l.mul0;
+        s.mul1[i] = l.mul1;
+    }
+    return s;
+}
+
+// Full packets of a row in LDS (16-byte aligned); this thread reads its 16 bytes.
+__device__ __forceinline__ void hh2_packets(HHPair& s, const uint8_t* row, int npk, int h) {
+    const uint4* p = reinterpret_cast<const uint4*>(row) + h;
+    if (npk <= 0) return;
+    uint4 w = p[0];
+    for (int i = 1; i < npk; ++i) {
+        const uint4 nxt = p[2 * i];
+        hh2_update(s, ((uint64_t)w.y << 32) | w.x, ((uint64_t)w.w << 32) | w.z);
+        w = nxt;
+    }
+    hh2_update(s, ((uint64_t)w.y << 32) | w.x, ((uint64_t)w.w << 32) | w.z);
+}
+
+// HighwayHashUpdateRemainder (n = 1..31 bytes at tail) for the lanes 2h, 2h+1.
+__device__ __forceinline__ void hh2_remainder(HHPair& s, const uint8_t* tail, uint32_t n, int h) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        s.v0[i] += ((uint64_t)n << 32) + n;
+        s.v1[i] = ((uint64_t)rotl32((uint32_t)(s.v1[i] >> 32), n) << 32) | rotl32((uint32_t)s.v1[i], n);
+    }
+    const uint32_t remain = n & ~3u, mod4 = n & 3u;
+    uint8_t b[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const uint32_t idx = 16u * h + i;
+        b[i] = idx < remain ? tail[idx] : 0;
+    }
+    if (n & 16u) {
+        if (h == 1) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) b[12 + i] = tail[n - 4 + i];
+        }
+    } else if (mod4) {
+        if (h == 1) {
+            b[0] = tail[remain];
+            b[1] = tail[remain + (mod4 >> 1)];
+            b[2] = tail[n - 1];
+        }
+    }
+    uint64_t w0 = 0, w1 = 0;
+#pragma unroll
+    for (int i = 7; i >= 0; --i) {
+        w0 = (w0 << 8) | b[i];
+        w1 = (w1 << 8) | b[8 + i];
+    }
+    hh2_update(s, w0, w1);
+}
+
+// Finalize-256.  Returns this thread's 16 digest bytes (h[2h], h[2h+1]).
+__device__ __forceinline__ void hh2_finalize256(HHPair& s, uint64_t& d0, uint64_t& d1) {
+    for (int r = 0; r < 10; ++r) {
+        // permuted[l] = rot32(v0[(l + 2) & 3]): lanes 2h, 2h+1 take the partner's v0
+        const uint32_t p0lo = dpp_xor1((uint32_t)s.v0[0]), p0hi = dpp_xor1((uint32_t)(s.v0[0] >> 32));
+        const uint32_t p1lo = dpp_xor1((uint32_t)s.v0[1]), p1hi = dpp_xor1((uint32_t)(s.v0[1] >> 32));
+        hh2_update(s, ((uint64_t)p0lo << 32) | p0hi, ((uint64_t)p1lo << 32) | p1hi);
+    }
+    const uint64_t a3 = (s.v1[1] + s.mul1[1]) & 0x3FFFFFFFFFFFFFFFULL;
+    const uint64_t a2 = s.v1[0] + s.mul1[0];
+    const uint64_t a1 = s.v0[1] + s.mul0[1];
+    const uint64_t a0 = s.v0[0] + s.mul0[0];
+    d1 = a1 ^ ((a3 << 1) | (a2 >> 63)) ^ ((a3 << 2) | (a2 >> 62));
+    d0 = a0 ^ (a2 << 1) ^ (a2 << 2);
+}
+
 }  // namespace zs3dev

@@ -115,7 +115,8 @@ __device__ __forceinline__ void stcol(uint8_t* p, const Col<NWd>& v) {
     __builtin_memcpy(p, &v, 4 * NWd);
 }
 
-template <int K, int M, int G, int T, int NBUF, int NT, int CW, int PF, bool NTL, bool STAMP = false, int DYB = 0>
+template <int K, int M, int G, int T, int NBUF, int NT, int CW, int PF, bool NTL, bool STAMP = false, int DYB = 0,
+          bool PAIR = false>
 __global__ void __launch_bounds__(NT) k_encode_hash(EncArgs a) {
     constexpr int R = K + M;
     constexpr int NWd = CW / 4;
@@ -135,12 +136,13 @@ __global__ void __launch_bounds__(NT) k_encode_hash(EncArgs a) {
 
     for (int i = tid; i < NTAB; i += NT) tabs[i] = DYB ? a.dtables[i] : a.tables[i];
 
-    // ---- hash-chain role: quad = one shard row of one stripe
-    const int chain = tid >> 2, lane = tid & 3;
+    // ---- hash-chain role: one shard row of one stripe per quad (PAIR: per thread pair)
+    const int chain = PAIR ? (tid >> 1) : (tid >> 2), lane = PAIR ? (tid & 1) : (tid & 3);
     const bool chain_live = chain < G * R && (blk0 + chain / R) < a.n_blocks;
     const int crow = chain < G * R ? chain : 0;
     const uint32_t sel = zipper_sel(lane);
     HHLane st = hh_init(lane, a.key[0], a.key[1], a.key[2], a.key[3]);
+    HHPair st2 = hh2_init(lane & 1, a.key[0], a.key[1], a.key[2], a.key[3]);
 
     // ---- encode role: CPT columns per thread.  Dead stripes of the last workgroup
     // alias the last live block and store byte-identical parity (benign), so the
@@ -244,8 +246,13 @@ __global__ void __launch_bounds__(NT) k_encode_hash(EncArgs a) {
         lds_barrier();
         const uint64_t s3 = stamp();
         const uint8_t* row = tl + crow * TS;
-        hh_packets(st, row, L >> 5, lane, sel);
-        if (t0 + L >= S && (L & 31)) hh_remainder(st, row + (L & ~31), (uint32_t)(L & 31), lane, sel);
+        if constexpr (PAIR) {
+            hh2_packets(st2, row, L >> 5, lane);
+            if (t0 + L >= S && (L & 31)) hh2_remainder(st2, row + (L & ~31), (uint32_t)(L & 31), lane);
+        } else {
+            hh_packets(st, row, L >> 5, lane, sel);
+            if (t0 + L >= S && (L & 31)) hh_remainder(st, row + (L & ~31), (uint32_t)(L & 31), lane, sel);
+        }
         const uint64_t s4 = stamp();
         if (NBUF == 1) lds_barrier();
         const uint64_t s5 = stamp();
@@ -265,12 +272,24 @@ __global__ void __launch_bounds__(NT) k_encode_hash(EncArgs a) {
             if (tp < S) step(xs[p], tp, it++);
         }
     }
-    const uint64_t h = hh_finalize256(st, lane, sel);
-    if (chain_live) {
-        const int64_t b = blk0 + chain / R;
-        const int s = chain % R;
-        uint8_t* out = a.sums + (b * R + s) * 32 + 8 * lane;
-        *reinterpret_cast<uint64_t*>(out) = h;
+    if constexpr (PAIR) {
+        uint64_t d0, d1;
+        hh2_finalize256(st2, d0, d1);
+        if (chain_live) {
+            const int64_t b = blk0 + chain / R;
+            const int s = chain % R;
+            uint64_t* out = reinterpret_cast<uint64_t*>(a.sums + (b * R + s) * 32 + 16 * lane);
+            out[0] = d0;
+            out[1] = d1;
+        }
+    } else {
+        const uint64_t h = hh_finalize256(st, lane, sel);
+        if (chain_live) {
+            const int64_t b = blk0 + chain / R;
+            const int s = chain % R;
+            uint8_t* out = a.sums + (b * R + s) * 32 + 8 * lane;
+            *reinterpret_cast<uint64_t*>(out) = h;
+        }
     }
     if constexpr (STAMP) {
         if ((tid & 63) == 0 && a.dbg) {
@@ -779,6 +798,35 @@ static void launch_pipe(const EncArgs& a, hipStream_t s) {
     }
 }
 
+// Pair-form fused kernel: 2 threads per hash chain, G = stripes so 2*G*R fills whole
+// wavefronts (RS(8+4): G = 8, 192 threads).
+template <int R>
+constexpr int pick_G2() {
+    int g = 32 / gcd_c(R, 32);
+    while (g > 1 && 2 * g * R > 512) g /= 2;
+    while (2 * g * R < 192) g *= 2;
+    return g;
+}
+
+template <int K, int M, int T, int NBUF, int CW, bool STAMP = false>
+static void launch_pair(const EncArgs& a, hipStream_t s) {
+    constexpr int R = K + M;
+    constexpr int G = pick_G2<R>();
+    constexpr int NT = round64(2 * G * R);
+    static_assert(T % CW == 0 && T % 32 == 0, "tile");
+    const int64_t grid = (a.n_blocks + G - 1) / G;
+    constexpr bool CAN_DY = (M == 2 || M == 4) && K % M == 0;
+    if constexpr (CAN_DY) {
+        if (a.dyb == M) {
+            hipLaunchKernelGGL((k_encode_hash<K, M, G, T, NBUF, NT, CW, 1, false, STAMP, M, true>), dim3((unsigned)grid),
+                               dim3(NT), 0, s, a);
+            return;
+        }
+    }
+    hipLaunchKernelGGL((k_encode_hash<K, M, G, T, NBUF, NT, CW, 1, false, STAMP, 0, true>), dim3((unsigned)grid),
+                       dim3(NT), 0, s, a);
+}
+
 static int env_variant() {
     static int v = -2;
     if (v == -2) {
@@ -815,6 +863,11 @@ static bool launch_variant(int v, const EncArgs& a, hipStream_t s) {
         case 22: launch_pipe<K, M, G, 256, 8>(a, s); return true;
         case 23: launch_pipe<K, M, G, 320, 8>(a, s); return true;
         case 120: launch_pipe<K, M, G, 384, 8, true>(a, s); return true;
+        case 30: launch_pair<K, M, 384, 1, 16>(a, s); return true;
+        case 31: launch_pair<K, M, 384, 2, 16>(a, s); return true;
+        case 32: launch_pair<K, M, 192, 2, 8>(a, s); return true;
+        case 33: launch_pair<K, M, 256, 1, 16>(a, s); return true;
+        case 34: launch_pair<K, M, 192, 1, 8>(a, s); return true;
         case 101: launch_fused<K, M, G, 384, 1, 8, 1, false, true>(a, s); return true;
         case 102: launch_fused<K, M, G, 256, 2, 16, 1, false, true>(a, s); return true;
         default: return false;

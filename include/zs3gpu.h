@@ -148,6 +148,20 @@ int zs3_decode_data_blocks(const zs3_codec* c, uint8_t* h_shards, int64_t shard_
 /* HighwayHash-256 of one host message (key NULL = bitrot magic key). */
 int zs3_hh256(const uint8_t* h_key, const uint8_t* h_msg, int64_t len, uint8_t* h_out32);
 
+/* End-to-end streaming encode (BASELINE config 5): an object of
+ * total_len host bytes (the PUT stream, erasure-encode.go:83-111 block loop) is cut
+ * into block_size blocks; each block is Split + Encoded and all k+m shard chunks are
+ * HighwayHash-256 summed on the device.  The pipeline double-buffers batches of
+ * batch_blocks blocks: pageable -> pinned staging (host threads) -> H2D -> fused
+ * kernel -> D2H, on separate streams.  Outputs (host):
+ *   h_parity: block b parity row r at h_parity + b*m*S + r*S (S = ShardSize; the
+ *             last partial block uses its own S' = ceil(len/k), rows still at m*S)
+ *   h_sums:   block b shard i sum at h_sums + (b*(k+m) + i)*32
+ * Data shards are the input bytes themselves (zero-padded for the last block), as
+ * Split's in-place views.  Returns the number of blocks or an error. */
+int64_t zs3_stream_encode(const zs3_codec* c, const uint8_t* h_src, int64_t total_len,
+                          uint8_t* h_parity, uint8_t* h_sums, int64_t batch_blocks);
+
 /* Startup self-tests through the device path: erasureSelfTest
  * (erasure-coding.go:158-216, 60 (k, m) xxhash64 KATs + shard-0 rebuild) and
  * bitrotSelfTest (bitrot.go:218-249).  Returns ZS3_OK or ZS3_ERR_FILE_CORRUPT. */

@@ -1,0 +1,88 @@
+"""Secondary measurements: reconstruct (BASELINE config 3),
+hash-only and verify (GET path), and the end-to-end host->device->host stream
+(config 5, PCIe-inclusive).  Prints one JSON line per measurement."""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import zs3server_amd as z  # noqa: E402
+
+
+def timeit(fn, steps=10):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(steps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / steps
+
+
+def out(**kw):
+    print(json.dumps(kw), flush=True)
+
+
+# ---- config 3: RS(8+4) 4096 x 1 MiB encode, then reconstruct with 2 erased
+k, m, blen, nobj = 8, 4, 1 << 20, 4096
+S = blen // k
+stride = (k + m) * S
+codec = z.Codec(k, m)
+buf = torch.empty(nobj * stride, dtype=torch.uint8, device="cuda")
+z.fill_batch(buf, stride, blen, nobj, seed=3)
+codec.encode_batch(buf, stride, blen, nobj, parity=buf, parity_offset=k * S, parity_stride=stride)
+torch.cuda.synchronize()
+for erased, data_only, label in (([0, 5], True, "ReconstructData, data shards 0+5 erased"),
+                                 ([2, 10], False, "Reconstruct, 1 data + 1 parity erased")):
+    pres = [i not in erased for i in range(k + m)]
+    ms = timeit(lambda: codec.reconstruct_batch(buf, stride, S, nobj, pres, data_only))
+    ab = nobj * (k * S + len(erased) * S)
+    out(path="reconstruct", shape="RS(8+4)", objects=nobj, what=label, ms=round(ms, 4),
+        GiBps_object=round(nobj * blen / ms / 1e-3 / 2**30, 1), hbm_GBps=round(ab / ms / 1e6, 1),
+        hbm_frac=round(ab / ms / 1e6 / 8000, 3))
+
+# ---- GET-side hash-only and verify over all 12 shards of every stripe
+sums = torch.empty(nobj * (k + m) * 32, dtype=torch.uint8, device="cuda")
+ms = timeit(lambda: z.hh256_batch(buf, S, S, nobj * (k + m), sums))
+out(path="hh256_batch", msgs=nobj * (k + m), msg_len=S, ms=round(ms, 4),
+    hbm_GBps=round(nobj * (k + m) * S / ms / 1e6, 1))
+bad = torch.empty(nobj * (k + m), dtype=torch.int32, device="cuda")
+ms = timeit(lambda: z.hh256_verify_batch(buf, S, S, nobj * (k + m), sums, bad))
+out(path="hh256_verify_batch", msgs=nobj * (k + m), msg_len=S, ms=round(ms, 4),
+    hbm_GBps=round(nobj * (k + m) * S / ms / 1e6, 1), bad=int(bad.sum()))
+del buf, sums, bad
+torch.cuda.empty_cache()
+
+# ---- config 5: end-to-end stream incl. pinned / pageable host buffers and PCIe
+gib = float(os.environ.get("E2E_GIB", "10"))
+for (k, m) in ((16, 4), (8, 4)):
+    bs = 1 << 20
+    total = int(gib * (1 << 30))
+    nblk = total // bs
+    S = bs // k
+    codec = z.Codec(k, m, bs)
+    for pinned in (True, False):
+        if pinned:
+            src, par, sums = z.HostBuffer(total), z.HostBuffer(nblk * m * S), z.HostBuffer(nblk * (k + m) * 32)
+            src.array[:] = 7
+        else:
+            src = np.full(total, 7, dtype=np.uint8)
+            par = np.zeros(nblk * m * S, np.uint8)
+            sums = np.zeros(nblk * (k + m) * 32, np.uint8)
+        codec.stream_encode(src, 64 * bs, par, sums, batch_blocks=64)  # warm
+        t0 = time.perf_counter()
+        codec.stream_encode(src, total, par, sums, batch_blocks=512)
+        dt = time.perf_counter() - t0
+        out(path="stream_encode_e2e", shape=f"RS({k}+{m})", GiB=gib, host_buffers="pinned" if pinned else "pageable",
+            seconds=round(dt, 3), GiBps=round(total / dt / 2**30, 2),
+            pcie_GBps=round((total + nblk * (m * S + 32 * (k + m))) / dt / 1e9, 1))
+        if pinned:
+            for x in (src, par, sums):
+                x.free()
+        del src, par, sums

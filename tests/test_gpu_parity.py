@@ -298,3 +298,40 @@ def test_full_size_rs84_properties(oracle):
         assert torch.equal(d, ref), erased
     del d, ref, sums, sums2
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("k,m,bs,nfull,tail,batch,pinned", [
+    (4, 2, 1 << 16, 5, 1000, 2, False), (8, 4, 1 << 16, 7, 0, 3, True), (16, 4, 1 << 16, 3, 17, 8, False),
+    (8, 4, 1 << 20, 4, (1 << 19) + 3, 2, True),
+])
+def test_stream_encode_end_to_end(oracle, k, m, bs, nfull, tail, batch, pinned):
+    """zs3_stream_encode: host stream -> H2D -> fused kernel -> D2H, multiple
+    double-buffered batches plus a partial last block (erasure-encode.go:83-111)."""
+    codec = z.Codec(k, m, bs)
+    total = nfull * bs + tail
+    S = -(-bs // k)
+    nblk = nfull + (1 if tail else 0)
+    data = np.concatenate([oracle.fill(31, b, bs) for b in range(nblk)])[:total]
+    bufs = []
+    if pinned:
+        src = z.HostBuffer(max(total, 1))
+        src.array[:total] = data
+        par = z.HostBuffer(nblk * m * S)
+        sums = z.HostBuffer(nblk * (k + m) * 32)
+        bufs = [src, par, sums]
+        par_a, sums_a = par.array, sums.array
+    else:
+        src, par_a, sums_a = data.copy(), np.zeros(nblk * m * S, np.uint8), np.zeros(nblk * (k + m) * 32, np.uint8)
+        par, sums = par_a, sums_a
+    assert codec.stream_encode(src, total, par, sums, batch_blocks=batch) == nblk
+    mat = oracle.build_matrix(k, m)
+    for b in range(nblk):
+        blk = data[b * bs: min((b + 1) * bs, total)]
+        want = oracle.encode_data(k, m, blk, mat)
+        Sb = want.shape[1]
+        got_p = par_a[b * m * S: b * m * S + m * Sb].reshape(m, Sb)
+        assert np.array_equal(got_p, want[k:]), b
+        assert np.array_equal(sums_a[b * (k + m) * 32:(b + 1) * (k + m) * 32].reshape(k + m, 32),
+                              oracle.hh256_rows(KEY, want)), b
+    for x in bufs:
+        x.free()

@@ -40,6 +40,7 @@ EXPORTS = [
     "zs3_shard_file_size", "zs3_shard_file_offset", "zs3_bitrot_shard_file_size",
     "zs3_encode_batch", "zs3_reconstruct_batch", "zs3_hh256_batch", "zs3_hh256_verify_batch",
     "zs3_fill_batch", "zs3_encode_data", "zs3_decode_data_blocks", "zs3_hh256", "zs3_selftest",
+    "zs3_stream_encode",
     "zs3_last_path", "zs3_debug_set_variant", "zs3_debug_set_buffer",
 ]
 
@@ -89,6 +90,10 @@ def lib():
     L.zs3_hh256.argtypes = [vp, vp, i64, vp]
     L.zs3_device_count.argtypes = [C.POINTER(C.c_int)]
     L.zs3_set_device.argtypes = [C.c_int]
+    L.zs3_stream_encode.argtypes = [vp, vp, i64, vp, vp, i64]
+    L.zs3_stream_encode.restype = i64
+    L.zs3_host_alloc.argtypes = [C.POINTER(vp), C.c_size_t]
+    L.zs3_host_free.argtypes = [vp]
     _L = L
     return L
 
@@ -183,11 +188,36 @@ class Codec:
         _check(S, "EncodeData")
         return S, (out.reshape(self.k + self.m, 32) if sums else None)
 
+    def stream_encode(self, src, total_len: int, parity, sums, batch_blocks: int = 256) -> int:
+        """End-to-end host stream: returns the number of blocks (zs3_stream_encode).
+        src/parity/sums are host buffers (numpy arrays or pinned HostBuffer)."""
+        def addr(x):
+            return x.ptr if isinstance(x, HostBuffer) else x.ctypes.data
+        n = lib().zs3_stream_encode(self._h, addr(src), total_len, addr(parity), addr(sums), batch_blocks)
+        return _check(n, "stream_encode")
+
     def decode_data_blocks(self, shards, present, data_only: bool) -> None:
         """Reconstruct in place on a (k+m, S) C-contiguous numpy uint8 array."""
         pres = (C.c_uint8 * (self.k + self.m))(*[1 if p else 0 for p in present])
         _check(lib().zs3_decode_data_blocks(self._h, shards.ctypes.data, shards.shape[1], pres,
                                             1 if data_only else 0), "DecodeDataBlocks")
+
+
+class HostBuffer:
+    """Pinned host memory from zs3_host_alloc (the pinned-bpool backing, §8f.2)."""
+
+    def __init__(self, nbytes: int):
+        import numpy as np
+        p = C.c_void_p()
+        _check(lib().zs3_host_alloc(C.byref(p), nbytes), "host_alloc")
+        self.ptr = p.value
+        self.nbytes = nbytes
+        self.array = np.ctypeslib.as_array((C.c_uint8 * nbytes).from_address(self.ptr))
+
+    def free(self):
+        if self.ptr:
+            lib().zs3_host_free(self.ptr)
+            self.ptr = None
 
 
 def bitrot_shard_file_size(size: int, shard_size: int) -> int:

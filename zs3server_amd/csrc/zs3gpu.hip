@@ -14,6 +14,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/zs3gpu.h"
@@ -609,6 +610,151 @@ int zs3_hh256(const uint8_t* key, const uint8_t* msg, int64_t len, uint8_t* out3
     if (rc) return rc;
     std::memcpy(out32, st->h + mb, 32);
     return ZS3_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+// Parallel memcpy for pageable <-> pinned staging (one PCIe Gen5 x16 link needs
+// more than one CPU core of memcpy bandwidth).
+void par_memcpy(uint8_t* dst, const uint8_t* src, size_t n, int threads) {
+    if (n < (8u << 20) || threads <= 1) {
+        std::memcpy(dst, src, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    const size_t per = ((n + threads - 1) / threads + 4095) & ~(size_t)4095;
+    for (int t = 0; t < threads; ++t) {
+        const size_t lo = (size_t)t * per;
+        if (lo >= n) break;
+        const size_t len = std::min(per, n - lo);
+        th.emplace_back([=] { std::memcpy(dst + lo, src + lo, len); });
+    }
+    for (auto& x : th) x.join();
+}
+
+bool is_pinned(const void* p) {
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return attr.type == hipMemoryTypeHost;
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t zs3_stream_encode(const zs3_codec* cc, const uint8_t* src, int64_t total_len, uint8_t* h_parity,
+                          uint8_t* h_sums, int64_t batch_blocks) {
+    zs3_codec* c = const_cast<zs3_codec*>(cc);
+    if (!c || total_len < 0 || batch_blocks <= 0 || (total_len > 0 && (!src || !h_parity || !h_sums)))
+        return ZS3_ERR_INVALID_ARG;
+    if (total_len == 0) return 0;
+    const int k = c->k, m = c->m, R = k + m;
+    const int64_t B = c->block_size;
+    const int64_t S = ceil_frac(B, k);
+    const int64_t nfull = total_len / B;
+    const int64_t tail = total_len % B;
+    const int64_t nblocks = nfull + (tail ? 1 : 0);
+    const int64_t stride = (int64_t)R * S;
+    const int64_t NB = batch_blocks;
+    const bool src_pinned = is_pinned(src);
+    const bool out_pinned = is_pinned(h_parity) && is_pinned(h_sums);
+    const int cpu_threads = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+
+    struct Slot {
+        uint8_t* d = nullptr;      // NB stripes [k*S data | m*S parity] + sums
+        uint8_t* hin = nullptr;    // pinned input staging
+        uint8_t* hout = nullptr;   // pinned parity+sums staging
+        hipEvent_t done_out = nullptr;
+        int64_t b0 = -1, nb = 0;
+    };
+    Slot sl[2];
+    hipStream_t s_in, s_comp, s_out;
+    int rc = ZS3_OK;
+    auto chk = [&](hipError_t e) {
+        if (e != hipSuccess && rc == ZS3_OK) rc = map_hip(e);
+        return e == hipSuccess;
+    };
+    chk(hipStreamCreateWithFlags(&s_in, hipStreamNonBlocking));
+    chk(hipStreamCreateWithFlags(&s_comp, hipStreamNonBlocking));
+    chk(hipStreamCreateWithFlags(&s_out, hipStreamNonBlocking));
+    const size_t dbytes = (size_t)NB * stride + (size_t)NB * R * 32;
+    const size_t obytes = (size_t)NB * m * S + (size_t)NB * R * 32;
+    for (auto& x : sl) {
+        chk(hipMalloc(&x.d, dbytes));
+        if (!src_pinned) chk(hipHostMalloc(&x.hin, (size_t)NB * B, hipHostMallocDefault));
+        if (!out_pinned) chk(hipHostMalloc(&x.hout, obytes, hipHostMallocDefault));
+        chk(hipEventCreateWithFlags(&x.done_out, hipEventDisableTiming));
+    }
+    // copy the finished outputs of a slot back to the caller's buffers (pageable case)
+    auto drain = [&](Slot& x) {
+        if (x.b0 < 0) return;
+        chk(hipEventSynchronize(x.done_out));
+        if (!out_pinned) {
+            par_memcpy(h_parity + x.b0 * m * S, x.hout, (size_t)x.nb * m * S, cpu_threads);
+            std::memcpy(h_sums + x.b0 * R * 32, x.hout + (size_t)NB * m * S, (size_t)x.nb * R * 32);
+        }
+        x.b0 = -1;
+    };
+    hipEvent_t ev_in, ev_comp;
+    chk(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
+    chk(hipEventCreateWithFlags(&ev_comp, hipEventDisableTiming));
+    for (int64_t b0 = 0, it = 0; b0 < nfull && rc == ZS3_OK; b0 += NB, ++it) {
+        Slot& x = sl[it & 1];
+        drain(x);  // slot reuse: its previous batch must be out
+        const int64_t nb = std::min(NB, nfull - b0);
+        const uint8_t* in = src + b0 * B;
+        if (!src_pinned) {
+            par_memcpy(x.hin, in, (size_t)nb * B, cpu_threads);
+            in = x.hin;
+        }
+        // H2D into the in-place stripe layout (row pitch (k+m)*S)
+        chk(hipMemcpy2DAsync(x.d, (size_t)stride, in, (size_t)B, (size_t)B, (size_t)nb, hipMemcpyHostToDevice, s_in));
+        chk(hipEventRecord(ev_in, s_in));
+        chk(hipStreamWaitEvent(s_comp, ev_in, 0));
+        uint8_t* dsums = x.d + (size_t)NB * stride;
+        rc = zs3_encode_batch(c, x.d, stride, B, nb, x.d + (size_t)k * S, stride, dsums, s_comp);
+        chk(hipEventRecord(ev_comp, s_comp));
+        chk(hipStreamWaitEvent(s_out, ev_comp, 0));
+        uint8_t* po = out_pinned ? h_parity + b0 * m * S : x.hout;
+        uint8_t* so = out_pinned ? h_sums + b0 * R * 32 : x.hout + (size_t)NB * m * S;
+        chk(hipMemcpy2DAsync(po, (size_t)m * S, x.d + (size_t)k * S, (size_t)stride, (size_t)m * S, (size_t)nb,
+                             hipMemcpyDeviceToHost, s_out));
+        chk(hipMemcpyAsync(so, dsums, (size_t)nb * R * 32, hipMemcpyDeviceToHost, s_out));
+        chk(hipEventRecord(x.done_out, s_out));
+        x.b0 = b0;
+        x.nb = nb;
+    }
+    for (auto& x : sl) drain(x);
+    if (rc == ZS3_OK && tail) {
+        // last partial block: EncodeData on its own shard size (erasure-encode.go:85-96)
+        std::vector<uint8_t> buf((size_t)R * ceil_frac(tail, k), 0);
+        std::memcpy(buf.data(), src + nfull * B, (size_t)tail);
+        uint8_t sums[32 * 256];
+        const int64_t St = zs3_encode_data(c, buf.data(), tail, (int64_t)buf.size(), sums);
+        if (St < 0) {
+            rc = (int)St;
+        } else {
+            std::memcpy(h_parity + nfull * m * S, buf.data() + (size_t)k * St, (size_t)m * St);
+            std::memcpy(h_sums + nfull * R * 32, sums, (size_t)R * 32);
+        }
+    }
+    for (auto& x : sl) {
+        if (x.d) (void)hipFree(x.d);
+        if (x.hin) (void)hipHostFree(x.hin);
+        if (x.hout) (void)hipHostFree(x.hout);
+        if (x.done_out) (void)hipEventDestroy(x.done_out);
+    }
+    (void)hipEventDestroy(ev_in);
+    (void)hipEventDestroy(ev_comp);
+    (void)hipStreamDestroy(s_in);
+    (void)hipStreamDestroy(s_comp);
+    (void)hipStreamDestroy(s_out);
+    return rc == ZS3_OK ? nblocks : rc;
 }
 
 int zs3_selftest(void) {

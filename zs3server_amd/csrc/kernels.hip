@@ -681,41 +681,69 @@ __global__ void __launch_bounds__(256) k_reconstruct_generic(RecArgs a) {
 // HighwayHash-256 of n messages (64 chains = 256 threads per workgroup), with
 // optional compare against expected digests (streamingBitrotReader.ReadAt,
 // cmd/bitrot-streaming.go:180-186: per-shard errFileCorrupt, not whole-batch).
+// Double-buffered: the next tile's 16-byte pieces are loaded into registers while
+// the current tile is hashed from LDS, so HBM latency overlaps the hash chain.
 constexpr int HB_CH = 64;
 constexpr int HB_T = 256;
 constexpr int HB_TS = HB_T + 32;
+constexpr int HB_PPT = HB_CH * (HB_T / 16) / 256;  // 16-byte pieces per thread per tile
 
 __global__ void __launch_bounds__(256) k_hash_batch(HashArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t tile[HB_CH * HB_TS];
+    __shared__ __attribute__((aligned(16))) uint8_t tile[2][HB_CH * HB_TS];
     const int tid = threadIdx.x;
     const int64_t m0 = (int64_t)blockIdx.x * HB_CH;
     const int chain = tid >> 2, lane = tid & 3;
     const uint32_t sel = zipper_sel(lane);
     HHLane st = hh_init(lane, a.key[0], a.key[1], a.key[2], a.key[3]);
     const int64_t len = a.len;
-    for (int64_t t0 = 0; t0 < len; t0 += HB_T) {
+    const int64_t ntile = (len + HB_T - 1) / HB_T;
+    uint4 v[HB_PPT];
+    auto load = [&](int64_t t0) {
         const int L = (int)((len - t0) < HB_T ? (len - t0) : HB_T);
-        // coalesced staging: 16-byte pieces, row-major
-        for (int i = tid; i < HB_CH * (HB_T / 16); i += 256) {
+#pragma unroll
+        for (int q = 0; q < HB_PPT; ++q) {
+            const int i = tid + q * 256;
             const int r = i / (HB_T / 16), o = (i % (HB_T / 16)) * 16;
             const int64_t msg = m0 + r;
+            v[q] = make_uint4(0, 0, 0, 0);
             if (msg < a.n && o < L) {
                 const uint8_t* src = a.msgs + msg * a.stride + t0 + o;
-                uint4 v;
                 if (o + 16 <= L) {
-                    v = ld16(src);
+                    v[q] = ld16(src);
                 } else {
                     uint8_t tb[16] = {0};
-                    for (int q = 0; q < L - o; ++q) tb[q] = src[q];
-                    __builtin_memcpy(&v, tb, 16);
+                    for (int z = 0; z < L - o; ++z) tb[z] = src[z];
+                    __builtin_memcpy(&v[q], tb, 16);
                 }
-                *reinterpret_cast<uint4*>(tile + r * HB_TS + o) = v;
             }
         }
-        lds_barrier();
-        const uint8_t* row = tile + chain * HB_TS;
+    };
+    auto stash = [&](uint8_t* tl) {
+#pragma unroll
+        for (int q = 0; q < HB_PPT; ++q) {
+            const int i = tid + q * 256;
+            const int r = i / (HB_T / 16), o = (i % (HB_T / 16)) * 16;
+            *reinterpret_cast<uint4*>(tl + r * HB_TS + o) = v[q];
+        }
+    };
+    if (ntile > 0) {
+        load(0);
+        stash(tile[0]);
+        if (ntile > 1) load(HB_T);
+    }
+    lds_barrier();
+    for (int64_t t = 0; t < ntile; ++t) {
+        const int64_t t0 = t * HB_T;
+        const int L = (int)((len - t0) < HB_T ? (len - t0) : HB_T);
+        uint8_t* cur = tile[t & 1];
+        // stash tile t+1 (registers) into the other buffer, then prefetch t+2
+        if (t + 1 < ntile) {
+            stash(tile[(t + 1) & 1]);
+            if (t + 2 < ntile) load(t0 + 2 * HB_T);
+        }
+        const uint8_t* row = cur + chain * HB_TS;
         hh_packets(st, row, L >> 5, lane, sel);
-        if (t0 + L >= len && (L & 31)) hh_remainder(st, row + (L & ~31), (uint32_t)(L & 31), lane, sel);
+        if (t + 1 >= ntile && (L & 31)) hh_remainder(st, row + (L & ~31), (uint32_t)(L & 31), lane, sel);
         lds_barrier();
     }
     const uint64_t h = hh_finalize256(st, lane, sel);

@@ -115,8 +115,10 @@ __device__ __forceinline__ void stcol(uint8_t* p, const Col<NWd>& v) {
     __builtin_memcpy(p, &v, 4 * NWd);
 }
 
+// ABL (diagnostics, timing only): 1 = skip the hash phase, 2 = skip the GF arithmetic
+// (parity rows = data row 0; loads, LDS and stores unchanged).
 template <int K, int M, int G, int T, int NBUF, int NT, int CW, int PF, bool NTL, bool STAMP = false, int DYB = 0,
-          bool PAIR = false>
+          bool PAIR = false, int ABL = 0>
 __global__ void __launch_bounds__(NT) k_encode_hash(EncArgs a) {
     constexpr int R = K + M;
     constexpr int NWd = CW / 4;
@@ -175,7 +177,12 @@ __global__ void __launch_bounds__(NT) k_encode_hash(EncArgs a) {
             const int64_t b = (blk0 + g) < a.n_blocks ? (blk0 + g) : (a.n_blocks - 1);
             if (o >= L) continue;
             Col<NWd> par[M];
-            if constexpr (DYB != 0) {
+            if constexpr (ABL == 2) {
+#pragma unroll
+                for (int r = 0; r < M; ++r) par[r] = x[c][r];
+#pragma unroll
+                for (int j = 0; j < K; ++j) stcol<NWd>(tl + (g * R + j) * TS + o, x[c][j]);
+            } else if constexpr (DYB != 0) {
                 encode_dyadic<NWd, K, M>(x[c], par, dtabs);
 #pragma unroll
                 for (int j = 0; j < K; ++j) stcol<NWd>(tl + (g * R + j) * TS + o, x[c][j]);
@@ -246,7 +253,8 @@ __global__ void __launch_bounds__(NT) k_encode_hash(EncArgs a) {
         lds_barrier();
         const uint64_t s3 = stamp();
         const uint8_t* row = tl + crow * TS;
-        if constexpr (PAIR) {
+        if constexpr (ABL == 1) {
+        } else if constexpr (PAIR) {
             hh2_packets(st2, row, L >> 5, lane);
             if (t0 + L >= S && (L & 31)) hh2_remainder(st2, row + (L & ~31), (uint32_t)(L & 31), lane);
         } else {
@@ -855,6 +863,17 @@ static void launch_pair(const EncArgs& a, hipStream_t s) {
                        dim3(NT), 0, s, a);
 }
 
+template <int K, int M, int ABL>
+static void launch_ablation(const EncArgs& a, hipStream_t s) {
+    constexpr int R = K + M;
+    constexpr int G = pick_G<R>();
+    constexpr int NT = round64(4 * G * R);
+    const int64_t grid = (a.n_blocks + G - 1) / G;
+    constexpr int DY = ((M == 2 || M == 4) && K % M == 0) ? M : 0;
+    hipLaunchKernelGGL((k_encode_hash<K, M, G, 384, 1, NT, 8, 1, false, false, DY, false, ABL>), dim3((unsigned)grid),
+                       dim3(NT), 0, s, a);
+}
+
 static int env_variant() {
     static int v = -2;
     if (v == -2) {
@@ -896,6 +915,8 @@ static bool launch_variant(int v, const EncArgs& a, hipStream_t s) {
         case 32: launch_pair<K, M, 192, 2, 8>(a, s); return true;
         case 33: launch_pair<K, M, 256, 1, 16>(a, s); return true;
         case 34: launch_pair<K, M, 192, 1, 8>(a, s); return true;
+        case 41: launch_ablation<K, M, 1>(a, s); return true;
+        case 42: launch_ablation<K, M, 2>(a, s); return true;
         case 101: launch_fused<K, M, G, 384, 1, 8, 1, false, true>(a, s); return true;
         case 102: launch_fused<K, M, G, 256, 2, 16, 1, false, true>(a, s); return true;
         default: return false;

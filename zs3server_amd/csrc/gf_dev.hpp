@@ -106,6 +106,17 @@ __device__ __forceinline__ Nib nib_xor(const Nib& x, const Nib& y) {
 
 __device__ __forceinline__ uint32_t fold3(const Prod3& p) { return xor3(p.a, p.b, p.c); }
 
+// XOR of N terms with ceil((N-1)/2) v_bitop3 (the last one a plain XOR if N is even).
+template <int N>
+__device__ __forceinline__ uint32_t fold_terms(const uint32_t (&t)[N]) {
+    uint32_t acc = t[0];
+    int i = 1;
+#pragma unroll
+    for (; i + 1 < N; i += 2) acc = xor3(acc, t[i], t[i + 1]);
+    if (i < N) acc ^= t[i];
+    return acc;
+}
+
 // An SGPR zero the compiler cannot see through: indexing the LDS coefficient
 // tables with it keeps their loads where they are used instead of hoisting every
 // table into VGPRs (which would cap occupancy).
@@ -115,68 +126,83 @@ __device__ __forceinline__ int opaque_zero() {
     return z;
 }
 
-// Dyadic encode (parity block = K/M blocks [[A,B],[B,A]]; see zs3gpu.hip).
-// M = 4, per block with generator (a,b,c,d) and inputs x0..x3:
-//   T = a.x0 + b.x1 + c.x2 + d.x3,  R = (a+b)(x0+x1) + (c+d)(x2+x3)
-//   UV = (a+c)(x0+x2) + (b+d)(x1+x3),  W = (a+b+c+d)(x0+x1+x2+x3)
-//   y0 = T, y1 = T+R, y2 = T+UV, y3 = T+R+UV+W          (9 multiplies, not 16)
-// M = 2: y0 = a.x0 + b.x1, y1 = y0 + (a+b)(x0+x1)      (3 multiplies, not 4)
-// Nibble splits are GF(2)-linear, so the split of a sum is the XOR of splits.
+// Dyadic encode.  The parity block is K/M blocks D_q[r ^ t] (see zs3gpu.hip), i.e.
+// y = sum_q A_q * x_q in the group algebra GF(256)[Z2^2] (M = 4) or GF(256)[Z2]
+// (M = 2).  In characteristic 2 that algebra is the local ring F[s,t]/(s^2,t^2)
+// with s = 1+g1, t = 1+g2; in the basis {1, s, t, st} a product is
+//   Y0 = A0 X0,  Y1 = A0 X1 + A1 X0,  Y2 = A0 X2 + A2 X0,
+//   Y3 = A0 X3 + A1 X2 + A2 X1 + A3 X0                       (9 multiplies)
+// with X = (x0+x1+x2+x3, x1+x3, x2+x3, x3) and, per block generator (a,b,c,d),
+// A = (a+b+c+d, b+d, c+d, d).  Only the 4 transformed inputs are nibble-split (the
+// Karatsuba form needed 9 split combinations) and each block has 4 coefficient
+// tables, not 9.  The Y accumulate over blocks and convert back once:
+//   y0 = Y0+Y1+Y2+Y3, y1 = Y1+Y3, y2 = Y2+Y3, y3 = Y3.
+// M = 2: X = (x0+x1, x1), A = (a+b, b), Y0 = A0 X0, Y1 = A0 X1 + A1 X0,
+// y0 = Y0+Y1, y1 = Y1.
 template <int NWd, int K, int M>
 __device__ __forceinline__ void encode_dyadic(const Col<NWd> (&x)[K], Col<NWd> (&out)[M], const uint32_t* dtabs) {
     static_assert(M == 2 || M == 4, "dyadic block");
-    constexpr int PER = M == 4 ? 9 : 3;
-    uint32_t acc[M][NWd];
-#pragma unroll
-    for (int r = 0; r < M; ++r)
-#pragma unroll
-        for (int w = 0; w < NWd; ++w) acc[r][w] = 0;
+    uint32_t Y[M][NWd];
 #pragma unroll
     for (int q = 0; q < K / M; ++q) {
         __builtin_amdgcn_sched_barrier(0);
-        const uint32_t* tq = dtabs + opaque_zero() + q * PER * 8;
-        CoefTab t[PER];
+        const uint32_t* tq = dtabs + opaque_zero() + q * M * 8;
+        CoefTab t[M];
 #pragma unroll
-        for (int i = 0; i < PER; ++i) t[i] = load_coef(tq, i);
+        for (int i = 0; i < M; ++i) t[i] = load_coef(tq, i);
 #pragma unroll
         for (int w = 0; w < NWd; ++w) {
             if constexpr (M == 4) {
-                const Nib n0 = split_nibbles(x[4 * q + 0].w[w]), n1 = split_nibbles(x[4 * q + 1].w[w]);
-                const Nib n2 = split_nibbles(x[4 * q + 2].w[w]), n3 = split_nibbles(x[4 * q + 3].w[w]);
-                const Nib d01 = nib_xor(n0, n1), d23 = nib_xor(n2, n3);
-                const Nib s0 = nib_xor(n0, n2), s1 = nib_xor(n1, n3), s01 = nib_xor(s0, s1);
-                const Prod3 P = gf_lookup(n0, t[0]), Q = gf_lookup(n1, t[1]);
-                const Prod3 P2 = gf_lookup(n2, t[3]), Q2 = gf_lookup(n3, t[4]);
-                const Prod3 R1 = gf_lookup(d01, t[2]), R2 = gf_lookup(d23, t[5]);
-                const Prod3 U = gf_lookup(s0, t[6]), V = gf_lookup(s1, t[7]);
-                const Prod3 W = gf_lookup(s01, t[8]);
-                uint32_t T = xor3(P.a, P.b, P.c);
-                T = xor3(T, Q.a, Q.b);
-                T = xor3(T, Q.c, P2.a);
-                T = xor3(T, P2.b, P2.c);
-                T = xor3(T, Q2.a, Q2.b);
-                T = T ^ Q2.c;
-                const uint32_t R = xor3(fold3(R1), R2.a, R2.b) ^ R2.c;
-                const uint32_t UV = xor3(fold3(U), V.a, V.b) ^ V.c;
-                const uint32_t Wv = fold3(W);
-                acc[0][w] ^= T;
-                acc[1][w] = xor3(acc[1][w], T, R);
-                acc[2][w] = xor3(acc[2][w], T, UV);
-                acc[3][w] = xor3(acc[3][w], xor3(T, R, UV), Wv);
+                const uint32_t x3 = x[4 * q + 3].w[w];
+                const uint32_t X1 = x[4 * q + 1].w[w] ^ x3, X2 = x[4 * q + 2].w[w] ^ x3;
+                const uint32_t X0 = xor3(x[4 * q + 0].w[w], X1, x[4 * q + 2].w[w]);
+                const Nib n0 = split_nibbles(X0), n1 = split_nibbles(X1);
+                const Nib n2 = split_nibbles(X2), n3 = split_nibbles(x3);
+                const Prod3 P00 = gf_lookup(n0, t[0]), P01 = gf_lookup(n1, t[0]);
+                const Prod3 P02 = gf_lookup(n2, t[0]), P03 = gf_lookup(n3, t[0]);
+                const Prod3 P10 = gf_lookup(n0, t[1]), P12 = gf_lookup(n2, t[1]);
+                const Prod3 P20 = gf_lookup(n0, t[2]), P21 = gf_lookup(n1, t[2]);
+                const Prod3 P30 = gf_lookup(n0, t[3]);
+                if (q == 0) {
+                    Y[0][w] = fold_terms<3>({P00.a, P00.b, P00.c});
+                    Y[1][w] = fold_terms<6>({P01.a, P01.b, P01.c, P10.a, P10.b, P10.c});
+                    Y[2][w] = fold_terms<6>({P02.a, P02.b, P02.c, P20.a, P20.b, P20.c});
+                    Y[3][w] = fold_terms<12>({P03.a, P03.b, P03.c, P12.a, P12.b, P12.c,
+                                              P21.a, P21.b, P21.c, P30.a, P30.b, P30.c});
+                } else {
+                    Y[0][w] = fold_terms<4>({Y[0][w], P00.a, P00.b, P00.c});
+                    Y[1][w] = fold_terms<7>({Y[1][w], P01.a, P01.b, P01.c, P10.a, P10.b, P10.c});
+                    Y[2][w] = fold_terms<7>({Y[2][w], P02.a, P02.b, P02.c, P20.a, P20.b, P20.c});
+                    Y[3][w] = fold_terms<13>({Y[3][w], P03.a, P03.b, P03.c, P12.a, P12.b, P12.c,
+                                              P21.a, P21.b, P21.c, P30.a, P30.b, P30.c});
+                }
             } else {
-                const Nib n0 = split_nibbles(x[2 * q + 0].w[w]), n1 = split_nibbles(x[2 * q + 1].w[w]);
-                const Nib d01 = nib_xor(n0, n1);
-                const Prod3 P = gf_lookup(n0, t[0]), Q = gf_lookup(n1, t[1]), R = gf_lookup(d01, t[2]);
-                const uint32_t PQ = xor3(fold3(P), Q.a, Q.b) ^ Q.c;
-                acc[0][w] ^= PQ;
-                acc[1][w] = xor3(acc[1][w], PQ, fold3(R));
+                const uint32_t x1 = x[2 * q + 1].w[w];
+                const uint32_t X0 = x[2 * q + 0].w[w] ^ x1;
+                const Nib n0 = split_nibbles(X0), n1 = split_nibbles(x1);
+                const Prod3 P00 = gf_lookup(n0, t[0]), P01 = gf_lookup(n1, t[0]), P10 = gf_lookup(n0, t[1]);
+                if (q == 0) {
+                    Y[0][w] = fold_terms<3>({P00.a, P00.b, P00.c});
+                    Y[1][w] = fold_terms<6>({P01.a, P01.b, P01.c, P10.a, P10.b, P10.c});
+                } else {
+                    Y[0][w] = fold_terms<4>({Y[0][w], P00.a, P00.b, P00.c});
+                    Y[1][w] = fold_terms<7>({Y[1][w], P01.a, P01.b, P01.c, P10.a, P10.b, P10.c});
+                }
             }
         }
     }
 #pragma unroll
-    for (int r = 0; r < M; ++r)
-#pragma unroll
-        for (int w = 0; w < NWd; ++w) out[r].w[w] = acc[r][w];
+    for (int w = 0; w < NWd; ++w) {
+        if constexpr (M == 4) {
+            out[0].w[w] = xor3(Y[0][w], Y[1][w], Y[2][w]) ^ Y[3][w];
+            out[1].w[w] = Y[1][w] ^ Y[3][w];
+            out[2].w[w] = Y[2][w] ^ Y[3][w];
+            out[3].w[w] = Y[3][w];
+        } else {
+            out[0].w[w] = Y[0][w] ^ Y[1][w];
+            out[1].w[w] = Y[1][w];
+        }
+    }
 }
 
 // Scalar GF multiply with log/exp tables (generic byte path).

@@ -106,6 +106,22 @@ __device__ __forceinline__ void hh_packets(HHLane& s, const uint8_t* row, int np
     hh_update(s, w, sel_hi);
 }
 
+// Full-tile form: NPK (compile-time) packets, fully unrolled so every ds_read_b64
+// uses an immediate offset and the register rotation of the loop disappears.
+// Next-packet prefetch as above.
+template <int NPK>
+__device__ __forceinline__ void hh_packets_n(HHLane& s, const uint8_t* row, int lane, uint32_t sel_hi) {
+    const uint64_t* p = reinterpret_cast<const uint64_t*>(row) + lane;
+    uint64_t w = p[0];
+#pragma unroll
+    for (int i = 1; i < NPK; ++i) {
+        const uint64_t nxt = p[4 * i];
+        hh_update(s, w, sel_hi);
+        w = nxt;
+    }
+    hh_update(s, w, sel_hi);
+}
+
 __device__ __forceinline__ uint32_t rotl32(uint32_t x, uint32_t n) {
     return __builtin_amdgcn_alignbit(x, x, 32u - n);  // n in 1..31
 }

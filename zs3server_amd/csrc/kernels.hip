@@ -127,7 +127,7 @@ __global__ void __launch_bounds__(NT) k_encode_hash(EncArgs a) {
     constexpr int NCOL = G * CPB;
     constexpr int CPT = (NCOL + NT - 1) / NT;
 
-    constexpr int NTAB = DYB ? (K / M) * (M == 4 ? 9 : 3) * 8 : M * K * 8;
+    constexpr int NTAB = DYB ? K * 8 : M * K * 8;
     __shared__ __attribute__((aligned(16))) uint8_t tile[NBUF][G * R * TS];
     __shared__ __attribute__((aligned(16))) uint32_t tabs[NTAB];
     const uint32_t* dtabs = tabs;
@@ -258,7 +258,10 @@ __global__ void __launch_bounds__(NT) k_encode_hash(EncArgs a) {
             hh2_packets(st2, row, L >> 5, lane);
             if (t0 + L >= S && (L & 31)) hh2_remainder(st2, row + (L & ~31), (uint32_t)(L & 31), lane);
         } else {
-            hh_packets(st, row, L >> 5, lane, sel);
+            if (L == T)
+                hh_packets_n<T / 32>(st, row, lane, sel);
+            else
+                hh_packets(st, row, L >> 5, lane, sel);
             if (t0 + L >= S && (L & 31)) hh_remainder(st, row + (L & ~31), (uint32_t)(L & 31), lane, sel);
         }
         const uint64_t s4 = stamp();
@@ -324,7 +327,7 @@ __global__ void __launch_bounds__(NT) k_encode_hash_pipe(EncArgs a) {
     constexpr int NPK = T / 32;
     static_assert(NCOL <= NT, "one column per thread");
 
-    constexpr int NTAB = DYB ? (K / M) * (M == 4 ? 9 : 3) * 8 : M * K * 8;
+    constexpr int NTAB = DYB ? K * 8 : M * K * 8;
     __shared__ __attribute__((aligned(16))) uint8_t tile[2][G * R * TS];
     __shared__ __attribute__((aligned(16))) uint32_t tabs[NTAB];
     const uint32_t* dtabs = tabs;

@@ -380,8 +380,8 @@ int zs3_codec_new(int k, int m, int64_t block_size, zs3_codec** out) {
             zs3::perm_tables(c->matrix[(size_t)(k + r) * k + j], &c->tables[((size_t)r * k + j) * 8]);
     // Dyadic structure: the Vandermonde points 0..k+m-1 make the parity block of the
     // power-of-two shapes (4+2, 8+4, 16+4, ...) dyadic in m x m blocks,
-    // P[r][q*m + t] = D_q[r ^ t], so each block is [[A,B],[B,A]] and a Karatsuba
-    // split needs 3 (m = 2) or 9 (m = 4) GF multiplies instead of m*m.
+    // P[r][q*m + t] = D_q[r ^ t], so each block is a group-algebra product that
+    // needs 3 (m = 2) or 9 (m = 4) GF multiplies instead of m*m (gf_dev.hpp).
     if ((m == 2 || m == 4) && k % m == 0) {
         bool dy = true;
         for (int r = 0; r < m && dy; ++r)
@@ -392,18 +392,16 @@ int zs3_codec_new(int k, int m, int64_t block_size, zs3_codec** out) {
         if (dy) {
             c->dyb = m;
             c->dyadic_off = c->tables.size();
-            const int per = m == 4 ? 9 : 3;
+            const int per = m;  // local-ring coefficients per block (gf_dev.hpp encode_dyadic)
             c->tables.resize(c->tables.size() + (size_t)(k / m) * per * 8, 0);
             for (int q = 0; q < k / m; ++q) {
                 const uint8_t* D = &c->matrix[(size_t)k * k + q * m];
-                uint8_t co[9];
+                uint8_t co[4];
                 if (m == 2) {
-                    co[0] = D[0]; co[1] = D[1]; co[2] = D[0] ^ D[1];
+                    co[0] = D[0] ^ D[1]; co[1] = D[1];
                 } else {
                     const uint8_t a = D[0], b = D[1], cc = D[2], d = D[3];
-                    co[0] = a; co[1] = b; co[2] = a ^ b;
-                    co[3] = cc; co[4] = d; co[5] = cc ^ d;
-                    co[6] = a ^ cc; co[7] = b ^ d; co[8] = a ^ b ^ cc ^ d;
+                    co[0] = a ^ b ^ cc ^ d; co[1] = b ^ d; co[2] = cc ^ d; co[3] = d;
                 }
                 for (int i = 0; i < per; ++i)
                     zs3::perm_tables(co[i], &c->tables[c->dyadic_off + ((size_t)q * per + i) * 8]);

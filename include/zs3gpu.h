@@ -113,6 +113,24 @@ int zs3_reconstruct_batch(const zs3_codec* c, uint8_t* d_shards, int64_t block_s
                           int64_t shard_len, int64_t n_blocks, const uint8_t* h_present,
                           int data_only, void* stream);
 
+/* zs3_verify_reconstruct_batch: the GET / heal pass in one kernel.
+ *   For every block: the k survivor shards the decode reads (the first k present,
+ *   as ReconstructData picks them, erasure-coding.go:108) are HighwayHash-256'd and
+ *   compared with their stored bitrot sums d_expect[b][i][32] (the 32-byte hash
+ *   streamingBitrotReader.ReadAt checks, bitrot-streaming.go:171-186); then the missing
+ *   shards (data only, or all with data_only == 0) are rebuilt in place from the same
+ *   reads.  d_bad[b][i] (k+m int32 per block, zeroed first) = 1 where survivor i failed
+ *   verification: that is the per-shard errFileCorrupt of erasure-decode.go:165-179,
+ *   and the rebuilt shards of that block are then invalid — re-issue the block with
+ *   shard i marked missing (parallelReader reads the next shard).  With d_sums_out
+ *   != NULL the rebuilt shards are hashed too (heal: erasure-healing.go writes them
+ *   through a new bitrot writer), digest at d_sums_out[b][i][32].  Nothing missing ->
+ *   verify only.  Errors as zs3_reconstruct_batch. */
+int zs3_verify_reconstruct_batch(const zs3_codec* c, uint8_t* d_shards, int64_t block_stride,
+                                 int64_t shard_len, int64_t n_blocks, const uint8_t* h_present,
+                                 int data_only, const uint8_t* d_expect, int32_t* d_bad,
+                                 uint8_t* d_sums_out, void* stream);
+
 /* HighwayHash-256 of n_msgs messages of msg_len bytes at d_msgs + i*msg_stride
  * (key = 32 bytes, NULL = the bitrot magic key).  Digest i at d_sums + 32*i. */
 int zs3_hh256_batch(const uint8_t* h_key, const uint8_t* d_msgs, int64_t msg_stride,

@@ -47,8 +47,25 @@ for erased, data_only, label in (([0, 5], True, "ReconstructData, data shards 0+
         GiBps_object=round(nobj * blen / ms / 1e-3 / 2**30, 1), hbm_GBps=round(ab / ms / 1e6, 1),
         hbm_frac=round(ab / ms / 1e6 / 8000, 3))
 
-# ---- GET-side hash-only and verify over all 12 shards of every stripe
+# ---- GET / heal fused pass (zs3_verify_reconstruct_batch): verify the k survivors
+# against stored sums and rebuild the missing shards; heal also hashes the rebuilt rows
 sums = torch.empty(nobj * (k + m) * 32, dtype=torch.uint8, device="cuda")
+codec.encode_batch(buf, stride, blen, nobj, parity=buf, parity_offset=k * S, parity_stride=stride, sums=sums)
+vbad = torch.empty(nobj * (k + m), dtype=torch.int32, device="cuda")
+hsum = torch.empty_like(sums)
+for erased, data_only, heal, label in (([], True, False, "GET, all data shards present: verify 8"),
+                                       ([0, 5], True, False, "GET, data 0+5 lost: verify 8 + rebuild 2"),
+                                       ([2, 10], False, True, "heal 1 data + 1 parity: verify 8, rebuild+hash 2")):
+    pres = [i not in erased for i in range(k + m)]
+    ms = timeit(lambda: codec.verify_reconstruct_batch(buf, stride, S, nobj, pres, data_only, sums, vbad,
+                                                       sums_out=hsum if heal else None))
+    e = len(erased)
+    ab = nobj * (k * S + e * S + 32 * k + (32 * e if heal else 0))
+    out(path="verify_reconstruct", shape="RS(8+4)", objects=nobj, what=label, ms=round(ms, 4),
+        GiBps_object=round(nobj * blen / ms / 1e-3 / 2**30, 1), hbm_GBps=round(ab / ms / 1e6, 1),
+        hbm_frac=round(ab / ms / 1e6 / 8000, 3), bad=int(vbad.sum()))
+
+# ---- GET-side hash-only and verify over all 12 shards of every stripe
 ms = timeit(lambda: z.hh256_batch(buf, S, S, nobj * (k + m), sums))
 out(path="hh256_batch", msgs=nobj * (k + m), msg_len=S, ms=round(ms, 4),
     hbm_GBps=round(nobj * (k + m) * S / ms / 1e6, 1))

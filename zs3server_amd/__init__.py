@@ -38,7 +38,8 @@ EXPORTS = [
     "zs3_dev_free", "zs3_host_alloc", "zs3_host_free", "zs3_memcpy_h2d", "zs3_memcpy_d2h",
     "zs3_stream_sync", "zs3_codec_new", "zs3_codec_free", "zs3_codec_matrix", "zs3_shard_size",
     "zs3_shard_file_size", "zs3_shard_file_offset", "zs3_bitrot_shard_file_size",
-    "zs3_encode_batch", "zs3_reconstruct_batch", "zs3_hh256_batch", "zs3_hh256_verify_batch",
+    "zs3_encode_batch", "zs3_reconstruct_batch", "zs3_verify_reconstruct_batch", "zs3_hh256_batch",
+    "zs3_hh256_verify_batch",
     "zs3_fill_batch", "zs3_encode_data", "zs3_decode_data_blocks", "zs3_hh256", "zs3_selftest",
     "zs3_stream_encode",
     "zs3_last_path", "zs3_debug_set_variant", "zs3_debug_set_buffer",
@@ -81,6 +82,7 @@ def lib():
     L.zs3_bitrot_shard_file_size.restype = i64
     L.zs3_encode_batch.argtypes = [vp, vp, i64, i64, i64, vp, i64, vp, vp]
     L.zs3_reconstruct_batch.argtypes = [vp, vp, i64, i64, i64, u8p, C.c_int, vp]
+    L.zs3_verify_reconstruct_batch.argtypes = [vp, vp, i64, i64, i64, u8p, C.c_int, vp, vp, vp, vp]
     L.zs3_hh256_batch.argtypes = [vp, vp, i64, i64, i64, vp, vp]
     L.zs3_hh256_verify_batch.argtypes = [vp, vp, i64, i64, i64, vp, vp, vp]
     L.zs3_fill_batch.argtypes = [vp, i64, i64, i64, C.c_uint64, C.c_uint64, vp]
@@ -175,6 +177,18 @@ class Codec:
         pres = (C.c_uint8 * (self.k + self.m))(*[1 if p else 0 for p in present])
         _check(lib().zs3_reconstruct_batch(self._h, _ptr(shards, offset), block_stride, shard_len, n_blocks,
                                            pres, 1 if data_only else 0, _stream(stream)), "reconstruct_batch")
+
+    def verify_reconstruct_batch(self, shards, block_stride: int, shard_len: int, n_blocks: int, present,
+                                 data_only: bool, expect, bad, sums_out=None, stream=None,
+                                 offset: int = 0) -> None:
+        """GET / heal pass (zs3_verify_reconstruct_batch): verify the k survivors
+        against `expect` ([n][k+m][32] device), flag failures in `bad` ([n][k+m]
+        int32 device), rebuild the missing shards in place, optionally hash them
+        into `sums_out`."""
+        pres = (C.c_uint8 * (self.k + self.m))(*[1 if p else 0 for p in present])
+        _check(lib().zs3_verify_reconstruct_batch(self._h, _ptr(shards, offset), block_stride, shard_len,
+                                                  n_blocks, pres, 1 if data_only else 0, _ptr(expect), _ptr(bad),
+                                                  _ptr(sums_out), _stream(stream)), "verify_reconstruct_batch")
 
     # ---- host-pointer calls ----
     def encode_data(self, buf, length: int, sums: bool = False):

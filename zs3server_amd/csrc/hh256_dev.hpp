@@ -246,6 +246,19 @@ __device__ __forceinline__ void hh2_packets(HHPair& s, const uint8_t* row, int n
     hh2_update(s, ((uint64_t)w.y << 32) | w.x, ((uint64_t)w.w << 32) | w.z);
 }
 
+template <int NPK>
+__device__ __forceinline__ void hh2_packets_n(HHPair& s, const uint8_t* row, int h) {
+    const uint4* p = reinterpret_cast<const uint4*>(row) + h;
+    uint4 w = p[0];
+#pragma unroll
+    for (int i = 1; i < NPK; ++i) {
+        const uint4 nxt = p[2 * i];
+        hh2_update(s, ((uint64_t)w.y << 32) | w.x, ((uint64_t)w.w << 32) | w.z);
+        w = nxt;
+    }
+    hh2_update(s, ((uint64_t)w.y << 32) | w.x, ((uint64_t)w.w << 32) | w.z);
+}
+
 // HighwayHashUpdateRemainder (n = 1..31 bytes at tail) for the lanes 2h, 2h+1.
 __device__ __forceinline__ void hh2_remainder(HHPair& s, const uint8_t* tail, uint32_t n, int h) {
 #pragma unroll

@@ -255,7 +255,10 @@ __global__ void __launch_bounds__(NT) k_encode_hash(EncArgs a) {
         const uint8_t* row = tl + crow * TS;
         if constexpr (ABL == 1) {
         } else if constexpr (PAIR) {
-            hh2_packets(st2, row, L >> 5, lane);
+            if (L == T)
+                hh2_packets_n<T / 32>(st2, row, lane);
+            else
+                hh2_packets(st2, row, L >> 5, lane);
             if (t0 + L >= S && (L & 31)) hh2_remainder(st2, row + (L & ~31), (uint32_t)(L & 31), lane);
         } else {
             if (L == T)
@@ -722,9 +725,11 @@ __global__ void __launch_bounds__(256) k_hash_batch(HashArgs a) {
                 if (o + 16 <= L) {
                     v[q] = ld16(src);
                 } else {
-                    uint8_t tb[16] = {0};
-                    for (int z = 0; z < L - o; ++z) tb[z] = src[z];
-                    __builtin_memcpy(&v[q], tb, 16);
+                    uint32_t w4[4] = {0, 0, 0, 0};
+#pragma unroll
+                    for (int z = 0; z < 16; ++z)
+                        if (z < L - o) w4[z >> 2] |= (uint32_t)src[z] << (8 * (z & 3));
+                    v[q] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
                 }
             }
         }
@@ -753,20 +758,132 @@ __global__ void __launch_bounds__(256) k_hash_batch(HashArgs a) {
             if (t + 2 < ntile) load(t0 + 2 * HB_T);
         }
         const uint8_t* row = cur + chain * HB_TS;
-        hh_packets(st, row, L >> 5, lane, sel);
+        if (L == HB_T)
+            hh_packets_n<HB_T / 32>(st, row, lane, sel);
+        else
+            hh_packets(st, row, L >> 5, lane, sel);
         if (t + 1 >= ntile && (L & 31)) hh_remainder(st, row + (L & ~31), (uint32_t)(L & 31), lane, sel);
         lds_barrier();
     }
     const uint64_t h = hh_finalize256(st, lane, sel);
     const int64_t msg = m0 + chain;
     if (msg < a.n) {
-        if (a.sums) *reinterpret_cast<uint64_t*>(a.sums + msg * 32 + 8 * lane) = h;
+        const int64_t ss = a.sum_stride ? a.sum_stride : 32, bs = a.bad_stride ? a.bad_stride : 1;
+        if (a.sums) *reinterpret_cast<uint64_t*>(a.sums + msg * ss + 8 * lane) = h;
         if (a.expect && a.bad) {
             uint64_t want;
-            __builtin_memcpy(&want, a.expect + msg * 32 + 8 * lane, 8);
+            __builtin_memcpy(&want, a.expect + msg * ss + 8 * lane, 8);
             const unsigned long long mism = __ballot(want != h);
             const unsigned q = (unsigned)((mism >> (tid & 60)) & 0xFull);
-            if (lane == 0) a.bad[msg] = q ? 1 : 0;
+            if (lane == 0) a.bad[msg * bs] = q ? 1 : 0;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// GET / heal fused pass: per stripe, the k survivor rows the decode
+// reads (ReconstructData's first k present shards, erasure-coding.go:108) are hashed
+// and compared with their stored bitrot sums (streamingBitrotReader.ReadAt,
+// bitrot-streaming.go:171-186: per-shard errFileCorrupt), and the e missing rows are
+// rebuilt from the same registers (one HBM read of each survivor).  HOUT also hashes
+// the rebuilt rows so a heal can write them with fresh sums (erasure-healing.go).
+// Layout as k_encode_hash: G stripes per workgroup, T-byte tiles, each thread one
+// CW-byte column, survivors (+ rebuilt rows) staged in LDS, one quad per hashed row.
+template <int K, int EMAX, bool HOUT>
+struct VrShape {
+    static constexpr int RH = K + (HOUT ? EMAX : 0);  // hashed rows per stripe
+    static constexpr int G = (256 / (4 * RH)) > 0 ? 256 / (4 * RH) : 1;
+    static constexpr int NT = round64(4 * G * RH);
+    static constexpr int T = 256, CW = 8;
+};
+
+template <int K, int EMAX, bool HOUT>
+__global__ void __launch_bounds__((VrShape<K, EMAX, HOUT>::NT)) k_verify_reconstruct(VrArgs a) {
+    using Sh = VrShape<K, EMAX, HOUT>;
+    constexpr int RH = Sh::RH, G = Sh::G, NT = Sh::NT, T = Sh::T, CW = Sh::CW;
+    constexpr int NWd = CW / 4, TS = T + 32, CPB = T / CW, NCOL = G * CPB;
+    constexpr int CPT = (NCOL + NT - 1) / NT;
+    __shared__ __attribute__((aligned(16))) uint8_t tile[G * RH * TS];
+    __shared__ __attribute__((aligned(16))) uint32_t tabs[(EMAX > 0 ? EMAX : 1) * K * 8];
+    __shared__ int32_t srows[K + EMAX];
+    const int tid = threadIdx.x;
+    const int E = a.e;
+    for (int i = tid; i < E * K * 8; i += NT) tabs[i] = a.tables[i];
+    for (int i = tid; i < K + E; i += NT) srows[i] = a.rows[i];
+    const int64_t S = a.S;
+    const int64_t blk0 = (int64_t)blockIdx.x * G;
+    const int R = a.k + a.m;
+    const int chain = tid >> 2, lane = tid & 3;
+    const int cj = chain % RH;
+    const bool chain_live = chain < G * RH && (blk0 + chain / RH) < a.n_blocks && (cj < K || cj - K < E);
+    const int crow = chain < G * RH ? chain : 0;
+    const uint32_t sel = zipper_sel(lane);
+    HHLane st = hh_init(lane, a.key[0], a.key[1], a.key[2], a.key[3]);
+    lds_barrier();
+    int64_t roff[K];  // survivor row offsets (wave-uniform)
+#pragma unroll
+    for (int j = 0; j < K; ++j) roff[j] = (int64_t)__builtin_amdgcn_readfirstlane(srows[j]) * S;
+    for (int64_t t0 = 0; t0 < S; t0 += T) {
+        const int L = (int)((S - t0) < T ? (S - t0) : T);
+#pragma unroll
+        for (int c = 0; c < CPT; ++c) {
+            const int col = tid + c * NT;
+            if (col >= NCOL) continue;
+            const int g = col / CPB;
+            const int o = (col % CPB) * CW;
+            if (o >= L) continue;
+            const int64_t b = (blk0 + g) < a.n_blocks ? (blk0 + g) : (a.n_blocks - 1);
+            uint8_t* blk = a.shards + b * a.block_stride + t0 + o;
+            Col<NWd> x[K];
+#pragma unroll
+            for (int j = 0; j < K; ++j) x[j] = ldcol<NWd>(blk + roff[j]);
+#pragma unroll
+            for (int j = 0; j < K; ++j) stcol<NWd>(tile + (g * RH + j) * TS + o, x[j]);
+            if constexpr (EMAX > 0) {
+                const uint32_t* tb = tabs + opaque_zero();
+#pragma unroll
+                for (int r = 0; r < EMAX; ++r) {
+                    if (r < E) {
+                        GfAcc acc[NWd];
+#pragma unroll
+                        for (int w = 0; w < NWd; ++w) acc_init(acc[w]);
+#pragma unroll
+                        for (int j = 0; j < K; ++j) {
+                            const CoefTab t = load_coef(tb, r * K + j);
+#pragma unroll
+                            for (int w = 0; w < NWd; ++w) acc_add(acc[w], gf_lookup(split_nibbles(x[j].w[w]), t));
+                        }
+                        Col<NWd> y;
+#pragma unroll
+                        for (int w = 0; w < NWd; ++w) y.w[w] = acc_done(acc[w]);
+                        const int64_t orow = (int64_t)__builtin_amdgcn_readfirstlane(srows[K + r]);
+                        stcol<NWd>(blk + orow * S, y);
+                        if constexpr (HOUT) stcol<NWd>(tile + (g * RH + K + r) * TS + o, y);
+                    }
+                }
+            }
+        }
+        lds_barrier();
+        const uint8_t* row = tile + crow * TS;
+        if (L == T)
+            hh_packets_n<T / 32>(st, row, lane, sel);
+        else
+            hh_packets(st, row, L >> 5, lane, sel);
+        if (t0 + L >= S && (L & 31)) hh_remainder(st, row + (L & ~31), (uint32_t)(L & 31), lane, sel);
+        lds_barrier();
+    }
+    const uint64_t h = hh_finalize256(st, lane, sel);
+    if (chain_live) {
+        const int64_t b = blk0 + chain / RH;
+        const int64_t srow = srows[cj];
+        if (cj < K) {
+            uint64_t want;
+            __builtin_memcpy(&want, a.expect + (b * R + srow) * 32 + 8 * lane, 8);
+            const unsigned long long mism = __ballot(want != h);
+            const unsigned q = (unsigned)((mism >> (tid & 60)) & 0xFull);
+            if (lane == 0) a.bad[b * R + srow] = q ? 1 : 0;
+        } else if (a.sums_out) {
+            *reinterpret_cast<uint64_t*>(a.sums_out + (b * R + srow) * 32 + 8 * lane) = h;
         }
     }
 }
@@ -940,17 +1057,15 @@ static hipError_t run_encode_fast(const EncArgs& a, hipStream_t s) {
         }
         if (!done) {
             // Tuned defaults (scripts/sweep_variants.py on MI355X, profiles/r01):
-            // 8-byte columns so every thread encodes, one 384-byte tile per step,
-            // one LDS tile.  The dyadic (Karatsuba) encode wins for k <= 8; at
-            // k = 16 its extra live tables cost more occupancy than it saves.
-            if constexpr (G * R * (384 + 32) + M * K * 32 <= 40960) {
-                if constexpr (K > 8) {
-                    EncArgs b = a;
-                    b.dyb = 0;
-                    launch_fused<K, M, G, 384, 1, 8>(b, s);
-                } else {
-                    launch_fused<K, M, G, 384, 1, 8>(a, s);
-                }
+            // 8-byte columns so every thread encodes, one 384-byte tile per step.
+            // k <= 8: one LDS tile.  k > 8 (RS(16+4)): two LDS tiles, so the
+            // next tile's encode does not wait for the slower stripes' hashing.
+            constexpr bool DY2 = K > 8 && (M == 2 || M == 4) && K % M == 0 &&
+                                 2 * G * R * (384 + 32) + K * 32 <= 81920;
+            if (DY2 && a.dyb == M) {
+                if constexpr (DY2) launch_fused<K, M, G, 384, 2, 8>(a, s);
+            } else if constexpr (G * R * (384 + 32) + M * K * 32 <= 40960) {
+                launch_fused<K, M, G, 384, 1, 8>(a, s);
             } else {
                 launch_fused<K, M, G, T, NBUF, 16>(a, s);
             }
@@ -1038,6 +1153,90 @@ hipError_t launch_reconstruct(const RecArgs& a, hipStream_t s, bool* used_fast) 
     const unsigned gy = (unsigned)(a.n_blocks < 65535 ? a.n_blocks : 65535);
     hipLaunchKernelGGL(k_reconstruct_generic, dim3(gx < 1024 ? gx : 1024, gy), dim3(256), lds, s, a);
     return hipGetLastError();
+}
+
+template <int K, int EMAX, bool HOUT>
+static hipError_t run_vr(const VrArgs& a, hipStream_t s) {
+    using Sh = VrShape<K, EMAX, HOUT>;
+    const int64_t grid = (a.n_blocks + Sh::G - 1) / Sh::G;
+    hipLaunchKernelGGL((k_verify_reconstruct<K, EMAX, HOUT>), dim3((unsigned)grid), dim3(Sh::NT), 0, s, a);
+    return hipGetLastError();
+}
+
+template <int K>
+static hipError_t run_vr_k(const VrArgs& a, hipStream_t s) {
+    const bool hout = a.sums_out != nullptr;
+    if (a.e == 0) return run_vr<K, 0, false>(a, s);
+    if (a.e <= 2) return hout ? run_vr<K, 2, true>(a, s) : run_vr<K, 2, false>(a, s);
+    return hout ? run_vr<K, 4, true>(a, s) : run_vr<K, 4, false>(a, s);
+}
+
+hipError_t launch_verify_reconstruct(const VrArgs& a, hipStream_t s, bool* used_fast) {
+    if (a.n_blocks <= 0 || a.S <= 0) return hipSuccess;
+    if (a.e <= 4 && (a.S % 16) == 0) {
+        if (used_fast) *used_fast = true;
+        switch (a.k) {
+            case 2: return run_vr_k<2>(a, s);
+            case 4: return run_vr_k<4>(a, s);
+            case 6: return run_vr_k<6>(a, s);
+            case 8: return run_vr_k<8>(a, s);
+            case 10: return run_vr_k<10>(a, s);
+            case 12: return run_vr_k<12>(a, s);
+            case 16: return run_vr_k<16>(a, s);
+            default: break;
+        }
+    }
+    // Any other shape: one verify launch per survivor row, then the reconstruct
+    // kernel, then (heal) one hash launch per rebuilt row.
+    if (used_fast) *used_fast = false;
+    const int R = a.k + a.m;
+    int32_t rows[256];
+    if (hipMemcpyAsync(rows, a.rows, (size_t)(a.k + a.e) * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return hipGetLastError();
+    for (int j = 0; j < a.k; ++j) {
+        HashArgs h{};
+        h.msgs = a.shards + (int64_t)rows[j] * a.S;
+        h.stride = a.block_stride;
+        h.len = a.S;
+        h.n = a.n_blocks;
+        h.expect = a.expect + (int64_t)rows[j] * 32;
+        h.bad = a.bad + rows[j];
+        h.sum_stride = (int64_t)R * 32;
+        h.bad_stride = R;
+        for (int q = 0; q < 4; ++q) h.key[q] = a.key[q];
+        hipError_t e = launch_hash(h, s);
+        if (e != hipSuccess) return e;
+    }
+    if (a.e > 0) {
+        RecArgs r{};
+        r.shards = a.shards;
+        r.block_stride = a.block_stride;
+        r.S = a.S;
+        r.n_blocks = a.n_blocks;
+        r.tables = a.tables;
+        r.coef = a.coef;
+        r.rows = a.rows;
+        r.k = a.k;
+        r.e = a.e;
+        hipError_t e = launch_reconstruct(r, s, nullptr);
+        if (e != hipSuccess) return e;
+        if (a.sums_out) {
+            for (int i = 0; i < a.e; ++i) {
+                HashArgs h{};
+                h.msgs = a.shards + (int64_t)rows[a.k + i] * a.S;
+                h.stride = a.block_stride;
+                h.len = a.S;
+                h.n = a.n_blocks;
+                h.sums = a.sums_out + (int64_t)rows[a.k + i] * 32;
+                h.sum_stride = (int64_t)R * 32;
+                for (int q = 0; q < 4; ++q) h.key[q] = a.key[q];
+                e = launch_hash(h, s);
+                if (e != hipSuccess) return e;
+            }
+        }
+    }
+    return hipSuccess;
 }
 
 hipError_t launch_hash(const HashArgs& a, hipStream_t s) {

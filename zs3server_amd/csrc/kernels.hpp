@@ -47,15 +47,35 @@ struct HashArgs {
     int64_t stride;
     int64_t len;
     int64_t n;
-    uint8_t* sums;            // n x 32
-    const uint8_t* expect;    // optional n x 32; mismatch flags -> bad
-    int32_t* bad;             // optional n flags (1 = errFileCorrupt)
+    uint8_t* sums;            // n x 32 (at sum_stride bytes per message)
+    const uint8_t* expect;    // optional n x 32 (at sum_stride); mismatch flags -> bad
+    int32_t* bad;             // optional n flags at bad_stride (1 = errFileCorrupt)
+    uint64_t key[4];
+    int64_t sum_stride;       // 0 = 32
+    int64_t bad_stride;       // 0 = 1
+};
+
+// GET / heal pass: verify the k survivor shards the decode reads
+// against their stored bitrot sums and rebuild the missing shards in one pass.
+struct VrArgs {
+    uint8_t* shards;          // [n][k+m][S] at block_stride
+    int64_t block_stride;
+    int64_t S;
+    int64_t n_blocks;
+    const uint32_t* tables;   // perm tables, 8 dwords per (e*k + t); may be null if e == 0
+    const uint8_t* coef;      // e x k coefficients (fallback path)
+    const int32_t* rows;      // k survivor row indices then e rebuilt row indices
+    int k, m, e;
+    const uint8_t* expect;    // [n][k+m][32] stored sums; survivors are compared
+    int32_t* bad;             // [n][k+m]: 1 = survivor failed bitrot (errFileCorrupt)
+    uint8_t* sums_out;        // optional [n][k+m][32]: HH256 of the rebuilt rows
     uint64_t key[4];
 };
 
 // Returns hipSuccess or an error from the launch.
 hipError_t launch_encode(const EncArgs& a, hipStream_t s, bool* used_fast);
 hipError_t launch_reconstruct(const RecArgs& a, hipStream_t s, bool* used_fast);
+hipError_t launch_verify_reconstruct(const VrArgs& a, hipStream_t s, bool* used_fast);
 hipError_t launch_hash(const HashArgs& a, hipStream_t s);
 hipError_t launch_fill(uint8_t* out, int64_t stride, int64_t len, int64_t n, uint64_t seed,
                        uint64_t obj0, hipStream_t s);

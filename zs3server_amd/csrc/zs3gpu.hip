@@ -130,17 +130,18 @@ std::shared_ptr<RecPlan> make_plan(const zs3_codec* c, const uint8_t* present, i
         p->status = ZS3_ERR_SHARD_NO_DATA;
         return p;
     }
+    std::vector<int32_t> valid;  // the k shards ReconstructData reads
+    for (int i = 0; i < n && (int)valid.size() < k; ++i)
+        if (present[i]) valid.push_back(i);
     if (np == n || (data_only && dp == k)) {
         p->noop = true;
+        p->rows = valid;  // verify-only pass (zs3_verify_reconstruct_batch)
         return p;
     }
     if (np < k) {
         p->status = ZS3_ERR_TOO_FEW_SHARDS;
         return p;
     }
-    std::vector<int32_t> valid;
-    for (int i = 0; i < n && (int)valid.size() < k; ++i)
-        if (present[i]) valid.push_back(i);
     std::vector<uint8_t> sub((size_t)k * k), dec((size_t)k * k);
     for (int r = 0; r < k; ++r) std::memcpy(&sub[(size_t)r * k], &c->matrix[(size_t)valid[r] * k], k);
     if (!zs3::gf_invert(sub.data(), k, dec.data())) {
@@ -495,6 +496,39 @@ int zs3_reconstruct_batch(const zs3_codec* cc, uint8_t* d_shards, int64_t block_
     a.e = plan->e;
     bool fast = false;
     rc = map_hip(zs3k::launch_reconstruct(a, (hipStream_t)stream, &fast));
+    t_last_path = fast ? 1 : 0;
+    return rc;
+}
+
+int zs3_verify_reconstruct_batch(const zs3_codec* cc, uint8_t* d_shards, int64_t block_stride, int64_t shard_len,
+                                 int64_t n_blocks, const uint8_t* present, int data_only, const uint8_t* d_expect,
+                                 int32_t* d_bad, uint8_t* d_sums_out, void* stream) {
+    zs3_codec* c = const_cast<zs3_codec*>(cc);
+    if (!c || !present || shard_len < 0 || n_blocks < 0) return ZS3_ERR_INVALID_ARG;
+    auto plan = get_plan(c, present, data_only);
+    if (plan->status) return plan->status;
+    if (shard_len == 0) return ZS3_ERR_SHARD_NO_DATA;
+    if (n_blocks == 0) return ZS3_OK;
+    if (!d_shards || !d_expect || !d_bad) return ZS3_ERR_INVALID_ARG;
+    const int R = c->k + c->m;
+    int rc = map_hip(hipMemsetAsync(d_bad, 0, (size_t)n_blocks * R * 4, (hipStream_t)stream));
+    if (rc) return rc;
+    zs3k::VrArgs a{};
+    rc = plan_device(c, plan.get(), &a.tables, &a.coef, &a.rows);
+    if (rc) return rc;
+    a.shards = d_shards;
+    a.block_stride = block_stride;
+    a.S = shard_len;
+    a.n_blocks = n_blocks;
+    a.k = c->k;
+    a.m = c->m;
+    a.e = plan->noop ? 0 : plan->e;
+    a.expect = d_expect;
+    a.bad = d_bad;
+    a.sums_out = a.e > 0 ? d_sums_out : nullptr;
+    key_words(nullptr, a.key);
+    bool fast = false;
+    rc = map_hip(zs3k::launch_verify_reconstruct(a, (hipStream_t)stream, &fast));
     t_last_path = fast ? 1 : 0;
     return rc;
 }

@@ -21,6 +21,10 @@ ERR_SHARD_NO_DATA, ERR_SHARD_SIZE, ERR_SHORT_DATA = -4, -5, -6
 ERR_FILE_CORRUPT, ERR_INVALID_ARGUMENT = -7, -8
 
 
+class ErasureReadQuorum(Exception):
+    """errErasureReadQuorum (cmd/erasure-errors.go): fewer than k readable shards."""
+
+
 class Erasure:
     """cmd/erasure-coding.go:35-39."""
 
@@ -96,6 +100,42 @@ class Erasure:
         self._reconstruct(data, False)
 
     # erasure-coding.go:122-150
+    def decode_verified(self, shards, S: int, n_blocks: int, present, expect, data_only: bool = True,
+                        sums_out=None, stream=None) -> set:
+        """GET path over a device batch [n][k+m][S] (torch uint8 on the GPU): verify
+        the survivors' bitrot sums and rebuild missing shards in one fused pass
+        (zs3_verify_reconstruct_batch).  A block whose survivor fails verification is
+        re-decoded without that shard, as parallelReader does (erasure-decode.go:165-179:
+        the corrupt reader is dropped and the next shard read); fewer than k good
+        shards -> ErasureReadQuorum (errErasureReadQuorum, :201).  Returns the set of
+        (block, shard) found corrupt (the bitrotHeal signal)."""
+        import torch
+
+        k, m = self.dataBlocks, self.parityBlocks
+        R = k + m
+        bad = torch.zeros((n_blocks, R), dtype=torch.int32, device=shards.device)
+        self._codec.verify_reconstruct_batch(shards, R * S, S, n_blocks, present, data_only, expect, bad,
+                                             sums_out=sums_out, stream=stream)
+        flags = bad.cpu().numpy()
+        corrupt = set()
+        base = [bool(p) for p in present]
+        for b in map(int, np.nonzero(flags.any(axis=1))[0]):
+            pres = list(base)
+            row = flags[b]
+            while row.any():
+                for i in map(int, np.nonzero(row)[0]):
+                    corrupt.add((b, i))
+                    pres[i] = False
+                if sum(pres) < k:
+                    raise ErasureReadQuorum(f"block {b}: {sum(pres)} verified shards < {k}")
+                one = torch.zeros(R, dtype=torch.int32, device=shards.device)
+                so = None if sums_out is None else sums_out.view(-1)[b * R * 32:]
+                self._codec.verify_reconstruct_batch(shards.view(-1)[b * R * S:], R * S, S, 1, pres, data_only,
+                                                     expect.view(-1)[b * R * 32:], one, sums_out=so,
+                                                     stream=stream)
+                row = one.cpu().numpy()
+        return corrupt
+
     def ShardSize(self) -> int:
         return self._codec.shard_size()
 

@@ -19,6 +19,11 @@ timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmcw -o p --output-format c
     python bench.py --steps 3 --warmup 1 --no-cpu > $OUT/pmcw.log 2>&1 || { tail -5 $OUT/pmcw.log; exit 7; }
 python scripts/pmc_traffic.py $(find $OUT/pmcf -name '*counter_collection.csv' | head -1) \
     $(find $OUT/pmcw -name '*counter_collection.csv' | head -1) $P/pmc_traffic.json
+echo "=== pmc VALU"
+timeout -k 10 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_LDS \
+    -d $OUT/pmcv -o p --output-format csv -- \
+    python bench.py --steps 3 --warmup 1 --no-cpu > $OUT/pmcv.log 2>&1 || { tail -5 $OUT/pmcv.log; exit 8; }
+python scripts/pmc_summary.py $(find $OUT/pmcv -name '*counter_collection.csv' | head -1) | tee $P/pmc_valu.txt
 echo "=== bench $(date +%T)"
 timeout -k 10 600 python bench.py > $OUT/bench.log 2>&1 || { cat $OUT/bench.log; exit 4; }
 grep '"metric"' $OUT/bench.log | tee $P/bench.json

@@ -1,0 +1,162 @@
+#!/usr/bin/env python3
+"""Static guard for the untracked (inline-asm) global loads of fused_v2.hip.
+
+The compiler does not know those loads are in flight, so nothing may read or write a
+load's destination VGPRs before an `s_waitcnt vmcnt(N)` has retired the load.  This
+runs a forward dataflow over each kernel's basic blocks: the state maps every pending
+asm-load destination to its age (vector-memory ops issued after it: every global_,
+buffer_, scratch_ and flat_ op counts on vmcnt), merged by minimum age at control-flow
+joins; `s_waitcnt vmcnt(N)` retires entries of age >= N.  Any instruction other than
+another asm load touching a pending destination is reported.
+
+  hipcc --offload-arch=gfx950 -O3 -std=c++17 --cuda-device-only -S -o v2.s fused_v2.hip
+  python scripts/check_async_loads.py v2.s [kernel-substring]
+Exit status 1 on any violation (or when no kernel matched).
+"""
+import re
+import sys
+
+REG = re.compile(r"\bv\[(\d+):(\d+)\]|\bv(\d+)\b")
+VMEM = ("global_", "buffer_", "scratch_", "flat_")
+
+
+def regs(text):
+    out = set()
+    for m in REG.finditer(text):
+        if m.group(3) is not None:
+            out.add(int(m.group(3)))
+        else:
+            out.update(range(int(m.group(1)), int(m.group(2)) + 1))
+    return frozenset(out)
+
+
+def parse_blocks(body):
+    """body: [(lineno, text)] -> ordered blocks [(label, [(ln, insn, is_asm)], succs)]."""
+    blocks, cur_label, cur, in_asm = [], "entry", [], False
+    order = []
+
+    def close(label, insns):
+        blocks.append([label, insns, []])
+
+    for ln, raw in body:
+        s = raw.strip()
+        if s.startswith(";;#ASMSTART"):
+            in_asm = True
+            continue
+        if s.startswith(";;#ASMEND"):
+            in_asm = False
+            continue
+        m = re.match(r"^(\.LBB\S+):", s)
+        if m:
+            close(cur_label, cur)
+            cur_label, cur = m.group(1), []
+            continue
+        code = s.split(";")[0].strip()
+        if not code or code.startswith("."):
+            continue
+        cur.append((ln, code, in_asm))
+        op = code.split()[0]
+        if op.startswith("s_cbranch") or op == "s_branch" or op == "s_setpc_b64":
+            close(cur_label, cur)
+            cur_label, cur = f"__after{ln}", []
+    close(cur_label, cur)
+    idx = {b[0]: i for i, b in enumerate(blocks)}
+    for i, b in enumerate(blocks):
+        last = b[1][-1][1] if b[1] else ""
+        op = last.split()[0] if last else ""
+        if op.startswith("s_cbranch") or op == "s_branch":
+            tgt = last.split()[1]
+            if tgt in idx:
+                b[2].append(idx[tgt])
+            if op != "s_branch" and i + 1 < len(blocks):
+                b[2].append(i + 1)
+        elif i + 1 < len(blocks):
+            b[2].append(i + 1)
+    return blocks
+
+
+def transfer(state, insns, report, name):
+    st = dict(state)
+    bad = 0
+    for ln, code, is_asm in insns:
+        op = code.split()[0]
+        args = code[len(op):]
+        m = re.search(r"vmcnt\((\d+)\)", code) if op.startswith("s_waitcnt") else None
+        if m:
+            n = int(m.group(1))
+            st = {r: a for r, a in st.items() if a < n}
+            continue
+        if op == "s_waitcnt" and args.strip() == "0":
+            st = {}
+            continue
+        touched = regs(args)
+        is_vmem = op.startswith(VMEM)
+        is_asm_load = is_vmem and is_asm and "load" in op
+        if not is_asm_load:
+            hit = [r for r in st if r & touched]
+            if hit and report:
+                print(f"{name}:{ln}: touches in-flight load destination {sorted(set().union(*hit) & touched)}: {code}")
+            bad += len(hit) > 0
+        if is_vmem:
+            st = {r: a + 1 for r, a in st.items()}
+            if is_asm_load:
+                dst = regs(args.split(",")[0])
+                st = {r: a for r, a in st.items() if not (r & dst)}
+                st[dst] = 0
+    return st, bad
+
+
+def check(body, name):
+    blocks = parse_blocks(body)
+    ins = [None] * len(blocks)
+    ins[0] = {}
+    work = [0]
+    while work:
+        i = work.pop()
+        out, _ = transfer(ins[i], blocks[i][1], False, name)
+        for s in blocks[i][2]:
+            if ins[s] is None:
+                new = dict(out)
+            else:
+                new = dict(ins[s])
+                for r, a in out.items():
+                    new[r] = min(a, new.get(r, a))
+            if new != ins[s]:
+                ins[s] = new
+                work.append(s)
+    bad = 0
+    for i, b in enumerate(blocks):
+        if ins[i] is not None:
+            bad += transfer(ins[i], b[1], True, name)[1]
+    return bad
+
+
+def main():
+    path = sys.argv[1]
+    want = sys.argv[2] if len(sys.argv) > 2 else "k_ehx"
+    text = open(path).read().split("\n")
+    funcs, cur = [], None
+    for i, l in enumerate(text, 1):
+        m = re.match(r"^(_Z\S+):", l)
+        if m:
+            cur = (m.group(1), [])
+            funcs.append(cur)
+            continue
+        if cur is not None:
+            if l.strip().startswith("s_endpgm"):
+                cur = None
+                continue
+            cur[1].append((i, l))
+    total, n = 0, 0
+    for name, body in funcs:
+        if want in name:
+            n += 1
+            b = check(body, name[:70])
+            total += b
+            print(f"{name[:70]}: {b} violations")
+    print(f"checked {n} kernels, {total} violations")
+    sys.exit(1 if total or n == 0 else 0)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,412 @@
+// fused_v2.hip — second-generation fused Split + Encode + HighwayHash-256 kernel.
+//
+// Replaces the arithmetic of Erasure.EncodeData (cmd/erasure-coding.go:77-91) plus
+// the k+m streamingBitrotWriter sums (cmd/bitrot-streaming.go:43-65) for the
+// dyadic RS shapes (m in {2,4}, m | k: RS(8+4), RS(4+2), RS(16+4), ...).
+//
+// Same work decomposition as k_encode_hash (kernels.hip): G whole stripes per
+// workgroup, one HighwayHash lane per thread (a quad per shard row), one CW-byte
+// column per thread for the encode, tiles of T bytes per shard row staged in LDS.
+// What changes is the memory pipeline, measured on MI355X (scripts/sweep_variants.py):
+//  * vmcnt is one in-order counter for loads AND stores, so the old order
+//    (store parity(i), then load tile i+1) made the wait for tile i+1's data also
+//    wait for tile i's store acknowledgements.  Here the loads of tile i+PF are
+//    issued BEFORE the parity stores of tile i, so the wait at step i+1 leaves the
+//    stores in flight.
+//  * every LDS read of a tile's hash words is issued before the first HighwayHash
+//    update (one lgkmcnt wait per tile instead of one per two packets).
+//  * NBUF = 2 LDS tiles: one barrier per step.
+//  * full tiles run a branch-free body; the ragged tail tile (S % T) is peeled.
+#include "kernels.hpp"
+#include "gf_dev.hpp"
+#include "hh256_dev.hpp"
+
+#include <type_traits>
+
+using namespace zs3dev;
+
+namespace zs3k {
+
+namespace {
+
+__device__ __forceinline__ void lds_barrier2() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+template <int NWd>
+__device__ __forceinline__ Col<NWd> ld_col(const uint8_t* p) {
+    Col<NWd> v;
+    __builtin_memcpy(&v, p, 4 * NWd);
+    return v;
+}
+template <int NWd>
+__device__ __forceinline__ void st_col(uint8_t* p, const Col<NWd>& v) {
+    __builtin_memcpy(p, &v, 4 * NWd);
+}
+template <int NWd>
+__device__ __forceinline__ void st_col_nt(uint8_t* p, const Col<NWd>& v) {
+    if constexpr (NWd == 4) {
+        typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+        u4 t = {v.w[0], v.w[1], v.w[2], v.w[3]};
+        __builtin_nontemporal_store(t, reinterpret_cast<u4*>(p));
+    } else if constexpr (NWd == 2) {
+        typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+        u2 t = {v.w[0], v.w[1]};
+        __builtin_nontemporal_store(t, reinterpret_cast<u2*>(p));
+    } else {
+        __builtin_nontemporal_store(v.w[0], reinterpret_cast<uint32_t*>(p));
+    }
+}
+
+// Raw 4/8/16-byte register types for the in-flight columns.
+template <int NWd> struct VecOf;
+template <> struct VecOf<1> { typedef uint32_t type; };
+template <> struct VecOf<2> { typedef uint32_t type __attribute__((ext_vector_type(2))); };
+template <> struct VecOf<4> { typedef uint32_t type __attribute__((ext_vector_type(4))); };
+
+// Global load whose completion the compiler does not track: LLVM's waitcnt pass waits
+// vmcnt(0) before the first use of a load that has stores issued after it, which
+// serialises the parity stores with the next tile's data (and defeats any deeper
+// prefetch).  The hardware retires vector-memory ops in issue order, so the kernel
+// waits for exactly the loads it needs with vm_wait<N>().  The destination is the
+// long-lived prefetch variable itself (no temporary), so its register stays
+// allocated until the wait; scripts/check_async_loads.py verifies in the ISA that no
+// instruction reads a load's destination before the next s_waitcnt vmcnt.
+template <int NWd>
+__device__ __forceinline__ void ld_async(typename VecOf<NWd>::type& dst, const uint8_t* p) {
+    if constexpr (NWd == 4)
+        asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(dst) : "v"(p) : "memory");
+    else if constexpr (NWd == 2)
+        asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(dst) : "v"(p) : "memory");
+    else
+        asm volatile("global_load_dword %0, %1, off" : "=v"(dst) : "v"(p) : "memory");
+}
+
+// s_waitcnt vmcnt(N), then an empty asm that "redefines" each column, so no use of a
+// column can be scheduled above the wait.
+template <int N, int K, typename V>
+__device__ __forceinline__ void vm_wait(V (&xs)[K]) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+#pragma unroll
+    for (int j = 0; j < K; ++j) asm volatile("" : "+v"(xs[j]));
+}
+
+template <int NWd>
+__device__ __forceinline__ Col<NWd> to_col(const typename VecOf<NWd>::type& v) {
+    Col<NWd> c;
+    if constexpr (NWd == 1) {
+        c.w[0] = v;
+    } else {
+#pragma unroll
+        for (int w = 0; w < NWd; ++w) c.w[w] = v[w];
+    }
+    return c;
+}
+
+}  // namespace
+
+// K data rows, M parity rows (dyadic), G stripes per workgroup, CW-byte columns,
+// PF tiles of register prefetch, NBUF LDS tiles, NTS = non-temporal parity stores.
+// ABL (timing-only diagnostics): 1 = no hash, 2 = no GF arithmetic (parity = data
+// rows 0..M-1), 3 = neither.
+// PIPE: software-pipelined body, one basic block per step holding encode(tile i)
+// AND hash(tile i-1), so the scheduler fills the HighwayHash chain's dependent
+// latency with independent GF work (requires NBUF = 2).
+template <int K, int M, int G, int CW, int PF, int NBUF, bool NTS, int ABL = 0, bool PIPE = false>
+__global__ void __launch_bounds__(4 * G * (K + M)) __attribute__((amdgpu_waves_per_eu(3))) k_ehx(EncArgs a) {
+    constexpr int R = K + M;
+    constexpr int NT = 4 * G * R;
+    constexpr int NWd = CW / 4;
+    constexpr int CPB = NT / G;        // columns per stripe = threads per stripe
+    constexpr int T = CPB * CW;        // tile bytes per shard row
+    constexpr int TS = T + 32;         // +8 banks per row: conflict-free b64 row reads
+    constexpr int NPK = T / 32;
+    constexpr int NTAB = K * 8;
+    static_assert(M == 2 || M == 4, "dyadic shapes only");
+    __shared__ __attribute__((aligned(16))) uint8_t tile[NBUF][G * R * TS];
+    __shared__ __attribute__((aligned(16))) uint32_t tabs[NTAB];
+
+    const int tid = threadIdx.x;
+    const int64_t blk0 = (int64_t)blockIdx.x * G;
+    const int64_t S = a.S;
+    for (int i = tid; i < NTAB; i += NT) tabs[i] = a.dtables[i];
+
+    // hash role: lane `lane` of shard row `chain` (stripe chain / R)
+    const int chain = tid >> 2, lane = tid & 3;
+    const bool chain_live = blk0 + chain / R < a.n_blocks;
+    const uint32_t sel = zipper_sel(lane);
+    HHLane st = hh_init(lane, a.key[0], a.key[1], a.key[2], a.key[3]);
+
+    // encode role: column o of stripe g (dead stripes of the last workgroup alias
+    // the last live block and store byte-identical parity)
+    const int g = tid / CPB, o = (tid % CPB) * CW;
+    const int64_t b = (blk0 + g) < a.n_blocks ? (blk0 + g) : (a.n_blocks - 1);
+    const uint8_t* src = a.data + b * a.data_stride + o;
+    uint8_t* pdst = a.parity + b * a.parity_stride + o;
+    const int col_off = g * R * TS + o;
+    const int row_off = chain * TS + 8 * lane;
+
+    const int64_t nfull = S / T;
+    const int tail = (int)(S - nfull * T);
+
+    typedef typename VecOf<NWd>::type VT;
+    VT x[PF][K];
+    auto load = [&](VT (&xs)[K], int64_t t0) {
+#pragma unroll
+        for (int j = 0; j < K; ++j) ld_async<NWd>(xs[j], src + (int64_t)j * S + t0);
+    };
+    auto load_tail = [&](VT (&xs)[K], int64_t t0) {
+        if (o < tail) {
+#pragma unroll
+            for (int j = 0; j < K; ++j) ld_async<NWd>(xs[j], src + (int64_t)j * S + t0);
+        } else {
+#pragma unroll
+            for (int j = 0; j < K; ++j) xs[j] = VT{};
+        }
+    };
+    // encode tile into LDS buffer `tl`, then issue the loads of tile `t_next`
+    // into the same registers, then store parity of tile t0.
+    auto encode = [&](VT (&xr)[K], uint8_t* tl, Col<NWd> (&par)[M]) {
+        Col<NWd> xs[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) xs[j] = to_col<NWd>(xr[j]);
+        if constexpr (ABL & 2) {
+#pragma unroll
+            for (int r = 0; r < M; ++r) par[r] = xs[r];
+        } else {
+            encode_dyadic<NWd, K, M, !PIPE>(xs, par, tabs);
+        }
+#pragma unroll
+        for (int j = 0; j < K; ++j) st_col<NWd>(tl + col_off + j * TS, xs[j]);
+#pragma unroll
+        for (int r = 0; r < M; ++r) st_col<NWd>(tl + col_off + (K + r) * TS, par[r]);
+    };
+    auto store_par = [&](const Col<NWd> (&par)[M], int64_t t0) {
+#pragma unroll
+        for (int r = 0; r < M; ++r) {
+            if (NTS)
+                st_col_nt<NWd>(pdst + (int64_t)r * S + t0, par[r]);
+            else
+                st_col<NWd>(pdst + (int64_t)r * S + t0, par[r]);
+        }
+    };
+    auto hash_full = [&](const uint8_t* tl) {
+        const uint64_t* p = reinterpret_cast<const uint64_t*>(tl + row_off);
+        uint64_t w[NPK];
+#pragma unroll
+        for (int i = 0; i < NPK; ++i) w[i] = p[4 * i];
+#pragma unroll
+        for (int i = 0; i < NPK; ++i) {
+            if constexpr (ABL & 1)
+                st.v0 ^= w[i];
+            else
+                hh_update(st, w[i], sel);
+        }
+    };
+    auto prefetch = [&](VT (&xs)[K], int64_t tn) {
+        if (tn < nfull)
+            load(xs, tn * T);
+        else if (tn == nfull && tail)
+            load_tail(xs, tn * T);
+    };
+    // One step on full tile ti held in xs: encode into LDS, issue the loads of tile
+    // ti+PF into the freed registers (UNC: known to be a full tile, no branch), then
+    // the parity stores, barrier, hash.
+    // Before encode(ti) the wave's pending vector-memory ops are, oldest first:
+    // loads(ti), stores(ti-PF), loads(ti+1), stores(ti-PF+1), ..., loads(ti+PF-1),
+    // stores(ti-1).  Steady state waits for loads(ti) only: vmcnt(M + (PF-1)*(K+M)).
+    // Peeled/conditional steps wait for everything.
+    auto step = [&](VT (&xs)[K], int64_t ti, auto unc) {
+        uint8_t* tl = tile[NBUF == 1 ? 0 : (ti & 1)];
+        Col<NWd> par[M];
+        if constexpr (decltype(unc)::value)
+            vm_wait<M + (PF - 1) * (K + M)>(xs);
+        else
+            vm_wait<0>(xs);
+        encode(xs, tl, par);
+        if constexpr (decltype(unc)::value)
+            load(xs, (ti + PF) * T);
+        else
+            prefetch(xs, ti + PF);
+        store_par(par, ti * T);
+        lds_barrier2();
+        hash_full(tl);
+        if (NBUF == 1) lds_barrier2();
+    };
+    auto tail_step = [&](VT (&xs)[K]) {
+        uint8_t* tl = tile[NBUF == 1 ? 0 : (nfull & 1)];
+        Col<NWd> par[M];
+        vm_wait<0>(xs);
+        encode(xs, tl, par);
+        if (o < tail) store_par(par, nfull * T);
+        lds_barrier2();
+        const uint8_t* row = tl + chain * TS;
+        hh_packets(st, row, tail >> 5, lane, sel);
+        if (tail & 31) hh_remainder(st, row + (tail & ~31), (uint32_t)(tail & 31), lane, sel);
+    };
+    using Unc = std::integral_constant<bool, true>;
+    using Cnd = std::integral_constant<bool, false>;
+
+    if constexpr (PIPE) {
+        static_assert(NBUF == 2, "pipelined body double-buffers the LDS tile");
+        // Step ti: hash tile ti-1 (buffer (ti-1)&1, written before the last barrier)
+        // and encode tile ti into buffer ti&1 (last read by hash(ti-2), which every
+        // wave finished before the last barrier); one barrier per step.
+        auto hash_words = [&](const uint8_t* tl, uint64_t (&w)[NPK]) {
+            const uint64_t* p = reinterpret_cast<const uint64_t*>(tl + row_off);
+#pragma unroll
+            for (int i2 = 0; i2 < NPK; ++i2) w[i2] = p[4 * i2];
+        };
+        auto hash_apply = [&](const uint64_t (&w)[NPK]) {
+#pragma unroll
+            for (int i2 = 0; i2 < NPK; ++i2) {
+                if constexpr (ABL & 1)
+                    st.v0 ^= w[i2];
+                else
+                    hh_update(st, w[i2], sel);
+            }
+        };
+        // steady state: full tile ti (>= 1) encoded, tile ti+PF known full
+        auto steady = [&](VT (&xs)[K], int64_t ti) {
+            uint64_t w[NPK];
+            hash_words(tile[(ti - 1) & 1], w);
+            vm_wait<M + (PF - 1) * (K + M)>(xs);
+            Col<NWd> par[M];
+            encode(xs, tile[ti & 1], par);
+            load(xs, (ti + PF) * T);
+            store_par(par, ti * T);
+            hash_apply(w);
+            lds_barrier2();
+        };
+        // Branch-free prefetch for the edge steps: a tile past the end (or a tail
+        // column past the tail) re-reads tile 0 of its own row, so x is defined on
+        // every path (no phi copies of in-flight registers) and the value is unused.
+        auto prefetch_any = [&](VT (&xs)[K], int64_t tn) {
+            const bool ok = tn < nfull || (tn == nfull && o < tail);
+            load(xs, ok ? tn * T : 0);
+        };
+        // any step ti >= 0: hash tile ti-1 if it is a full tile, encode tile ti if it
+        // exists (full or tail); always prefetch tile ti+PF and hit the barrier.
+        auto edge = [&](VT (&xs)[K], int64_t ti) {
+            uint64_t w[NPK];
+            const bool do_hash = ti >= 1 && ti <= nfull;
+            if (do_hash) hash_words(tile[(ti - 1) & 1], w);
+            vm_wait<0>(xs);
+            if (ti < nfull || (ti == nfull && tail)) {
+                Col<NWd> par[M];
+                encode(xs, tile[ti & 1], par);
+                if (ti < nfull || o < tail) store_par(par, ti * T);
+            }
+            prefetch_any(xs, ti + PF);
+            if (do_hash) hash_apply(w);
+            lds_barrier2();
+        };
+        lds_barrier2();  // tables visible
+#pragma unroll
+        for (int p = 0; p < PF; ++p) prefetch_any(x[p], p);
+#pragma unroll
+        for (int p = 0; p < PF; ++p) edge(x[p], p);
+        int64_t i = PF;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        for (; i + 2 * PF <= nfull; i += PF) {
+#pragma unroll
+            for (int p = 0; p < PF; ++p) steady(x[p], i + p);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int p = 0; p < 2 * PF; ++p) edge(x[p % PF], i + p);
+        if (tail) {
+            const uint8_t* row = tile[nfull & 1] + chain * TS;
+            hh_packets(st, row, tail >> 5, lane, sel);
+            if (tail & 31) hh_remainder(st, row + (tail & ~31), (uint32_t)(tail & 31), lane, sel);
+        }
+    } else {
+        lds_barrier2();  // tables visible
+    #pragma unroll
+        for (int p = 0; p < PF; ++p) prefetch(x[p], p);
+        // Peeled first PF steps: the steady-state loop is entered with the same pending
+        // vector-memory ops as its back edge (loads of the next tiles, then stores), so
+        // the compiler's vmcnt before each encode leaves the parity stores in flight.
+    #pragma unroll
+        for (int p = 0; p < PF; ++p)
+            if (p < nfull) step(x[p], p, Cnd{});
+        int64_t i = PF;
+        // Drain once before the steady state: its in-loop vmcnt counts then only have to
+        // hold for the loop's own issue order (and scripts/check_async_loads.py can prove
+        // it without path-sensitive reasoning about the peeled steps).
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        for (; i + 2 * PF <= nfull; i += PF) {
+    #pragma unroll
+            for (int p = 0; p < PF; ++p) step(x[p], i + p, Unc{});
+        }
+    #pragma unroll
+        for (int p = 0; p < 2 * PF; ++p)
+            if (i + p < nfull) step(x[p % PF], i + p, Cnd{});
+        if (tail) {
+    #pragma unroll
+            for (int p = 0; p < PF; ++p)
+                if (nfull % PF == p) tail_step(x[p]);
+        }
+
+    }
+
+    // Keep every prefetch register allocated until all loads have retired: a load
+    // whose value turns out unused must not have its destination handed to other code
+    // while it is still in flight.
+#pragma unroll
+    for (int p = 0; p < PF; ++p) vm_wait<0>(x[p]);
+
+    const uint64_t h = hh_finalize256(st, lane, sel);
+    if (chain_live) {
+        const int64_t bb = blk0 + chain / R;
+        const int s = chain % R;
+        *reinterpret_cast<uint64_t*>(a.sums + (bb * R + s) * 32 + 8 * lane) = h;
+    }
+}
+
+template <int K, int M, int CW, int PF, int NBUF, bool NTS = false, int ABL = 0, bool PIPE = false>
+static bool launch_ehx_t(const EncArgs& a, hipStream_t s) {
+    constexpr int R = K + M;
+    // G: smallest number of stripes making 4*G*R a multiple of 64 (whole wavefronts)
+    constexpr int G = (R % 16 == 0) ? 1 : (R % 8 == 0) ? 2 : (R % 4 == 0) ? 4 : (R % 2 == 0) ? 8 : 16;
+    constexpr int NT = 4 * G * R;
+    constexpr int T = (NT / G) * CW;
+    constexpr size_t lds = (size_t)NBUF * G * R * (T + 32) + K * 32;
+    if constexpr (lds > 65536 || NT > 1024) {
+        return false;
+    } else {
+        if (a.dyb != M) return false;
+        const int64_t grid = (a.n_blocks + G - 1) / G;
+        hipLaunchKernelGGL((k_ehx<K, M, G, CW, PF, NBUF, NTS, ABL, PIPE>), dim3((unsigned)grid), dim3(NT), 0, s, a);
+        return true;
+    }
+}
+
+// Only instances that scripts/check_async_loads.py proves clean are compiled (wider
+// columns and deeper prefetch on the other shapes make hipcc copy or re-use
+// registers of in-flight loads).
+template <int K, int M>
+static bool launch_ehx_km(int v, const EncArgs& a, hipStream_t s) {
+    constexpr bool deep = K == 8 && M == 4;
+    switch (v) {
+        case 50: return launch_ehx_t<K, M, 8, 1, 2>(a, s);
+        case 51: return launch_ehx_t<K, M, 8, 1, 1>(a, s);
+        case 52: if constexpr (deep) return launch_ehx_t<K, M, 8, 2, 2>(a, s); else return false;
+        case 53: if constexpr (deep) return launch_ehx_t<K, M, 8, 2, 1>(a, s); else return false;
+        case 55: return launch_ehx_t<K, M, 8, 1, 2, true>(a, s);
+        case 70: return launch_ehx_t<K, M, 8, 1, 2, false, 0, true>(a, s);
+        case 71: if constexpr (deep) return launch_ehx_t<K, M, 8, 2, 2, false, 0, true>(a, s); else return false;
+        case 61: if constexpr (deep) return launch_ehx_t<K, M, 8, 1, 2, false, 1>(a, s); else return false;
+        case 64: if constexpr (deep) return launch_ehx_t<K, M, 8, 2, 2, false, 1>(a, s); else return false;
+        default: return false;
+    }
+}
+
+bool launch_ehx(int v, const EncArgs& a, hipStream_t s) {
+    if (a.k == 8 && a.m == 4) return launch_ehx_km<8, 4>(v, a, s);
+    if (a.k == 4 && a.m == 2) return launch_ehx_km<4, 2>(v, a, s);
+    if (a.k == 16 && a.m == 4) return launch_ehx_km<16, 4>(v, a, s);
+    return false;
+}
+
+}  // namespace zs3k

@@ -139,13 +139,15 @@ __device__ __forceinline__ int opaque_zero() {
 //   y0 = Y0+Y1+Y2+Y3, y1 = Y1+Y3, y2 = Y2+Y3, y3 = Y3.
 // M = 2: X = (x0+x1, x1), A = (a+b, b), Y0 = A0 X0, Y1 = A0 X1 + A1 X0,
 // y0 = Y0+Y1, y1 = Y1.
-template <int NWd, int K, int M>
+// SB: a scheduling barrier per block keeps each block's table reads local (fewer
+// VGPRs); without it the scheduler may interleave the encode with other work.
+template <int NWd, int K, int M, bool SB = true>
 __device__ __forceinline__ void encode_dyadic(const Col<NWd> (&x)[K], Col<NWd> (&out)[M], const uint32_t* dtabs) {
     static_assert(M == 2 || M == 4, "dyadic block");
     uint32_t Y[M][NWd];
 #pragma unroll
     for (int q = 0; q < K / M; ++q) {
-        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
         const uint32_t* tq = dtabs + opaque_zero() + q * M * 8;
         CoefTab t[M];
 #pragma unroll

@@ -116,7 +116,8 @@ __device__ __forceinline__ void stcol(uint8_t* p, const Col<NWd>& v) {
 }
 
 // ABL (diagnostics, timing only): 1 = skip the hash phase, 2 = skip the GF arithmetic
-// (parity rows = data row 0; loads, LDS and stores unchanged).
+// (parity rows = data row 0; loads, LDS and stores unchanged), 3 = skip hash and the
+// parity stores, 4 = skip hash and the LDS tile writes.
 template <int K, int M, int G, int T, int NBUF, int NT, int CW, int PF, bool NTL, bool STAMP = false, int DYB = 0,
           bool PAIR = false, int ABL = 0>
 __global__ void __launch_bounds__(NT) k_encode_hash(EncArgs a) {
@@ -184,8 +185,10 @@ __global__ void __launch_bounds__(NT) k_encode_hash(EncArgs a) {
                 for (int j = 0; j < K; ++j) stcol<NWd>(tl + (g * R + j) * TS + o, x[c][j]);
             } else if constexpr (DYB != 0) {
                 encode_dyadic<NWd, K, M>(x[c], par, dtabs);
+                if constexpr (ABL != 4) {
 #pragma unroll
-                for (int j = 0; j < K; ++j) stcol<NWd>(tl + (g * R + j) * TS + o, x[c][j]);
+                    for (int j = 0; j < K; ++j) stcol<NWd>(tl + (g * R + j) * TS + o, x[c][j]);
+                }
             } else {
                 const uint32_t* tb = tabs + opaque_zero();
                 GfAcc acc[M][NWd];
@@ -216,8 +219,10 @@ __global__ void __launch_bounds__(NT) k_encode_hash(EncArgs a) {
 #pragma unroll
             for (int r = 0; r < M; ++r) {
                 const Col<NWd>& p = par[r];
-                stcol<NWd>(tl + (g * R + K + r) * TS + o, p);
-                if (NTL)
+                if constexpr (ABL != 4) stcol<NWd>(tl + (g * R + K + r) * TS + o, p);
+                if constexpr (ABL == 3) {
+                    if (p.w[0] == 0x12345678u && p.w[NWd - 1] == 0x9abcdef0u) stcol<NWd>(pbase + (int64_t)r * S, p);
+                } else if (NTL)
                     stcol_nt<NWd>(pbase + (int64_t)r * S, p);
                 else
                     stcol<NWd>(pbase + (int64_t)r * S, p);
@@ -253,7 +258,7 @@ __global__ void __launch_bounds__(NT) k_encode_hash(EncArgs a) {
         lds_barrier();
         const uint64_t s3 = stamp();
         const uint8_t* row = tl + crow * TS;
-        if constexpr (ABL == 1) {
+        if constexpr (ABL == 1 || ABL == 3 || ABL == 4) {
         } else if constexpr (PAIR) {
             if (L == T)
                 hh2_packets_n<T / 32>(st2, row, lane);
@@ -983,14 +988,14 @@ static void launch_pair(const EncArgs& a, hipStream_t s) {
                        dim3(NT), 0, s, a);
 }
 
-template <int K, int M, int ABL>
+template <int K, int M, int ABL, int T = 384, int CW = 8, int NBUF = 1, int PF = 1>
 static void launch_ablation(const EncArgs& a, hipStream_t s) {
     constexpr int R = K + M;
     constexpr int G = pick_G<R>();
     constexpr int NT = round64(4 * G * R);
     const int64_t grid = (a.n_blocks + G - 1) / G;
     constexpr int DY = ((M == 2 || M == 4) && K % M == 0) ? M : 0;
-    hipLaunchKernelGGL((k_encode_hash<K, M, G, 384, 1, NT, 8, 1, false, false, DY, false, ABL>), dim3((unsigned)grid),
+    hipLaunchKernelGGL((k_encode_hash<K, M, G, T, NBUF, NT, CW, PF, false, false, DY, false, ABL>), dim3((unsigned)grid),
                        dim3(NT), 0, s, a);
 }
 
@@ -1037,9 +1042,15 @@ static bool launch_variant(int v, const EncArgs& a, hipStream_t s) {
         case 34: launch_pair<K, M, 192, 1, 8>(a, s); return true;
         case 41: launch_ablation<K, M, 1>(a, s); return true;
         case 42: launch_ablation<K, M, 2>(a, s); return true;
+        case 43: launch_ablation<K, M, 3>(a, s); return true;
+        case 44: launch_ablation<K, M, 4>(a, s); return true;
+        case 45: launch_ablation<K, M, 1, 768, 16>(a, s); return true;
+        case 46: launch_ablation<K, M, 1, 384, 8, 1, 2>(a, s); return true;
+        case 47: launch_ablation<K, M, 3, 768, 16>(a, s); return true;
+        case 48: launch_ablation<K, M, 4, 768, 16>(a, s); return true;
         case 101: launch_fused<K, M, G, 384, 1, 8, 1, false, true>(a, s); return true;
         case 102: launch_fused<K, M, G, 256, 2, 16, 1, false, true>(a, s); return true;
-        default: return false;
+        default: return launch_ehx(v, a, s);
     }
 }
 

@@ -83,6 +83,10 @@ hipError_t launch_fill(uint8_t* out, int64_t stride, int64_t len, int64_t n, uin
 // Number of (k, m) pairs with a specialised fused kernel, and whether (k, m) has one.
 bool has_fast_encode(int k, int m);
 
+// Second-generation fused encode+hash kernel (fused_v2.hip), variant numbers 50+.
+// Returns false when the variant does not apply to a.k/a.m (caller falls back).
+bool launch_ehx(int v, const EncArgs& a, hipStream_t s);
+
 // Tuning knob for experiments: 0 = default variant.
 void set_variant(int v);
 int get_variant();

@@ -1,0 +1,49 @@
+"""ISA guard for fused_v2.hip (CPU, needs hipcc): the kernels issue global loads the
+compiler does not track (inline asm, exact s_waitcnt vmcnt(N) by hand), so no
+instruction may touch a load's destination VGPRs before a wait retires it.  Compiles
+the device code to assembly and runs scripts/check_async_loads.py's dataflow check on
+every compiled k_ehx instance; a compiler change that copies or re-uses an in-flight
+register fails here, before any GPU run."""
+import os
+import shutil
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "scripts"))
+
+
+def _hipcc():
+    for c in ("/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    return None
+
+
+@pytest.mark.skipif(_hipcc() is None, reason="hipcc not available")
+def test_untracked_loads_never_touched_in_flight(tmp_path):
+    import check_async_loads as cal
+
+    asm = tmp_path / "fused_v2.s"
+    subprocess.check_call([_hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "--cuda-device-only", "-S",
+                           "-o", str(asm), os.path.join(ROOT, "zs3server_amd", "csrc", "fused_v2.hip"),
+                           "-I", os.path.join(ROOT, "include")], stderr=subprocess.DEVNULL)
+    text = asm.read_text().split("\n")
+    funcs, cur = [], None
+    for i, line in enumerate(text, 1):
+        if line.startswith("_Z") and line.rstrip().endswith(":") or (line.startswith("_Z") and ":" in line and "@" in line):
+            name = line.split(":")[0]
+            cur = (name, [])
+            funcs.append(cur)
+            continue
+        if cur is not None:
+            if line.strip().startswith("s_endpgm"):
+                cur = None
+                continue
+            cur[1].append((i, line))
+    kernels = [(n, b) for n, b in funcs if "k_ehx" in n]
+    assert kernels, "no k_ehx instance found in the assembly"
+    bad = {n: cal.check(b, n) for n, b in kernels}
+    assert all(v == 0 for v in bad.values()), bad

@@ -112,7 +112,10 @@ __device__ __forceinline__ Col<NWd> to_col(const typename VecOf<NWd>::type& v) {
 // PIPE: software-pipelined body, one basic block per step holding encode(tile i)
 // AND hash(tile i-1), so the scheduler fills the HighwayHash chain's dependent
 // latency with independent GF work (requires NBUF = 2).
-template <int K, int M, int G, int CW, int PF, int NBUF, bool NTS, int ABL = 0, bool PIPE = false>
+// PRIO: rotate s_setprio by (tile + workgroup) so co-resident workgroups of a CU
+// progress at equal rates (oldest-first issue otherwise lets the first workgroup of a
+// CU finish far ahead and leaves the CU under-occupied for the rest of the launch).
+template <int K, int M, int G, int CW, int PF, int NBUF, bool NTS, int ABL = 0, bool PIPE = false, bool PRIO = false>
 __global__ void __launch_bounds__(4 * G * (K + M)) __attribute__((amdgpu_waves_per_eu(3))) k_ehx(EncArgs a) {
     constexpr int R = K + M;
     constexpr int NT = 4 * G * R;
@@ -123,8 +126,19 @@ __global__ void __launch_bounds__(4 * G * (K + M)) __attribute__((amdgpu_waves_p
     constexpr int NPK = T / 32;
     constexpr int NTAB = K * 8;
     static_assert(M == 2 || M == 4, "dyadic shapes only");
-    __shared__ __attribute__((aligned(16))) uint8_t tile[NBUF][G * R * TS];
+    // tile buffers in dynamic LDS (one workgroup may take up to 160 KiB)
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem_dyn[];
+    uint8_t(*tile)[G * R * TS] = reinterpret_cast<uint8_t(*)[G * R * TS]>(smem_dyn);
     __shared__ __attribute__((aligned(16))) uint32_t tabs[NTAB];
+    auto set_prio = [&](int64_t ti) {
+        if constexpr (PRIO) {
+            const int q = (int)((ti + blockIdx.x) & 3);
+            if (q == 0) __builtin_amdgcn_s_setprio(0);
+            else if (q == 1) __builtin_amdgcn_s_setprio(1);
+            else if (q == 2) __builtin_amdgcn_s_setprio(2);
+            else __builtin_amdgcn_s_setprio(3);
+        }
+    };
 
     const int tid = threadIdx.x;
     const int64_t blk0 = (int64_t)blockIdx.x * G;
@@ -148,6 +162,14 @@ __global__ void __launch_bounds__(4 * G * (K + M)) __attribute__((amdgpu_waves_p
 
     const int64_t nfull = S / T;
     const int tail = (int)(S - nfull * T);
+
+    // Diagnostics (a.dbg set): per-wave start/end real time, shader clocks, HW_ID and
+    // XCC_ID, to see load balance across CUs/XCDs and the in-kernel clock.
+    uint64_t rt0 = 0, ct0 = 0;
+    if (a.dbg) {
+        rt0 = __builtin_amdgcn_s_memrealtime();
+        ct0 = __builtin_amdgcn_s_memtime();
+    }
 
     typedef typename VecOf<NWd>::type VT;
     VT x[PF][K];
@@ -217,6 +239,7 @@ __global__ void __launch_bounds__(4 * G * (K + M)) __attribute__((amdgpu_waves_p
     // stores(ti-1).  Steady state waits for loads(ti) only: vmcnt(M + (PF-1)*(K+M)).
     // Peeled/conditional steps wait for everything.
     auto step = [&](VT (&xs)[K], int64_t ti, auto unc) {
+        set_prio(ti);
         uint8_t* tl = tile[NBUF == 1 ? 0 : (ti & 1)];
         Col<NWd> par[M];
         if constexpr (decltype(unc)::value)
@@ -268,6 +291,7 @@ __global__ void __launch_bounds__(4 * G * (K + M)) __attribute__((amdgpu_waves_p
         };
         // steady state: full tile ti (>= 1) encoded, tile ti+PF known full
         auto steady = [&](VT (&xs)[K], int64_t ti) {
+            set_prio(ti);
             uint64_t w[NPK];
             hash_words(tile[(ti - 1) & 1], w);
             vm_wait<M + (PF - 1) * (K + M)>(xs);
@@ -362,22 +386,46 @@ __global__ void __launch_bounds__(4 * G * (K + M)) __attribute__((amdgpu_waves_p
         const int s = chain % R;
         *reinterpret_cast<uint64_t*>(a.sums + (bb * R + s) * 32 + 8 * lane) = h;
     }
+    if (a.dbg && (tid & 63) == 0) {
+        const uint64_t rt1 = __builtin_amdgcn_s_memrealtime();
+        const uint64_t ct1 = __builtin_amdgcn_s_memtime();
+        uint64_t* d = a.dbg + ((int64_t)blockIdx.x * (NT / 64) + (tid >> 6)) * 5;
+        d[0] = rt0;
+        d[1] = rt1;
+        d[2] = ct1 - ct0;
+        d[3] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+        d[4] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+    }
 }
 
-template <int K, int M, int CW, int PF, int NBUF, bool NTS = false, int ABL = 0, bool PIPE = false>
+// GM multiplies the minimal stripe count per workgroup (GM = 4 on RS(8+4): 16 stripes,
+// 12 waves, one workgroup per CU, all of a CU's waves in one barrier domain).
+// LDSMIN pads the dynamic LDS so that at most 163840 / LDSMIN workgroups share a CU.
+template <int K, int M, int CW, int PF, int NBUF, bool NTS = false, int ABL = 0, bool PIPE = false,
+          int GM = 1, bool PRIO = false, int LDSMIN = 0>
 static bool launch_ehx_t(const EncArgs& a, hipStream_t s) {
     constexpr int R = K + M;
     // G: smallest number of stripes making 4*G*R a multiple of 64 (whole wavefronts)
-    constexpr int G = (R % 16 == 0) ? 1 : (R % 8 == 0) ? 2 : (R % 4 == 0) ? 4 : (R % 2 == 0) ? 8 : 16;
+    constexpr int G0 = (R % 16 == 0) ? 1 : (R % 8 == 0) ? 2 : (R % 4 == 0) ? 4 : (R % 2 == 0) ? 8 : 16;
+    constexpr int G = G0 * GM;
     constexpr int NT = 4 * G * R;
     constexpr int T = (NT / G) * CW;
-    constexpr size_t lds = (size_t)NBUF * G * R * (T + 32) + K * 32;
-    if constexpr (lds > 65536 || NT > 1024) {
+    constexpr size_t tiles = (size_t)NBUF * G * R * (T + 32);
+    constexpr size_t dyn = tiles > (size_t)LDSMIN ? tiles : (size_t)LDSMIN;
+    if constexpr (dyn + K * 32 > 163840 || NT > 1024) {
         return false;
     } else {
         if (a.dyb != M) return false;
+        auto kern = k_ehx<K, M, G, CW, PF, NBUF, NTS, ABL, PIPE, PRIO>;
+        static bool attr = false;
+        if (!attr) {
+            if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn) !=
+                hipSuccess)
+                return false;
+            attr = true;
+        }
         const int64_t grid = (a.n_blocks + G - 1) / G;
-        hipLaunchKernelGGL((k_ehx<K, M, G, CW, PF, NBUF, NTS, ABL, PIPE>), dim3((unsigned)grid), dim3(NT), 0, s, a);
+        hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), dyn, s, a);
         return true;
     }
 }
@@ -396,6 +444,12 @@ static bool launch_ehx_km(int v, const EncArgs& a, hipStream_t s) {
         case 55: return launch_ehx_t<K, M, 8, 1, 2, true>(a, s);
         case 70: return launch_ehx_t<K, M, 8, 1, 2, false, 0, true>(a, s);
         case 71: if constexpr (deep) return launch_ehx_t<K, M, 8, 2, 2, false, 0, true>(a, s); else return false;
+        case 80: if constexpr (deep) return launch_ehx_t<K, M, 8, 1, 2, false, 0, false, 4>(a, s); else return false;
+        case 81: if constexpr (deep) return launch_ehx_t<K, M, 8, 1, 1, false, 0, false, 4, false, 83968>(a, s); else return false;
+        case 82: return launch_ehx_t<K, M, 8, 1, 2, false, 0, false, 1, true>(a, s);
+        case 83: if constexpr (deep) return launch_ehx_t<K, M, 8, 2, 2, false, 0, false, 4>(a, s); else return false;
+        case 84: if constexpr (deep) return launch_ehx_t<K, M, 8, 1, 2, false, 0, false, 2>(a, s); else return false;
+        case 85: if constexpr (deep) return launch_ehx_t<K, M, 8, 1, 2, false, 0, true, 4>(a, s); else return false;
         case 61: if constexpr (deep) return launch_ehx_t<K, M, 8, 1, 2, false, 1>(a, s); else return false;
         case 64: if constexpr (deep) return launch_ehx_t<K, M, 8, 2, 2, false, 1>(a, s); else return false;
         default: return false;

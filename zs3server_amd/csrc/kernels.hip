@@ -1066,6 +1066,15 @@ static hipError_t run_encode_fast(const EncArgs& a, hipStream_t s) {
             const int v = env_variant();
             if (v > 0) done = launch_variant<K, M>(v, a, s);
         }
+        if constexpr (K == 8 && M == 4) {
+            // Default RS(8+4): fused_v2 with 16 stripes per workgroup, i.e. one
+            // workgroup of 12 waves per CU in one barrier domain (variant 80).  With
+            // 4 independent workgroups per CU, oldest-first issue let the first finish
+            // in ~0.7 ms and the last in ~1.6 ms (per-wave stamps, scripts/stamps3.py),
+            // leaving CUs under-occupied for half the launch; one workgroup per CU
+            // keeps all of a CU's waves in lockstep (1.42 -> 1.31 ms).
+            if (!done && a.dyb == M && a.n_blocks >= 16 * 256) done = launch_ehx(80, a, s);
+        }
         if (!done) {
             // Tuned defaults (scripts/sweep_variants.py on MI355X, profiles/r01):
             // 8-byte columns so every thread encodes, one 384-byte tile per step.

@@ -24,7 +24,7 @@ fetch = per_kernel(sys.argv[1], "FETCH_SIZE")
 write = per_kernel(sys.argv[2], "WRITE_SIZE")
 out = {}
 for name in fetch:
-    if "encode" not in name:
+    if "encode" not in name and "k_ehx" not in name:
         continue
     f = sum(fetch[name]) / len(fetch[name])
     w = sum(write.get(name, [0])) / max(1, len(write.get(name, [0])))

@@ -72,6 +72,68 @@ __global__ void __launch_bounds__(192) k_defer(uint8_t* buf) {
     }
 }
 
+// Lockstep G4/NT192/CW8 (T384) with PF tiles of loads in flight (register ring).
+template <int PF>
+__global__ void __launch_bounds__(192) k_lockpf(uint8_t* buf) {
+    typedef V<8>::t VT;
+    constexpr int G = 4, NT = 192, CW = 8, CPB = NT / G, T = CPB * CW;
+    constexpr int64_t NST = S / T / PF * PF;  // whole PF-groups of full tiles
+    const int g = threadIdx.x / CPB, o = (threadIdx.x % CPB) * CW;
+    uint8_t* base = buf + ((int64_t)blockIdx.x * G + g) * STRIDE + o;
+    VT x[PF][K];
+#pragma unroll
+    for (int p = 0; p < PF; ++p)
+        for (int j = 0; j < K; ++j) x[p][j] = *reinterpret_cast<const VT*>(base + j * S + p * T);
+    for (int64_t s0 = 0; s0 < NST; s0 += PF) {
+#pragma unroll
+        for (int p = 0; p < PF; ++p) {
+            const int64_t t0 = (s0 + p) * T;
+            VT p0 = x[p][0] ^ x[p][1], p1 = x[p][2] ^ x[p][3], p2 = x[p][4] ^ x[p][5], p3 = x[p][6] ^ x[p][7];
+            if (s0 + p + PF < NST)
+                for (int j = 0; j < K; ++j) x[p][j] = *reinterpret_cast<const VT*>(base + j * S + t0 + PF * T);
+            *reinterpret_cast<VT*>(base + (K + 0) * S + t0) = p0;
+            *reinterpret_cast<VT*>(base + (K + 1) * S + t0) = p1;
+            *reinterpret_cast<VT*>(base + (K + 2) * S + t0) = p2;
+            *reinterpret_cast<VT*>(base + (K + 3) * S + t0) = p3;
+            __syncthreads();
+        }
+    }
+}
+
+// Lockstep G4/NT192/CW8 (T384) with a runtime stripe stride (layout skew probe).
+template <int POL>
+__device__ __forceinline__ void st8(uint8_t* p, V<8>::t v) {
+    if constexpr (POL == 0) {
+        *reinterpret_cast<V<8>::t*>(p) = v;
+    } else if constexpr (POL == 1) {
+        __builtin_nontemporal_store(v, reinterpret_cast<V<8>::t*>(p));
+    } else if constexpr (POL == 2) {
+        asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+    } else {
+        asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+    }
+}
+
+template <int POL = 0>
+__global__ void __launch_bounds__(192) k_lockskew(uint8_t* buf, int64_t stride) {
+    typedef V<8>::t VT;
+    constexpr int G = 4, NT = 192, CW = 8, CPB = NT / G, T = CPB * CW;
+    const int g = threadIdx.x / CPB, o = (threadIdx.x % CPB) * CW;
+    uint8_t* base = buf + ((int64_t)blockIdx.x * G + g) * stride + o;
+    VT x[K];
+    for (int j = 0; j < K; ++j) x[j] = *reinterpret_cast<const VT*>(base + j * S);
+    for (int64_t t0 = 0; t0 + T <= S; t0 += T) {
+        VT p0 = x[0] ^ x[1], p1 = x[2] ^ x[3], p2 = x[4] ^ x[5], p3 = x[6] ^ x[7];
+        if (t0 + 2 * T <= S)
+            for (int j = 0; j < K; ++j) x[j] = *reinterpret_cast<const VT*>(base + j * S + t0 + T);
+        st8<POL>(base + (K + 0) * S + t0, p0);
+        st8<POL>(base + (K + 1) * S + t0, p1);
+        st8<POL>(base + (K + 2) * S + t0, p2);
+        st8<POL>(base + (K + 3) * S + t0, p3);
+        __syncthreads();
+    }
+}
+
 // encode_only-style: grid (S / (256*16), NOBJ), one 16-B column per thread.
 __global__ void __launch_bounds__(256) k_stream(uint8_t* buf) {
     typedef V<16>::t VT;
@@ -109,14 +171,27 @@ static void timeit(const char* name, F launch) {
 }
 
 template <int G, int NT, int CW, bool BAR, int MAP = 0>
-static void lock(const char* name, uint8_t* d) {
-    timeit(name, [&] { hipLaunchKernelGGL((k_lockstep<G, NT, CW, BAR, MAP>), dim3(NOBJ / G), dim3(NT), 0, 0, d); });
+static void lock(const char* name, uint8_t* d, int lds = 0) {
+    if (lds > 65536)
+        (void)hipFuncSetAttribute((const void*)k_lockstep<G, NT, CW, BAR, MAP>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    timeit(name, [&] { hipLaunchKernelGGL((k_lockstep<G, NT, CW, BAR, MAP>), dim3(NOBJ / G), dim3(NT), lds, 0, d); });
 }
 
 int main() {
     uint8_t* d;
-    if (hipMalloc(&d, NOBJ * STRIDE) != hipSuccess) return 1;
-    hipMemset(d, 1, NOBJ * STRIDE);
+    const int64_t maxskew = 1 << 20;
+    if (hipMalloc(&d, NOBJ * (STRIDE + maxskew)) != hipSuccess) return 1;
+    (void)hipMemset(d, 1, NOBJ * (STRIDE + maxskew));
+    for (int64_t skew : {(int64_t)0, (int64_t)256, (int64_t)4096, (int64_t)4096 + 384, (int64_t)65536 + 4096 + 640,
+                         (int64_t)(1 << 20)}) {
+        char nm[64];
+        snprintf(nm, sizeof nm, "lockskew +%lld", (long long)skew);
+        timeit(nm, [&] { hipLaunchKernelGGL(k_lockskew<0>, dim3(NOBJ / 4), dim3(192), 0, 0, d, STRIDE + skew); });
+    }
+    timeit("lock stores nt", [&] { hipLaunchKernelGGL(k_lockskew<1>, dim3(NOBJ / 4), dim3(192), 0, 0, d, STRIDE); });
+    timeit("lock stores sc1", [&] { hipLaunchKernelGGL(k_lockskew<2>, dim3(NOBJ / 4), dim3(192), 0, 0, d, STRIDE); });
+    timeit("lock stores sc0 sc1", [&] { hipLaunchKernelGGL(k_lockskew<3>, dim3(NOBJ / 4), dim3(192), 0, 0, d, STRIDE); });
     timeit("stream (encode_only shape)", [&] { hipLaunchKernelGGL(k_stream, dim3(S / 4096, NOBJ), dim3(256), 0, 0, d); });
     lock<4, 192, 8, false>("lock G4 NT192 CW8 (T384)", d);
     timeit("defer N1", [&] { hipLaunchKernelGGL(k_defer<1>, dim3(NOBJ / 4), dim3(192), 0, 0, d); });
@@ -125,6 +200,17 @@ int main() {
     timeit("defer N8", [&] { hipLaunchKernelGGL(k_defer<8>, dim3(NOBJ / 4), dim3(192), 0, 0, d); });
     timeit("defer N16", [&] { hipLaunchKernelGGL(k_defer<16>, dim3(NOBJ / 4), dim3(192), 0, 0, d); });
     lock<4, 192, 8, true>("lock G4 NT192 CW8 (T384) bar", d);
+    timeit("lockpf PF1 bar", [&] { hipLaunchKernelGGL(k_lockpf<1>, dim3(NOBJ / 4), dim3(192), 0, 0, d); });
+    timeit("lockpf PF2 bar", [&] { hipLaunchKernelGGL(k_lockpf<2>, dim3(NOBJ / 4), dim3(192), 0, 0, d); });
+    timeit("lockpf PF3 bar", [&] { hipLaunchKernelGGL(k_lockpf<3>, dim3(NOBJ / 4), dim3(192), 0, 0, d); });
+    timeit("lockpf PF4 bar", [&] { hipLaunchKernelGGL(k_lockpf<4>, dim3(NOBJ / 4), dim3(192), 0, 0, d); });
+    timeit("lockpf PF6 bar", [&] { hipLaunchKernelGGL(k_lockpf<6>, dim3(NOBJ / 4), dim3(192), 0, 0, d); });
+    lock<1, 256, 16, false>("window G1 T4096 2/CU (512 live)", d, 80 * 1024);
+    lock<1, 256, 16, false>("window G1 T4096 1/CU (256 live)", d, 150 * 1024);
+    lock<1, 256, 16, false>("window G1 T4096 4/CU (1024 live)", d, 40 * 1024);
+    lock<1, 256, 16, false>("window G1 T4096 8/CU (2048 live)", d, 20 * 1024);
+    lock<4, 192, 8, true>("lock G4 T384 2/CU (2048 live)", d, 80 * 1024);
+    lock<4, 192, 8, true>("lock G4 T384 1/CU (1024 live)", d, 150 * 1024);
     lock<4, 192, 8, true, 1>("lock ... bar map spread", d);
     lock<4, 192, 8, true, 2>("lock ... bar map xcd-contig", d);
     lock<1, 64, 16, true, 2>("lock G1 NT64 bar xcd-contig", d);

@@ -194,7 +194,9 @@ __global__ void __launch_bounds__(4 * G * (K + M)) __attribute__((amdgpu_waves_p
         for (int j = 0; j < K; ++j) xs[j] = to_col<NWd>(xr[j]);
         if constexpr (ABL & 2) {
 #pragma unroll
-            for (int r = 0; r < M; ++r) par[r] = xs[r];
+            for (int r = 0; r < M; ++r)
+#pragma unroll
+                for (int w = 0; w < NWd; ++w) par[r].w[w] = xs[r].w[w] ^ xs[r + M].w[w];
         } else {
             encode_dyadic<NWd, K, M, !PIPE>(xs, par, tabs);
         }
@@ -450,6 +452,9 @@ static bool launch_ehx_km(int v, const EncArgs& a, hipStream_t s) {
         case 83: if constexpr (deep) return launch_ehx_t<K, M, 8, 2, 2, false, 0, false, 4>(a, s); else return false;
         case 84: if constexpr (deep) return launch_ehx_t<K, M, 8, 1, 2, false, 0, false, 2>(a, s); else return false;
         case 85: if constexpr (deep) return launch_ehx_t<K, M, 8, 1, 2, false, 0, true, 4>(a, s); else return false;
+        case 86: if constexpr (deep) return launch_ehx_t<K, M, 8, 1, 2, false, 1, false, 4>(a, s); else return false;
+        case 87: if constexpr (deep) return launch_ehx_t<K, M, 8, 1, 2, false, 2, false, 4>(a, s); else return false;
+        case 88: if constexpr (deep) return launch_ehx_t<K, M, 8, 1, 2, false, 3, false, 4>(a, s); else return false;
         case 61: if constexpr (deep) return launch_ehx_t<K, M, 8, 1, 2, false, 1>(a, s); else return false;
         case 64: if constexpr (deep) return launch_ehx_t<K, M, 8, 2, 2, false, 1>(a, s); else return false;
         default: return false;

@@ -794,21 +794,29 @@ __global__ void __launch_bounds__(256) k_hash_batch(HashArgs a) {
 // the rebuilt rows so a heal can write them with fresh sums (erasure-healing.go).
 // Layout as k_encode_hash: G stripes per workgroup, T-byte tiles, each thread one
 // CW-byte column, survivors (+ rebuilt rows) staged in LDS, one quad per hashed row.
-template <int K, int EMAX, bool HOUT>
+// GX > 0 overrides the stripes per workgroup: with GX = 16 on a 4096-stripe batch the
+// launch is one workgroup per CU (LDS padded so no two share a CU), all of a CU's
+// waves in one barrier domain -- independent workgroups sharing a CU progress at very
+// different rates under oldest-first issue and leave the CU under-occupied at the end
+// (the fused encode kernel's finding, fused_v2.hip / scripts/stamps3.py).
+template <int K, int EMAX, bool HOUT, int GX = 0>
 struct VrShape {
     static constexpr int RH = K + (HOUT ? EMAX : 0);  // hashed rows per stripe
-    static constexpr int G = (256 / (4 * RH)) > 0 ? 256 / (4 * RH) : 1;
+    static constexpr int G = GX > 0 ? GX : ((256 / (4 * RH)) > 0 ? 256 / (4 * RH) : 1);
     static constexpr int NT = round64(4 * G * RH);
     static constexpr int T = 256, CW = 8;
+    static constexpr int TS = T + 32;
+    static constexpr size_t TILE = (size_t)G * RH * TS;
 };
 
-template <int K, int EMAX, bool HOUT>
-__global__ void __launch_bounds__((VrShape<K, EMAX, HOUT>::NT)) k_verify_reconstruct(VrArgs a) {
-    using Sh = VrShape<K, EMAX, HOUT>;
+template <int K, int EMAX, bool HOUT, int GX = 0>
+__global__ void __launch_bounds__((VrShape<K, EMAX, HOUT, GX>::NT)) k_verify_reconstruct(VrArgs a) {
+    using Sh = VrShape<K, EMAX, HOUT, GX>;
     constexpr int RH = Sh::RH, G = Sh::G, NT = Sh::NT, T = Sh::T, CW = Sh::CW;
     constexpr int NWd = CW / 4, TS = T + 32, CPB = T / CW, NCOL = G * CPB;
     constexpr int CPT = (NCOL + NT - 1) / NT;
-    __shared__ __attribute__((aligned(16))) uint8_t tile[G * RH * TS];
+    extern __shared__ __attribute__((aligned(16))) uint8_t vr_smem[];
+    uint8_t* tile = vr_smem;  // [G * RH][TS], dynamic (may be padded to limit occupancy)
     __shared__ __attribute__((aligned(16))) uint32_t tabs[(EMAX > 0 ? EMAX : 1) * K * 8];
     __shared__ int32_t srows[K + EMAX];
     const int tid = threadIdx.x;
@@ -1177,9 +1185,32 @@ hipError_t launch_reconstruct(const RecArgs& a, hipStream_t s, bool* used_fast) 
 
 template <int K, int EMAX, bool HOUT>
 static hipError_t run_vr(const VrArgs& a, hipStream_t s) {
+    // Variant 201 (diagnostics): 16 stripes per workgroup, one workgroup per CU (LDS
+    // >= 80 KiB + 1).  Measured SLOWER than the default on RS(8+4) 4096 x 1 MiB
+    // (verify 1.09 vs 0.84 ms, verify+rebuild 1.57 vs 1.40, heal 1.69 vs 1.50;
+    // scripts/get_ab.py): at 2 waves per SIMD this kernel, unlike the encode, is short of
+    // loads in flight, and the default's two workgroups per CU already balance.
+    using Big = VrShape<K, EMAX, HOUT, 16>;
+    if constexpr (Big::NT <= 1024) {
+        if (a.n_blocks >= 16 * 256 && g_variant == 201) {
+            auto kern = k_verify_reconstruct<K, EMAX, HOUT, 16>;
+            constexpr size_t dyn = Big::TILE > 82 * 1024 ? Big::TILE : 82 * 1024;
+            static bool attr = false;
+            if (!attr) {
+                hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                   (int)dyn);
+                if (e != hipSuccess) return e;
+                attr = true;
+            }
+            const int64_t grid = (a.n_blocks + Big::G - 1) / Big::G;
+            hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(Big::NT), dyn, s, a);
+            return hipGetLastError();
+        }
+    }
     using Sh = VrShape<K, EMAX, HOUT>;
+    static_assert(Sh::TILE <= 65536, "default GET tile fits the default LDS limit");
     const int64_t grid = (a.n_blocks + Sh::G - 1) / Sh::G;
-    hipLaunchKernelGGL((k_verify_reconstruct<K, EMAX, HOUT>), dim3((unsigned)grid), dim3(Sh::NT), 0, s, a);
+    hipLaunchKernelGGL((k_verify_reconstruct<K, EMAX, HOUT>), dim3((unsigned)grid), dim3(Sh::NT), Sh::TILE, s, a);
     return hipGetLastError();
 }
 

@@ -180,11 +180,11 @@ static void lock(const char* name, uint8_t* d, int lds = 0) {
 
 int main() {
     uint8_t* d;
-    const int64_t maxskew = 1 << 20;
+    const int64_t maxskew = 2 << 20;
     if (hipMalloc(&d, NOBJ * (STRIDE + maxskew)) != hipSuccess) return 1;
     (void)hipMemset(d, 1, NOBJ * (STRIDE + maxskew));
-    for (int64_t skew : {(int64_t)0, (int64_t)256, (int64_t)4096, (int64_t)4096 + 384, (int64_t)65536 + 4096 + 640,
-                         (int64_t)(1 << 20)}) {
+    for (int64_t skew : {(int64_t)0, (int64_t)4096, (int64_t)65536, (int64_t)131072, (int64_t)262144,
+                         (int64_t)524288, (int64_t)(1 << 20), (int64_t)(3 << 19), (int64_t)(2 << 20), (int64_t)0}) {
         char nm[64];
         snprintf(nm, sizeof nm, "lockskew +%lld", (long long)skew);
         timeit(nm, [&] { hipLaunchKernelGGL(k_lockskew<0>, dim3(NOBJ / 4), dim3(192), 0, 0, d, STRIDE + skew); });

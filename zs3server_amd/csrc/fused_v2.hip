@@ -227,50 +227,32 @@ __global__ void __launch_bounds__(4 * G * (K + M)) __attribute__((amdgpu_waves_p
                 hh_update(st, w[i], sel);
         }
     };
-    auto prefetch = [&](VT (&xs)[K], int64_t tn) {
-        if (tn < nfull)
-            load(xs, tn * T);
-        else if (tn == nfull && tail)
-            load_tail(xs, tn * T);
+    // Branch-free prefetch for the edge steps: a tile past the end (or a tail column
+    // past the tail) re-reads tile 0 of its own row, so x is defined on every path (no
+    // phi copies of in-flight registers) and the value is unused.
+    auto prefetch_any = [&](VT (&xs)[K], int64_t tn) {
+        const bool ok = tn < nfull || (tn == nfull && o < tail);
+        load(xs, ok ? tn * T : 0);
     };
-    // One step on full tile ti held in xs: encode into LDS, issue the loads of tile
-    // ti+PF into the freed registers (UNC: known to be a full tile, no branch), then
-    // the parity stores, barrier, hash.
+    // Steady-state step on full tile ti held in xs (tile ti+PF known full): encode
+    // into LDS, issue the loads of tile ti+PF into the freed registers, then the
+    // parity stores, barrier, hash.
     // Before encode(ti) the wave's pending vector-memory ops are, oldest first:
     // loads(ti), stores(ti-PF), loads(ti+1), stores(ti-PF+1), ..., loads(ti+PF-1),
     // stores(ti-1).  Steady state waits for loads(ti) only: vmcnt(M + (PF-1)*(K+M)).
-    // Peeled/conditional steps wait for everything.
-    auto step = [&](VT (&xs)[K], int64_t ti, auto unc) {
+    // Edge steps (below) wait for everything.
+    auto step = [&](VT (&xs)[K], int64_t ti) {
         set_prio(ti);
         uint8_t* tl = tile[NBUF == 1 ? 0 : (ti & 1)];
         Col<NWd> par[M];
-        if constexpr (decltype(unc)::value)
-            vm_wait<M + (PF - 1) * (K + M)>(xs);
-        else
-            vm_wait<0>(xs);
+        vm_wait<M + (PF - 1) * (K + M)>(xs);
         encode(xs, tl, par);
-        if constexpr (decltype(unc)::value)
-            load(xs, (ti + PF) * T);
-        else
-            prefetch(xs, ti + PF);
+        load(xs, (ti + PF) * T);
         store_par(par, ti * T);
         lds_barrier2();
         hash_full(tl);
         if (NBUF == 1) lds_barrier2();
     };
-    auto tail_step = [&](VT (&xs)[K]) {
-        uint8_t* tl = tile[NBUF == 1 ? 0 : (nfull & 1)];
-        Col<NWd> par[M];
-        vm_wait<0>(xs);
-        encode(xs, tl, par);
-        if (o < tail) store_par(par, nfull * T);
-        lds_barrier2();
-        const uint8_t* row = tl + chain * TS;
-        hh_packets(st, row, tail >> 5, lane, sel);
-        if (tail & 31) hh_remainder(st, row + (tail & ~31), (uint32_t)(tail & 31), lane, sel);
-    };
-    using Unc = std::integral_constant<bool, true>;
-    using Cnd = std::integral_constant<bool, false>;
 
     if constexpr (PIPE) {
         static_assert(NBUF == 2, "pipelined body double-buffers the LDS tile");
@@ -303,13 +285,6 @@ __global__ void __launch_bounds__(4 * G * (K + M)) __attribute__((amdgpu_waves_p
             store_par(par, ti * T);
             hash_apply(w);
             lds_barrier2();
-        };
-        // Branch-free prefetch for the edge steps: a tile past the end (or a tail
-        // column past the tail) re-reads tile 0 of its own row, so x is defined on
-        // every path (no phi copies of in-flight registers) and the value is unused.
-        auto prefetch_any = [&](VT (&xs)[K], int64_t tn) {
-            const bool ok = tn < nfull || (tn == nfull && o < tail);
-            load(xs, ok ? tn * T : 0);
         };
         // any step ti >= 0: hash tile ti-1 if it is a full tile, encode tile ti if it
         // exists (full or tail); always prefetch tile ti+PF and hit the barrier.
@@ -347,32 +322,44 @@ __global__ void __launch_bounds__(4 * G * (K + M)) __attribute__((amdgpu_waves_p
             if (tail & 31) hh_remainder(st, row + (tail & ~31), (uint32_t)(tail & 31), lane, sel);
         }
     } else {
+        // Any step ti >= 0 outside the steady state: encode tile ti if it exists (full
+        // or tail), always prefetch tile ti+PF (branch-free), barrier, hash what was
+        // encoded.  Every wave runs every edge step, so barriers stay matched.
+        auto edge = [&](VT (&xs)[K], int64_t ti) {
+            uint8_t* tl = tile[NBUF == 1 ? 0 : (ti & 1)];
+            const bool full = ti < nfull, part = ti == nfull && tail;
+            vm_wait<0>(xs);
+            Col<NWd> par[M];
+            if (full || part) encode(xs, tl, par);
+            prefetch_any(xs, ti + PF);
+            if (full || (part && o < tail)) store_par(par, ti * T);
+            lds_barrier2();
+            if (full) {
+                hash_full(tl);
+            } else if (part) {
+                const uint8_t* row = tl + chain * TS;
+                hh_packets(st, row, tail >> 5, lane, sel);
+                if (tail & 31) hh_remainder(st, row + (tail & ~31), (uint32_t)(tail & 31), lane, sel);
+            }
+            if (NBUF == 1) lds_barrier2();
+        };
         lds_barrier2();  // tables visible
     #pragma unroll
-        for (int p = 0; p < PF; ++p) prefetch(x[p], p);
-        // Peeled first PF steps: the steady-state loop is entered with the same pending
-        // vector-memory ops as its back edge (loads of the next tiles, then stores), so
-        // the compiler's vmcnt before each encode leaves the parity stores in flight.
+        for (int p = 0; p < PF; ++p) prefetch_any(x[p], p);
     #pragma unroll
-        for (int p = 0; p < PF; ++p)
-            if (p < nfull) step(x[p], p, Cnd{});
+        for (int p = 0; p < PF; ++p) edge(x[p], p);
         int64_t i = PF;
-        // Drain once before the steady state: its in-loop vmcnt counts then only have to
-        // hold for the loop's own issue order (and scripts/check_async_loads.py can prove
-        // it without path-sensitive reasoning about the peeled steps).
+        // Drain once before the steady state and once after it: the in-loop vmcnt counts
+        // then only have to hold for the loop's own issue order (and
+        // scripts/check_async_loads.py can prove it without path-sensitive reasoning).
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         for (; i + 2 * PF <= nfull; i += PF) {
     #pragma unroll
-            for (int p = 0; p < PF; ++p) step(x[p], i + p, Unc{});
+            for (int p = 0; p < PF; ++p) step(x[p], i + p);
         }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     #pragma unroll
-        for (int p = 0; p < 2 * PF; ++p)
-            if (i + p < nfull) step(x[p % PF], i + p, Cnd{});
-        if (tail) {
-    #pragma unroll
-            for (int p = 0; p < PF; ++p)
-                if (nfull % PF == p) tail_step(x[p]);
-        }
+        for (int p = 0; p < 2 * PF; ++p) edge(x[p % PF], i + p);
 
     }
 
@@ -438,7 +425,13 @@ static bool launch_ehx_t(const EncArgs& a, hipStream_t s) {
 template <int K, int M>
 static bool launch_ehx_km(int v, const EncArgs& a, hipStream_t s) {
     constexpr bool deep = K == 8 && M == 4;
+    constexpr bool few = K == 4 && M == 2;  // BASELINE config 2: 1024 objects, latency-bound
     switch (v) {
+        case 90: if constexpr (few) return launch_ehx_t<K, M, 8, 4, 2, false, 0, false, 1, false, 83968>(a, s); else return false;
+        case 91: if constexpr (few) return launch_ehx_t<K, M, 8, 4, 2, false, 0, true, 1, false, 83968>(a, s); else return false;
+        case 92: if constexpr (few) return launch_ehx_t<K, M, 8, 2, 2, false, 0, false, 1, false, 83968>(a, s); else return false;
+        case 93: if constexpr (few) return launch_ehx_t<K, M, 8, 4, 2>(a, s); else return false;
+        case 94: if constexpr (few) return launch_ehx_t<K, M, 8, 8, 2, false, 0, false, 1, false, 83968>(a, s); else return false;
         case 50: return launch_ehx_t<K, M, 8, 1, 2>(a, s);
         case 51: return launch_ehx_t<K, M, 8, 1, 1>(a, s);
         case 52: if constexpr (deep) return launch_ehx_t<K, M, 8, 2, 2>(a, s); else return false;

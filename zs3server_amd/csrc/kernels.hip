@@ -1083,6 +1083,14 @@ static hipError_t run_encode_fast(const EncArgs& a, hipStream_t s) {
             // keeps all of a CU's waves in lockstep (1.42 -> 1.31 ms).
             if (!done && a.dyb == M && a.n_blocks >= 16 * 256) done = launch_ehx(80, a, s);
         }
+        if constexpr (K == 4 && M == 2) {
+            // Default RS(4+2) for batches of at most one 8-stripe workgroup per CU
+            // (BASELINE config 2, 1024 objects: 6144 hash chains, one wave per SIMD on
+            // 128 CUs, latency-bound): fused_v2 variant 91 = pipelined body (encode of
+            // tile i beside the hash of tile i-1), 4 tiles of loads in flight, one
+            // workgroup per CU.  1.03 -> 0.84 ms (scripts/box_sweep.sh).
+            if (!done && a.dyb == M && a.n_blocks <= 8 * 256) done = launch_ehx(91, a, s);
+        }
         if (!done) {
             // Tuned defaults (scripts/sweep_variants.py on MI355X, profiles/r01):
             // 8-byte columns so every thread encodes, one 384-byte tile per step.

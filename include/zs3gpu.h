@@ -143,6 +143,30 @@ int zs3_hh256_verify_batch(const uint8_t* h_key, const uint8_t* d_msgs, int64_t 
                            int64_t msg_len, int64_t n_msgs, const uint8_t* d_want,
                            int32_t* d_bad, void* stream);
 
+/* ---- PUT-stream object digests ------------------------------- */
+
+/* S3 ETag of n_msgs objects: MD5 (RFC 1321, Go crypto/md5) of message i = d_msgs +
+ * i*msg_stride, length d_lens[i] (device int64 array) or msg_len when d_lens is NULL.
+ * Digest i (16 bytes) at d_out + 16*i.  Replaces etag.NewReader's md5.Write/Sum
+ * (internal/etag/reader.go:106-144). */
+int zs3_md5_batch(const uint8_t* d_msgs, int64_t msg_stride, int64_t msg_len, const int64_t* d_lens,
+                  int64_t n_msgs, uint8_t* d_out, void* stream);
+
+/* SHA-256 (FIPS 180-4, sha256-simd) of the same message layout; digest i (32 bytes,
+ * big-endian) at d_out + 32*i.  Replaces hash.Reader's content SHA-256 checked at
+ * EOF (internal/hash/reader.go:123-153). */
+int zs3_sha256_batch(const uint8_t* d_msgs, int64_t msg_stride, int64_t msg_len, const int64_t* d_lens,
+                     int64_t n_msgs, uint8_t* d_out, void* stream);
+
+/* etag.Multipart (internal/etag/etag.go:211-226): h_etags holds n_etags ETags,
+ * etag i at h_etags + offsets[i] with length lens[i] (16 = singlepart MD5; longer =
+ * multipart "-N" or encrypted, both skipped as the reference skips them).  Writes
+ * MD5(concatenated singlepart ETags) followed by "-<count>" to h_out (capacity >= 40)
+ * and returns its length; returns 0 (nil ETag) when n_etags == 0.  The MD5 runs on
+ * the device (zs3_md5_batch). */
+int zs3_etag_multipart(const uint8_t* h_etags, const int64_t* offsets, const int64_t* lens, int64_t n_etags,
+                       uint8_t* h_out);
+
 /* Deterministic synthetic blocks (splitmix64 counter stream; identical to the
  * oracle's fill): block b gets object id obj0 + b. */
 int zs3_fill_batch(uint8_t* d_out, int64_t stride, int64_t len, int64_t n_blocks,

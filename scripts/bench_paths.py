@@ -73,6 +73,20 @@ bad = torch.empty(nobj * (k + m), dtype=torch.int32, device="cuda")
 ms = timeit(lambda: z.hh256_verify_batch(buf, S, S, nobj * (k + m), sums, bad))
 out(path="hh256_verify_batch", msgs=nobj * (k + m), msg_len=S, ms=round(ms, 4),
     hbm_GBps=round(nobj * (k + m) * S / ms / 1e6, 1), bad=int(bad.sum()))
+# ---- PUT-stream object digests: S3 ETag (MD5) and content SHA-256
+# of 4096 x 1 MiB device-resident objects, one lane per object (serial chains)
+for name, fn, width in (("md5_batch", z.md5_batch, 16), ("sha256_batch", z.sha256_batch, 32)):
+    dout = torch.empty(nobj * width, dtype=torch.uint8, device="cuda")
+    ms = timeit(lambda: fn(buf, stride, blen, nobj, dout), steps=3)
+    out(path=name, objects=nobj, object_bytes=blen, ms=round(ms, 3),
+        GiBps=round(nobj * blen / ms / 1e-3 / 2**30, 1))
+import hashlib  # noqa: E402
+sample = np.frombuffer(os.urandom(64 << 20), dtype=np.uint8)
+for name, h in (("md5_cpu_1thread", hashlib.md5), ("sha256_cpu_1thread", hashlib.sha256)):
+    t0 = time.perf_counter()
+    h(sample.tobytes()).digest()
+    dt = time.perf_counter() - t0
+    out(path=name, bytes=len(sample), GiBps=round(len(sample) / dt / 2**30, 2))
 del buf, sums, bad
 torch.cuda.empty_cache()
 

@@ -41,7 +41,7 @@ EXPORTS = [
     "zs3_encode_batch", "zs3_reconstruct_batch", "zs3_verify_reconstruct_batch", "zs3_hh256_batch",
     "zs3_hh256_verify_batch",
     "zs3_fill_batch", "zs3_encode_data", "zs3_decode_data_blocks", "zs3_hh256", "zs3_selftest",
-    "zs3_stream_encode",
+    "zs3_stream_encode", "zs3_md5_batch", "zs3_sha256_batch", "zs3_etag_multipart",
     "zs3_last_path", "zs3_debug_set_variant", "zs3_debug_set_buffer",
 ]
 
@@ -94,6 +94,9 @@ def lib():
     L.zs3_set_device.argtypes = [C.c_int]
     L.zs3_stream_encode.argtypes = [vp, vp, i64, vp, vp, i64]
     L.zs3_stream_encode.restype = i64
+    L.zs3_md5_batch.argtypes = [vp, i64, i64, vp, i64, vp, vp]
+    L.zs3_sha256_batch.argtypes = [vp, i64, i64, vp, i64, vp, vp]
+    L.zs3_etag_multipart.argtypes = [vp, vp, vp, i64, vp]
     L.zs3_host_alloc.argtypes = [C.POINTER(vp), C.c_size_t]
     L.zs3_host_free.argtypes = [vp]
     _L = L
@@ -250,6 +253,37 @@ def hh256_verify_batch(msgs, msg_stride: int, msg_len: int, n_msgs: int, want, b
     kb = C.create_string_buffer(key, 32) if key else None
     _check(lib().zs3_hh256_verify_batch(kb, _ptr(msgs, offset), msg_stride, msg_len, n_msgs, _ptr(want),
                                         _ptr(bad), _stream(stream)), "hh256_verify_batch")
+
+
+def md5_batch(msgs, msg_stride: int, msg_len: int, n_msgs: int, out, lens=None, offset: int = 0,
+              stream=None) -> None:
+    """S3 ETag (MD5) of n device messages (zs3_md5_batch); `lens` = optional device int64
+    per-message lengths; digest i at out[16*i : 16*i+16]."""
+    _check(lib().zs3_md5_batch(_ptr(msgs, offset), msg_stride, msg_len, _ptr(lens), n_msgs, _ptr(out),
+                               _stream(stream)), "md5_batch")
+
+
+def sha256_batch(msgs, msg_stride: int, msg_len: int, n_msgs: int, out, lens=None, offset: int = 0,
+                 stream=None) -> None:
+    """Content SHA-256 of n device messages (zs3_sha256_batch); digest i at out[32*i:]."""
+    _check(lib().zs3_sha256_batch(_ptr(msgs, offset), msg_stride, msg_len, _ptr(lens), n_msgs, _ptr(out),
+                                  _stream(stream)), "sha256_batch")
+
+
+def etag_multipart(etags) -> bytes:
+    """etag.Multipart (internal/etag/etag.go:211-226) over a list of raw ETag byte
+    strings; returns b"" (the nil ETag) for an empty list."""
+    import numpy as np
+    n = len(etags)
+    if n == 0:
+        return b""
+    cat = np.frombuffer(b"".join(etags) or b"\0", dtype=np.uint8).copy()
+    lens = np.array([len(e) for e in etags], dtype=np.int64)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+    out = np.zeros(48, dtype=np.uint8)
+    r = _check(lib().zs3_etag_multipart(cat.ctypes.data, offs.ctypes.data, lens.ctypes.data, n, out.ctypes.data),
+               "etag_multipart")
+    return out[:r].tobytes()
 
 
 def fill_batch(out, stride: int, length: int, n_blocks: int, seed: int = 0, obj0: int = 0,

@@ -72,11 +72,24 @@ struct VrArgs {
     uint64_t key[4];
 };
 
+// Batched MD5 / SHA-256 (digest.hip): message i of lens[i] (or len) bytes at
+// msgs + i*stride; digest i at out + i*16 (MD5) or out + i*32 (SHA-256).
+struct DigestArgs {
+    const uint8_t* msgs;
+    int64_t stride;
+    int64_t len;
+    const int64_t* lens;      // optional per-message lengths (device)
+    int64_t n;
+    uint8_t* out;
+};
+
 // Returns hipSuccess or an error from the launch.
 hipError_t launch_encode(const EncArgs& a, hipStream_t s, bool* used_fast);
 hipError_t launch_reconstruct(const RecArgs& a, hipStream_t s, bool* used_fast);
 hipError_t launch_verify_reconstruct(const VrArgs& a, hipStream_t s, bool* used_fast);
 hipError_t launch_hash(const HashArgs& a, hipStream_t s);
+hipError_t launch_md5(const DigestArgs& a, hipStream_t s);
+hipError_t launch_sha256(const DigestArgs& a, hipStream_t s);
 hipError_t launch_fill(uint8_t* out, int64_t stride, int64_t len, int64_t n, uint64_t seed,
                        uint64_t obj0, hipStream_t s);
 

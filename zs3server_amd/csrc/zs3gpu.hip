@@ -533,6 +533,59 @@ int zs3_verify_reconstruct_batch(const zs3_codec* cc, uint8_t* d_shards, int64_t
     return rc;
 }
 
+static int digest_batch(bool sha, const uint8_t* d_msgs, int64_t stride, int64_t len, const int64_t* d_lens,
+                        int64_t n, uint8_t* d_out, void* stream) {
+    if (n < 0 || (n > 0 && (!d_out || !d_msgs)) || (!d_lens && len < 0)) return ZS3_ERR_INVALID_ARG;
+    zs3k::DigestArgs a{};
+    a.msgs = d_msgs;
+    a.stride = stride;
+    a.len = len;
+    a.lens = d_lens;
+    a.n = n;
+    a.out = d_out;
+    return map_hip(sha ? zs3k::launch_sha256(a, (hipStream_t)stream) : zs3k::launch_md5(a, (hipStream_t)stream));
+}
+
+int zs3_md5_batch(const uint8_t* d_msgs, int64_t stride, int64_t len, const int64_t* d_lens, int64_t n,
+                  uint8_t* d_out, void* stream) {
+    return digest_batch(false, d_msgs, stride, len, d_lens, n, d_out, stream);
+}
+
+int zs3_sha256_batch(const uint8_t* d_msgs, int64_t stride, int64_t len, const int64_t* d_lens, int64_t n,
+                     uint8_t* d_out, void* stream) {
+    return digest_batch(true, d_msgs, stride, len, d_lens, n, d_out, stream);
+}
+
+// etag.Multipart (internal/etag/etag.go:211-226): skip multipart ("-N") and encrypted
+// (longer than 16 bytes, no '-') ETags, MD5 the concatenation of the rest on the device,
+// append '-' and the decimal count.
+int zs3_etag_multipart(const uint8_t* h_etags, const int64_t* offsets, const int64_t* lens, int64_t n,
+                       uint8_t* h_out) {
+    if (n < 0 || (n > 0 && (!h_etags || !offsets || !lens)) || !h_out) return ZS3_ERR_INVALID_ARG;
+    if (n == 0) return 0;
+    std::vector<uint8_t> cat;
+    int64_t count = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        if (lens[i] < 0) return ZS3_ERR_INVALID_ARG;
+        if (lens[i] > 16) continue;  // IsMultipart or IsEncrypted (etag.go:145-155)
+        cat.insert(cat.end(), h_etags + offsets[i], h_etags + offsets[i] + lens[i]);
+        ++count;
+    }
+    uint8_t* d = nullptr;
+    const size_t bytes = cat.size() + 16;
+    if (hipMalloc(&d, bytes) != hipSuccess) return ZS3_ERR_NOMEM;
+    int rc = ZS3_OK;
+    if (!cat.empty()) rc = map_hip(hipMemcpy(d, cat.data(), cat.size(), hipMemcpyHostToDevice));
+    if (!rc) rc = zs3_md5_batch(d, 0, (int64_t)cat.size(), nullptr, 1, d + cat.size(), nullptr);
+    if (!rc) rc = map_hip(hipMemcpy(h_out, d + cat.size(), 16, hipMemcpyDeviceToHost));
+    hipFree(d);
+    if (rc) return rc;
+    char suffix[24];
+    const int ns = snprintf(suffix, sizeof suffix, "-%lld", (long long)count);
+    memcpy(h_out + 16, suffix, (size_t)ns);
+    return 16 + ns;
+}
+
 int zs3_hh256_batch(const uint8_t* key, const uint8_t* d_msgs, int64_t stride, int64_t len, int64_t n,
                     uint8_t* d_sums, void* stream) {
     if (len < 0 || n < 0 || (n > 0 && !d_sums)) return ZS3_ERR_INVALID_ARG;

@@ -14,6 +14,9 @@ SHAPES = [tuple(int(x) for x in t.split(":")) for t in os.environ.get("SWEEP_SHA
 REPEAT = int(os.environ.get("SWEEP_REPEAT", "2"))
 VARIANTS = [int(v) for v in os.environ.get("SWEEP_VARIANTS", "0,1,2,3,4,5,6,7,8").split(",")]
 steps = int(os.environ.get("SWEEP_STEPS", "10"))
+# SWEEP_ALIAS=1: every block reads stripe 0 and writes stripe 0's parity (strides 0), so
+# the data stays in L2 and the launch measures the kernel's compute-bound time.
+ALIAS = os.environ.get("SWEEP_ALIAS", "0") == "1"
 res = []
 for k, m, nobj in SHAPES:
     blen = 1 << 20
@@ -28,7 +31,8 @@ for k, m, nobj in SHAPES:
         z.set_variant(v)
         buf.view(nobj, k + m, S)[:, k:, :] = 0
         sums.zero_()
-        codec.encode_batch(buf, stride, blen, nobj, parity=buf, parity_offset=k * S, parity_stride=stride, sums=sums)
+        st = 0 if ALIAS else stride
+        codec.encode_batch(buf, st, blen, nobj, parity=buf, parity_offset=k * S, parity_stride=st, sums=sums)
         torch.cuda.synchronize()
         sig = (int(buf.view(torch.int64).sum()), int(sums.view(torch.int64).sum()))
         if ref is None:
@@ -37,13 +41,13 @@ for k, m, nobj in SHAPES:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(steps):
-            codec.encode_batch(buf, stride, blen, nobj, parity=buf, parity_offset=k * S, parity_stride=stride, sums=sums)
+            codec.encode_batch(buf, st, blen, nobj, parity=buf, parity_offset=k * S, parity_stride=st, sums=sums)
         e1.record()
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / steps
         ab = nobj * (blen + m * S + 32 * (k + m))
         r = {"k": k, "m": m, "objects": nobj, "variant": v, "ms": round(ms, 4),
-             "GiBps": round(nobj * blen / ms / 1e-3 / 2**30, 1), "hbm_GBps": round(ab / ms / 1e6, 1), "match": ok}
+             "GiBps": round(nobj * blen / ms / 1e-3 / 2**30, 1), "hbm_GBps": round(ab / ms / 1e6, 1), "match": ok, "alias": ALIAS}
         print(json.dumps(r), flush=True)
         res.append(r)
     del buf, sums

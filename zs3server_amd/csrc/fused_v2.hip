@@ -387,6 +387,172 @@ __global__ void __launch_bounds__(4 * G * (K + M)) __attribute__((amdgpu_waves_p
     }
 }
 
+// Warp-specialised form (one workgroup per CU, G stripes): the first NH = 2*G*R threads
+// only hash, one HighwayHash chain per thread PAIR (hh256_dev.hpp pair form: no DPP and
+// a shared zipper v_perm, 16 instead of 19 VALU per lane-packet); the other NE threads
+// only encode, one 16-byte column each (dwordx4 loads/stores, half the memory
+// instructions per byte of the 8-byte form).  Step s: encode waves encode tile s into
+// LDS buffer s&1 and store its parity; hash waves hash tile s-1 from buffer (s-1)&1;
+// one barrier.  Both roles run the same number of steps, so barriers stay matched.
+// With 6 + 6 waves on 4 SIMDs the busiest SIMD carries one hash and two encode waves:
+// ~6 % less issue than three mixed waves (asm_loops.py + scripts/ubench/opcost.hip).
+template <int K, int M, int G, int T, int PF>
+__global__ void __launch_bounds__(2 * G * (K + M) + G * (T / 16)) __attribute__((amdgpu_waves_per_eu(3)))
+k_ehx_ws(EncArgs a) {
+    constexpr int R = K + M;
+    constexpr int NH = 2 * G * R;   // hash threads
+    constexpr int CPS = T / 16;     // 16-byte columns per stripe row
+    constexpr int NE = G * CPS;     // encode threads
+    constexpr int NT = NH + NE;
+    constexpr int TS = T + 16;      // b128 row reads of 4 chains hit disjoint banks
+    constexpr int NPK = T / 32;
+    constexpr int NTAB = K * 8;
+    static_assert(M == 2 || M == 4, "dyadic shapes only");
+    static_assert(NH % 64 == 0 && NE % 64 == 0 && T % 32 == 0, "whole wavefronts per role");
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem_dyn[];
+    uint8_t(*tile)[G * R * TS] = reinterpret_cast<uint8_t(*)[G * R * TS]>(smem_dyn);
+    __shared__ __attribute__((aligned(16))) uint32_t tabs[NTAB];
+
+    const int tid = threadIdx.x;
+    const int64_t blk0 = (int64_t)blockIdx.x * G;
+    const int64_t S = a.S;
+    for (int i = tid; i < NTAB; i += NT) tabs[i] = a.dtables[i];
+    const int64_t nfull = S / T;
+    const int tail = (int)(S - nfull * T);  // multiple of 16 (launch requires S % 16 == 0)
+    // Step schedule shared by both roles: PF edge steps, the steady loop in units of PF
+    // while i + 2*PF <= nfull, 2*PF edge steps, one step that only hashes.
+    int64_t iend = PF;
+    if (nfull >= 3 * PF) iend = PF + ((nfull - 3 * PF) / PF + 1) * PF;
+    const int64_t total = iend + 2 * PF + 1;
+
+    if (__builtin_amdgcn_readfirstlane(tid) < NH) {
+        // ---- hash role: lanes (2hh, 2hh+1) of chain `chain` = shard row s of stripe g
+        const int chain = tid >> 1, hh = tid & 1;
+        const int row_off = chain * TS;
+        HHPair st = hh2_init(hh, a.key[0], a.key[1], a.key[2], a.key[3]);
+        lds_barrier2();  // tables (matches the encode role)
+        lds_barrier2();  // step 0: tile 0 being encoded
+        for (int64_t s = 1; s <= nfull; ++s) {
+            const uint4* p = reinterpret_cast<const uint4*>(tile[(s - 1) & 1] + row_off) + hh;
+            uint4 w[NPK];
+#pragma unroll
+            for (int i = 0; i < NPK; ++i) w[i] = p[2 * i];
+#pragma unroll
+            for (int i = 0; i < NPK; ++i)
+                hh2_update(st, ((uint64_t)w[i].y << 32) | w[i].x, ((uint64_t)w[i].w << 32) | w[i].z);
+            lds_barrier2();
+        }
+        if (tail) {
+            const uint8_t* row = tile[nfull & 1] + row_off;
+            hh2_packets(st, row, tail >> 5, hh);
+            if (tail & 31) hh2_remainder(st, row + (tail & ~31), (uint32_t)(tail & 31), hh);
+        }
+        for (int64_t s = nfull + 1; s < total; ++s) lds_barrier2();
+        uint64_t d0, d1;
+        hh2_finalize256(st, d0, d1);
+        if (blk0 + chain / R < a.n_blocks) {
+            const int64_t bb = blk0 + chain / R;
+            uint64_t* out = reinterpret_cast<uint64_t*>(a.sums + (bb * R + chain % R) * 32 + 16 * hh);
+            out[0] = d0;
+            out[1] = d1;
+        }
+        return;
+    }
+
+    // ---- encode role: 16-byte column o of stripe g (dead stripes of the last
+    // workgroup alias the last live block and store byte-identical parity)
+    constexpr int NWd = 4;
+    typedef typename VecOf<NWd>::type VT;
+    const int e = tid - NH;
+    const int g = e / CPS, o = (e % CPS) * 16;
+    const int64_t b = (blk0 + g) < a.n_blocks ? (blk0 + g) : (a.n_blocks - 1);
+    const uint8_t* src = a.data + b * a.data_stride + o;
+    uint8_t* pdst = a.parity + b * a.parity_stride + o;
+    const int col_off = g * R * TS + o;
+
+    VT x[PF][K];
+    auto load = [&](VT (&xs)[K], int64_t t0) {
+#pragma unroll
+        for (int j = 0; j < K; ++j) ld_async<NWd>(xs[j], src + (int64_t)j * S + t0);
+    };
+    auto prefetch_any = [&](VT (&xs)[K], int64_t tn) {
+        const bool ok = tn < nfull || (tn == nfull && o < tail);
+        load(xs, ok ? tn * T : 0);
+    };
+    auto encode = [&](VT (&xr)[K], uint8_t* tl, Col<NWd> (&par)[M]) {
+        Col<NWd> xs[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) xs[j] = to_col<NWd>(xr[j]);
+        encode_dyadic<NWd, K, M>(xs, par, tabs);
+#pragma unroll
+        for (int j = 0; j < K; ++j) st_col<NWd>(tl + col_off + j * TS, xs[j]);
+#pragma unroll
+        for (int r = 0; r < M; ++r) st_col<NWd>(tl + col_off + (K + r) * TS, par[r]);
+    };
+    auto store_par = [&](const Col<NWd> (&par)[M], int64_t t0) {
+#pragma unroll
+        for (int r = 0; r < M; ++r) st_col<NWd>(pdst + (int64_t)r * S + t0, par[r]);
+    };
+    // steady step (see k_ehx): wait for loads(ti) only
+    auto step = [&](VT (&xs)[K], int64_t ti) {
+        Col<NWd> par[M];
+        vm_wait<M + (PF - 1) * (K + M)>(xs);
+        encode(xs, tile[ti & 1], par);
+        load(xs, (ti + PF) * T);
+        store_par(par, ti * T);
+        lds_barrier2();
+    };
+    auto edge = [&](VT (&xs)[K], int64_t ti) {
+        const bool full = ti < nfull, part = ti == nfull && tail;
+        vm_wait<0>(xs);
+        Col<NWd> par[M];
+        if (full || part) encode(xs, tile[ti & 1], par);
+        prefetch_any(xs, ti + PF);
+        if (full || (part && o < tail)) store_par(par, ti * T);
+        lds_barrier2();
+    };
+    lds_barrier2();  // tables visible
+#pragma unroll
+    for (int p = 0; p < PF; ++p) prefetch_any(x[p], p);
+#pragma unroll
+    for (int p = 0; p < PF; ++p) edge(x[p], p);
+    int64_t i = PF;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (; i + 2 * PF <= nfull; i += PF) {
+#pragma unroll
+        for (int p = 0; p < PF; ++p) step(x[p], i + p);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int p = 0; p < 2 * PF; ++p) edge(x[p % PF], i + p);
+    lds_barrier2();  // the hash-only step
+#pragma unroll
+    for (int p = 0; p < PF; ++p) vm_wait<0>(x[p]);
+}
+
+template <int K, int M, int G, int T, int PF>
+static bool launch_ws_t(const EncArgs& a, hipStream_t s) {
+    constexpr int R = K + M;
+    constexpr int NT = 2 * G * R + G * (T / 16);
+    constexpr size_t dyn = (size_t)2 * G * R * (T + 16);
+    if constexpr (dyn + K * 32 > 163840 || NT > 1024) {
+        return false;
+    } else {
+        if (a.dyb != M || (a.S % 16) != 0) return false;
+        auto kern = k_ehx_ws<K, M, G, T, PF>;
+        static bool attr = false;
+        if (!attr) {
+            if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn) !=
+                hipSuccess)
+                return false;
+            attr = true;
+        }
+        const int64_t grid = (a.n_blocks + G - 1) / G;
+        hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), dyn, s, a);
+        return true;
+    }
+}
+
 // GM multiplies the minimal stripe count per workgroup (GM = 4 on RS(8+4): 16 stripes,
 // 12 waves, one workgroup per CU, all of a CU's waves in one barrier domain).
 // LDSMIN pads the dynamic LDS so that at most 163840 / LDSMIN workgroups share a CU.
@@ -448,6 +614,8 @@ static bool launch_ehx_km(int v, const EncArgs& a, hipStream_t s) {
         case 86: if constexpr (deep) return launch_ehx_t<K, M, 8, 1, 2, false, 1, false, 4>(a, s); else return false;
         case 87: if constexpr (deep) return launch_ehx_t<K, M, 8, 1, 2, false, 2, false, 4>(a, s); else return false;
         case 88: if constexpr (deep) return launch_ehx_t<K, M, 8, 1, 2, false, 3, false, 4>(a, s); else return false;
+        case 100: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1>(a, s); else return false;
+        case 101: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 2>(a, s); else return false;
         case 61: if constexpr (deep) return launch_ehx_t<K, M, 8, 1, 2, false, 1>(a, s); else return false;
         case 64: if constexpr (deep) return launch_ehx_t<K, M, 8, 2, 2, false, 1>(a, s); else return false;
         default: return false;

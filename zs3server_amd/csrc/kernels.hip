@@ -1081,6 +1081,10 @@ static hipError_t run_encode_fast(const EncArgs& a, hipStream_t s) {
             // in ~0.7 ms and the last in ~1.6 ms (per-wave stamps, scripts/stamps3.py),
             // leaving CUs under-occupied for half the launch; one workgroup per CU
             // keeps all of a CU's waves in lockstep (1.42 -> 1.31 ms).
+            // Variant 100 (warp-specialised k_ehx_ws: 6 hash waves in the pair form + 6
+            // encode waves with 16-byte columns) takes ~11 % off the compute-bound time
+            // (L2-resident alias runs 1.08 -> 0.96 ms) and 3 % off the HBM launch.
+            if (!done && a.dyb == M && a.n_blocks >= 16 * 256) done = launch_ehx(100, a, s);
             if (!done && a.dyb == M && a.n_blocks >= 16 * 256) done = launch_ehx(80, a, s);
         }
         if constexpr (K == 4 && M == 2) {

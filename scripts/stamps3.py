@@ -16,6 +16,9 @@ codec = z.Codec(k, m)
 buf = torch.empty(nobj * stride, dtype=torch.uint8, device="cuda")
 sums = torch.empty(nobj * (k + m) * 32, dtype=torch.uint8, device="cuda")
 z.fill_batch(buf, stride, blen, nobj, seed=5)
+# STAMP_ALIAS=1: strides 0 (every block reads stripe 0: L2-resident, compute-bound)
+ALIAS = os.environ.get("STAMP_ALIAS", "0") == "1"
+st = 0 if ALIAS else stride
 G = 4
 nwave = nobj // G * 3
 dbg = torch.zeros(nwave * 5, dtype=torch.int64, device="cuda")
@@ -23,16 +26,18 @@ for v in [int(x) for x in os.environ.get("VARIANTS", "50").split(",")]:
     z.set_variant(v)
     z.set_debug_buffer(None)
     for _ in range(3):
-        codec.encode_batch(buf, stride, blen, nobj, parity=buf, parity_offset=k * S, parity_stride=stride, sums=sums)
+        codec.encode_batch(buf, st, blen, nobj, parity=buf, parity_offset=k * S, parity_stride=st, sums=sums)
     dbg.zero_()
     z.set_debug_buffer(dbg)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    codec.encode_batch(buf, stride, blen, nobj, parity=buf, parity_offset=k * S, parity_stride=stride, sums=sums)
+    codec.encode_batch(buf, st, blen, nobj, parity=buf, parity_offset=k * S, parity_stride=st, sums=sums)
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1)
     d = dbg.view(-1, 5).cpu()
+    wid = torch.arange(d.shape[0]) % 12  # wave index within a 12-wave workgroup
+    wid = wid[d[:, 1] > 0]
     d = d[d[:, 1] > 0]
     rt0, rt1, cyc = d[:, 0].double(), d[:, 1].double(), d[:, 2].double()
     life = (rt1 - rt0) / 100.0
@@ -46,7 +51,7 @@ for v in [int(x) for x in os.environ.get("VARIANTS", "50").split(",")]:
     simd = (hw >> 4) & 0x3
     xcc = d[:, 4].long() & 0xF
     q = torch.tensor([0, 0.1, 0.5, 0.9, 1.0], dtype=torch.float64)
-    print(f"variant {v}: kernel {ms:.3f} ms, waves {d.shape[0]}")
+    print(f"variant {v}{' (alias)' if ALIAS else ''}: kernel {ms:.3f} ms, waves {d.shape[0]}")
     print("  lifetime us q0/10/50/90/100:", [round(float(x), 1) for x in torch.quantile(life, q)])
     print("  start us   q0/10/50/90/100:", [round(float(x), 1) for x in torch.quantile(start, q)])
     print("  end us     q0/10/50/90/100:", [round(float(x), 1) for x in torch.quantile(end, q)])
@@ -56,6 +61,11 @@ for v in [int(x) for x in os.environ.get("VARIANTS", "50").split(",")]:
     print("  waves per CU histogram:", sorted(Counter(per_cu.values()).items()))
     simdkey = Counter([(a, b, c, e, int(f)) for (a, b, c, e), f in zip(cukey, simd)])
     print("  waves per SIMD histogram:", sorted(Counter(simdkey.values()).items()))
+    print("  (wave index in a 12-wave workgroup, SIMD) counts:", sorted(Counter(zip(wid.tolist(), simd.tolist())).items())[:24])
+    for r in range(12):
+        sel = wid == r
+        if sel.any():
+            print(f"  wave {r:2d}: life mean {float(life[sel].mean()):.1f} us, clock {float(clk[sel].mean()):.3f} GHz")
     for x in sorted(set(int(t) for t in xcc)):
         sel = xcc == x
         print(f"  xcc {x}: waves {int(sel.sum())} life mean {float(life[sel].mean()):.1f} end max {float(end[sel].max()):.1f}")

@@ -396,7 +396,10 @@ __global__ void __launch_bounds__(4 * G * (K + M)) __attribute__((amdgpu_waves_p
 // one barrier.  Both roles run the same number of steps, so barriers stay matched.
 // With 6 + 6 waves on 4 SIMDs the busiest SIMD carries one hash and two encode waves:
 // ~6 % less issue than three mixed waves (asm_loops.py + scripts/ubench/opcost.hip).
-template <int K, int M, int G, int T, int PF>
+// BUF: the encode role addresses rows through buffer resources (workgroup base in
+// SGPRs, row/tile offset in an SGPR soffset, one constant per-lane voffset) instead
+// of 64-bit per-lane pointers: no VALU address arithmetic per load/store.
+template <int K, int M, int G, int T, int PF, bool BUF = false>
 __global__ void __launch_bounds__(2 * G * (K + M) + G * (T / 16)) __attribute__((amdgpu_waves_per_eu(3)))
 k_ehx_ws(EncArgs a) {
     constexpr int R = K + M;
@@ -424,6 +427,26 @@ k_ehx_ws(EncArgs a) {
     int64_t iend = PF;
     if (nfull >= 3 * PF) iend = PF + ((nfull - 3 * PF) / PF + 1) * PF;
     const int64_t total = iend + 2 * PF + 1;
+
+    // Diagnostics (a.dbg set): per-wave real time, shader clocks, HW_ID, XCC_ID, as in
+    // k_ehx (waves 0..NH/64-1 of a workgroup hash, the rest encode).
+    uint64_t rt0 = 0, ct0 = 0;
+    if (a.dbg) {
+        rt0 = __builtin_amdgcn_s_memrealtime();
+        ct0 = __builtin_amdgcn_s_memtime();
+    }
+    auto stamp = [&]() {
+        if (a.dbg && (tid & 63) == 0) {
+            const uint64_t rt1 = __builtin_amdgcn_s_memrealtime();
+            const uint64_t ct1 = __builtin_amdgcn_s_memtime();
+            uint64_t* d = a.dbg + ((int64_t)blockIdx.x * (NT / 64) + (tid >> 6)) * 5;
+            d[0] = rt0;
+            d[1] = rt1;
+            d[2] = ct1 - ct0;
+            d[3] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+            d[4] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+        }
+    };
 
     if (__builtin_amdgcn_readfirstlane(tid) < NH) {
         // ---- hash role: lanes (2hh, 2hh+1) of chain `chain` = shard row s of stripe g
@@ -456,6 +479,7 @@ k_ehx_ws(EncArgs a) {
             out[0] = d0;
             out[1] = d1;
         }
+        stamp();
         return;
     }
 
@@ -469,15 +493,40 @@ k_ehx_ws(EncArgs a) {
     const uint8_t* src = a.data + b * a.data_stride + o;
     uint8_t* pdst = a.parity + b * a.parity_stride + o;
     const int col_off = g * R * TS + o;
+    // buffer form (launch checks that every offset fits in 31 bits)
+    const __amdgpu_buffer_rsrc_t rs_d =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(a.data + blk0 * a.data_stride), 0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs_p =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(a.parity + blk0 * a.parity_stride), 0, 0x7FFFFFFF, 0x00020000);
+    const uint32_t vo_d = (uint32_t)((b - blk0) * a.data_stride + o);
+    const uint32_t vo_p = (uint32_t)((b - blk0) * a.parity_stride + o);
 
     VT x[PF][K];
-    auto load = [&](VT (&xs)[K], int64_t t0) {
+    // rows j of tile offset t0u (wave-uniform) at per-lane byte offset vo within the row
+    auto load_buf = [&](VT (&xs)[K], uint32_t vo, int64_t t0u) {
 #pragma unroll
-        for (int j = 0; j < K; ++j) ld_async<NWd>(xs[j], src + (int64_t)j * S + t0);
+        for (int j = 0; j < K; ++j) {
+            const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)(j * S + t0u));
+            asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen"
+                         : "=v"(xs[j])
+                         : "v"(vo), "s"(rs_d), "s"(so)
+                         : "memory");
+        }
+    };
+    auto load = [&](VT (&xs)[K], int64_t t0) {
+        if constexpr (BUF) {
+            load_buf(xs, vo_d, t0);
+        } else {
+#pragma unroll
+            for (int j = 0; j < K; ++j) ld_async<NWd>(xs[j], src + (int64_t)j * S + t0);
+        }
     };
     auto prefetch_any = [&](VT (&xs)[K], int64_t tn) {
         const bool ok = tn < nfull || (tn == nfull && o < tail);
-        load(xs, ok ? tn * T : 0);
+        if constexpr (BUF)
+            load_buf(xs, vo_d + (ok ? (uint32_t)(tn * T) : 0u), 0);  // per-lane part in voffset
+        else
+            load(xs, ok ? tn * T : 0);
     };
     auto encode = [&](VT (&xr)[K], uint8_t* tl, Col<NWd> (&par)[M]) {
         Col<NWd> xs[K];
@@ -491,7 +540,15 @@ k_ehx_ws(EncArgs a) {
     };
     auto store_par = [&](const Col<NWd> (&par)[M], int64_t t0) {
 #pragma unroll
-        for (int r = 0; r < M; ++r) st_col<NWd>(pdst + (int64_t)r * S + t0, par[r]);
+        for (int r = 0; r < M; ++r) {
+            if constexpr (BUF) {
+                const VT v = {par[r].w[0], par[r].w[1], par[r].w[2], par[r].w[3]};
+                __builtin_amdgcn_raw_buffer_store_b128(v, rs_p, (int)vo_p,
+                                                       (int)__builtin_amdgcn_readfirstlane((uint32_t)(r * S + t0)), 0);
+            } else {
+                st_col<NWd>(pdst + (int64_t)r * S + t0, par[r]);
+            }
+        }
     };
     // steady step (see k_ehx): wait for loads(ti) only
     auto step = [&](VT (&xs)[K], int64_t ti) {
@@ -528,9 +585,10 @@ k_ehx_ws(EncArgs a) {
     lds_barrier2();  // the hash-only step
 #pragma unroll
     for (int p = 0; p < PF; ++p) vm_wait<0>(x[p]);
+    stamp();
 }
 
-template <int K, int M, int G, int T, int PF>
+template <int K, int M, int G, int T, int PF, bool BUF = false>
 static bool launch_ws_t(const EncArgs& a, hipStream_t s) {
     constexpr int R = K + M;
     constexpr int NT = 2 * G * R + G * (T / 16);
@@ -539,7 +597,10 @@ static bool launch_ws_t(const EncArgs& a, hipStream_t s) {
         return false;
     } else {
         if (a.dyb != M || (a.S % 16) != 0) return false;
-        auto kern = k_ehx_ws<K, M, G, T, PF>;
+        if (BUF && ((G - 1) * a.data_stride + K * a.S > 0x7FFFFFFF ||
+                    (G - 1) * a.parity_stride + M * a.S > 0x7FFFFFFF || a.data_stride < 0 || a.parity_stride < 0))
+            return false;
+        auto kern = k_ehx_ws<K, M, G, T, PF, BUF>;
         static bool attr = false;
         if (!attr) {
             if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn) !=
@@ -616,6 +677,7 @@ static bool launch_ehx_km(int v, const EncArgs& a, hipStream_t s) {
         case 88: if constexpr (deep) return launch_ehx_t<K, M, 8, 1, 2, false, 3, false, 4>(a, s); else return false;
         case 100: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1>(a, s); else return false;
         case 101: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 2>(a, s); else return false;
+        case 103: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 2, true>(a, s); else return false;
         case 61: if constexpr (deep) return launch_ehx_t<K, M, 8, 1, 2, false, 1>(a, s); else return false;
         case 64: if constexpr (deep) return launch_ehx_t<K, M, 8, 2, 2, false, 1>(a, s); else return false;
         default: return false;

@@ -67,7 +67,7 @@ def test_rs84_variant_dead_stripes(oracle, variant, nb):
     run_case(oracle, 8, 4, 8 * (384 * 4 + 128), nb, variant, seed=nb)
 
 
-@pytest.mark.parametrize("variant", [50, 51, 55, 70, 82, 90, 91, 92, 93, 94])
+@pytest.mark.parametrize("variant", [50, 51, 55, 70, 82, 90, 91, 92, 93, 94, 110, 111, 112, 120])
 @pytest.mark.parametrize("k,m,blen", [(4, 2, 4 * 16), (4, 2, 4 * (384 * 3 + 48)), (4, 2, 1 << 20),
                                       (16, 4, 16 * 640 * 2), (16, 4, 1 << 20)])
 def test_other_shapes_variants(oracle, variant, k, m, blen):

@@ -399,15 +399,32 @@ __global__ void __launch_bounds__(4 * G * (K + M)) __attribute__((amdgpu_waves_p
 // BUF: the encode role addresses rows through buffer resources (workgroup base in
 // SGPRs, row/tile offset in an SGPR soffset, one constant per-lane voffset) instead
 // of 64-bit per-lane pointers: no VALU address arithmetic per load/store.
-template <int K, int M, int G, int T, int PF, bool BUF = false>
-__global__ void __launch_bounds__(2 * G * (K + M) + G * (T / 16)) __attribute__((amdgpu_waves_per_eu(3)))
+// HQ: the hash waves use the quad form (one HH lane per thread, as k_ehx; 19 VALU per
+// lane-packet but the shortest dependent chain per packet) — for small batches, where a
+// hash wave has its SIMD to itself and the chain latency, not issue, bounds the launch
+// (RS(4+2) config 2: 6 144 chains); the hash thread count is padded to whole waves, the
+// pad quads hash a real row and discard the digest.
+template <int K, int M, int G, int T, bool HQ>
+constexpr int ws_nh() {
+    return HQ ? ((4 * G * (K + M) + 63) / 64) * 64 : 2 * G * (K + M);
+}
+// Encode column width: 16 bytes, 8 for K > 8 (16 rows of 16-byte columns do not fit
+// the 168-VGPR budget beside the encode's working set).
+template <int K>
+constexpr int ws_cwe() {
+    return K > 8 ? 8 : 16;
+}
+
+template <int K, int M, int G, int T, int PF, bool BUF = false, bool HQ = false>
+__global__ void __launch_bounds__((ws_nh<K, M, G, T, HQ>() + G * (T / ws_cwe<K>()))) __attribute__((amdgpu_waves_per_eu(3)))
 k_ehx_ws(EncArgs a) {
     constexpr int R = K + M;
-    constexpr int NH = 2 * G * R;   // hash threads
-    constexpr int CPS = T / 16;     // 16-byte columns per stripe row
+    constexpr int NH = ws_nh<K, M, G, T, HQ>();  // hash threads
+    constexpr int CWE = ws_cwe<K>();
+    constexpr int CPS = T / CWE;    // encode columns per stripe row
     constexpr int NE = G * CPS;     // encode threads
     constexpr int NT = NH + NE;
-    constexpr int TS = T + 16;      // b128 row reads of 4 chains hit disjoint banks
+    constexpr int TS = HQ ? T + 32 : T + 16;  // conflict-free b64 (quad) / b128 (pair) row reads
     constexpr int NPK = T / 32;
     constexpr int NTAB = K * 8;
     static_assert(M == 2 || M == 4, "dyadic shapes only");
@@ -448,7 +465,40 @@ k_ehx_ws(EncArgs a) {
         }
     };
 
-    if (__builtin_amdgcn_readfirstlane(tid) < NH) {
+    if (HQ && __builtin_amdgcn_readfirstlane(tid) < NH) {
+        // ---- hash role, quad form: lane `lane` of chain `chain`
+        const int chain = tid >> 2, lane = tid & 3;
+        const bool live = chain < G * R && blk0 + chain / R < a.n_blocks;
+        const int crow = chain < G * R ? chain : chain - G * R;
+        const int row_off = crow * TS + 8 * lane;
+        const uint32_t sel = zipper_sel(lane);
+        HHLane st = hh_init(lane, a.key[0], a.key[1], a.key[2], a.key[3]);
+        lds_barrier2();  // tables (matches the encode role)
+        lds_barrier2();  // step 0: tile 0 being encoded
+        for (int64_t s = 1; s <= nfull; ++s) {
+            const uint64_t* p = reinterpret_cast<const uint64_t*>(tile[(s - 1) & 1] + row_off);
+            uint64_t w[NPK];
+#pragma unroll
+            for (int i = 0; i < NPK; ++i) w[i] = p[4 * i];
+#pragma unroll
+            for (int i = 0; i < NPK; ++i) hh_update(st, w[i], sel);
+            lds_barrier2();
+        }
+        if (tail) {
+            const uint8_t* row = tile[nfull & 1] + crow * TS;
+            hh_packets(st, row, tail >> 5, lane, sel);
+            if (tail & 31) hh_remainder(st, row + (tail & ~31), (uint32_t)(tail & 31), lane, sel);
+        }
+        for (int64_t s = nfull + 1; s < total; ++s) lds_barrier2();
+        const uint64_t h = hh_finalize256(st, lane, sel);
+        if (live) {
+            const int64_t bb = blk0 + chain / R;
+            *reinterpret_cast<uint64_t*>(a.sums + (bb * R + chain % R) * 32 + 8 * lane) = h;
+        }
+        stamp();
+        return;
+    }
+    if (!HQ && __builtin_amdgcn_readfirstlane(tid) < NH) {
         // ---- hash role: lanes (2hh, 2hh+1) of chain `chain` = shard row s of stripe g
         const int chain = tid >> 1, hh = tid & 1;
         const int row_off = chain * TS;
@@ -485,10 +535,10 @@ k_ehx_ws(EncArgs a) {
 
     // ---- encode role: 16-byte column o of stripe g (dead stripes of the last
     // workgroup alias the last live block and store byte-identical parity)
-    constexpr int NWd = 4;
+    constexpr int NWd = CWE / 4;
     typedef typename VecOf<NWd>::type VT;
     const int e = tid - NH;
-    const int g = e / CPS, o = (e % CPS) * 16;
+    const int g = e / CPS, o = (e % CPS) * CWE;
     const int64_t b = (blk0 + g) < a.n_blocks ? (blk0 + g) : (a.n_blocks - 1);
     const uint8_t* src = a.data + b * a.data_stride + o;
     uint8_t* pdst = a.parity + b * a.parity_stride + o;
@@ -507,10 +557,16 @@ k_ehx_ws(EncArgs a) {
 #pragma unroll
         for (int j = 0; j < K; ++j) {
             const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)(j * S + t0u));
-            asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen"
-                         : "=v"(xs[j])
-                         : "v"(vo), "s"(rs_d), "s"(so)
-                         : "memory");
+            if constexpr (NWd == 4)
+                asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen"
+                             : "=v"(xs[j])
+                             : "v"(vo), "s"(rs_d), "s"(so)
+                             : "memory");
+            else
+                asm volatile("buffer_load_dwordx2 %0, %1, %2, %3 offen"
+                             : "=v"(xs[j])
+                             : "v"(vo), "s"(rs_d), "s"(so)
+                             : "memory");
         }
     };
     auto load = [&](VT (&xs)[K], int64_t t0) {
@@ -542,9 +598,14 @@ k_ehx_ws(EncArgs a) {
 #pragma unroll
         for (int r = 0; r < M; ++r) {
             if constexpr (BUF) {
-                const VT v = {par[r].w[0], par[r].w[1], par[r].w[2], par[r].w[3]};
-                __builtin_amdgcn_raw_buffer_store_b128(v, rs_p, (int)vo_p,
-                                                       (int)__builtin_amdgcn_readfirstlane((uint32_t)(r * S + t0)), 0);
+                const int so = (int)__builtin_amdgcn_readfirstlane((uint32_t)(r * S + t0));
+                if constexpr (NWd == 4) {
+                    const VT v = {par[r].w[0], par[r].w[1], par[r].w[2], par[r].w[3]};
+                    __builtin_amdgcn_raw_buffer_store_b128(v, rs_p, (int)vo_p, so, 0);
+                } else {
+                    const VT v = {par[r].w[0], par[r].w[1]};
+                    __builtin_amdgcn_raw_buffer_store_b64(v, rs_p, (int)vo_p, so, 0);
+                }
             } else {
                 st_col<NWd>(pdst + (int64_t)r * S + t0, par[r]);
             }
@@ -588,11 +649,12 @@ k_ehx_ws(EncArgs a) {
     stamp();
 }
 
-template <int K, int M, int G, int T, int PF, bool BUF = false>
+template <int K, int M, int G, int T, int PF, bool BUF = false, bool HQ = false, int LDSMIN = 0>
 static bool launch_ws_t(const EncArgs& a, hipStream_t s) {
     constexpr int R = K + M;
-    constexpr int NT = 2 * G * R + G * (T / 16);
-    constexpr size_t dyn = (size_t)2 * G * R * (T + 16);
+    constexpr int NT = ws_nh<K, M, G, T, HQ>() + G * (T / ws_cwe<K>());
+    constexpr size_t tiles = (size_t)2 * G * R * (HQ ? T + 32 : T + 16);
+    constexpr size_t dyn = tiles > (size_t)LDSMIN ? tiles : (size_t)LDSMIN;
     if constexpr (dyn + K * 32 > 163840 || NT > 1024) {
         return false;
     } else {
@@ -600,7 +662,7 @@ static bool launch_ws_t(const EncArgs& a, hipStream_t s) {
         if (BUF && ((G - 1) * a.data_stride + K * a.S > 0x7FFFFFFF ||
                     (G - 1) * a.parity_stride + M * a.S > 0x7FFFFFFF || a.data_stride < 0 || a.parity_stride < 0))
             return false;
-        auto kern = k_ehx_ws<K, M, G, T, PF, BUF>;
+        auto kern = k_ehx_ws<K, M, G, T, PF, BUF, HQ>;
         static bool attr = false;
         if (!attr) {
             if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn) !=
@@ -678,6 +740,10 @@ static bool launch_ehx_km(int v, const EncArgs& a, hipStream_t s) {
         case 100: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1>(a, s); else return false;
         case 101: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 2>(a, s); else return false;
         case 103: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 2, true>(a, s); else return false;
+        case 120: if constexpr (K == 16 && M == 4) return launch_ws_t<K, M, 8, 384, 1, true>(a, s); else return false;
+        case 110: if constexpr (few) return launch_ws_t<K, M, 4, 512, 2, false, true, 83968>(a, s); else return false;
+        case 111: if constexpr (few) return launch_ws_t<K, M, 4, 512, 4, false, true, 83968>(a, s); else return false;
+        case 112: if constexpr (few) return launch_ws_t<K, M, 4, 256, 4, false, true, 83968>(a, s); else return false;
         case 61: if constexpr (deep) return launch_ehx_t<K, M, 8, 1, 2, false, 1>(a, s); else return false;
         case 64: if constexpr (deep) return launch_ehx_t<K, M, 8, 2, 2, false, 1>(a, s); else return false;
         default: return false;

@@ -300,6 +300,34 @@ def test_full_size_rs84_properties(oracle):
     torch.cuda.empty_cache()
 
 
+def test_full_size_rs42_config2(oracle):
+    """BASELINE config 2 at full size: RS(4+2), 1024 x 1 MiB through the default launch
+    (warp-specialised small-batch kernel); sampled blocks against the oracle, every sum
+    against the standalone hash kernel."""
+    k, m, blen, nb = 4, 2, 1 << 20, 1024
+    S = blen // k
+    stride = (k + m) * S
+    codec = z.Codec(k, m)
+    d = torch.empty(nb * stride, dtype=torch.uint8, device=DEV)
+    z.fill_batch(d, stride, blen, nb, seed=42)
+    sums = torch.zeros(nb * (k + m) * 32, dtype=torch.uint8, device=DEV)
+    codec.encode_batch(d, stride, blen, nb, parity=d, parity_offset=k * S, parity_stride=stride, sums=sums)
+    torch.cuda.synchronize()
+    v = d.view(nb, k + m, S)
+    hs = sums.view(nb, k + m, 32)
+    mat = oracle.build_matrix(k, m)
+    for b in (0, 3, 511, 1023):
+        want = oracle.encode_data(k, m, oracle.fill(42, b, blen), mat)
+        assert np.array_equal(v[b].cpu().numpy(), want)
+        assert np.array_equal(hs[b].cpu().numpy(), oracle.hh256_rows(KEY, want))
+    sums2 = torch.zeros_like(sums)
+    z.hh256_batch(d, S, S, nb * (k + m), sums2)
+    torch.cuda.synchronize()
+    assert torch.equal(sums, sums2)
+    del d, sums, sums2
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("k,m,bs,nfull,tail,batch,pinned", [
     (4, 2, 1 << 16, 5, 1000, 2, False), (8, 4, 1 << 16, 7, 0, 3, True), (16, 4, 1 << 16, 3, 17, 8, False),
     (8, 4, 1 << 20, 4, (1 << 19) + 3, 2, True),

@@ -1093,6 +1093,11 @@ static hipError_t run_encode_fast(const EncArgs& a, hipStream_t s) {
             // 128 CUs, latency-bound): fused_v2 variant 91 = pipelined body (encode of
             // tile i beside the hash of tile i-1), 4 tiles of loads in flight, one
             // workgroup per CU.  1.03 -> 0.84 ms (scripts/box_sweep.sh).
+            // Up to one 4-stripe workgroup per CU: warp-specialised k_ehx_ws variant 111
+            // (quad-form hash waves alone on their SIMDs, encode on the other two, 4
+            // tiles of loads in flight): the hash chains' latency, not issue, sets the
+            // pace; 0.83 -> 0.41 ms on config 2.
+            if (!done && a.dyb == M && a.n_blocks <= 4 * 256) done = launch_ehx(111, a, s);
             if (!done && a.dyb == M && a.n_blocks <= 8 * 256) done = launch_ehx(91, a, s);
         }
         if (!done) {

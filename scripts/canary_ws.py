@@ -6,7 +6,7 @@ k, m, blen = 8, 4, 1 << 20
 S = blen // k; stride = (k + m) * S
 codec = z.Codec(k, m)
 for nobj in (33, 4096):
-    for v in (100, 102, 103):
+    for v in (100, 102, 103, 104):
         guard = 1 << 22
         big = torch.full((guard + nobj * stride + guard,), 0x5A, dtype=torch.uint8, device="cuda")
         buf = big[guard: guard + nobj * stride]

@@ -14,7 +14,7 @@ codec = z.Codec(k, m)
 buf = torch.empty(nobj * stride, dtype=torch.uint8, device="cuda")
 sums = torch.empty(nobj * (k + m) * 32, dtype=torch.uint8, device="cuda")
 z.fill_batch(buf, stride, blen, nobj, seed=5)
-for v in [int(x) for x in os.environ.get('STAMP_VARIANTS', '101,120').split(',')]:
+for v in [int(x) for x in os.environ.get('STAMP_VARIANTS', '17,24').split(',')]:
     dbg = torch.zeros(1024 * 8 * 5, dtype=torch.int64, device="cuda")
     z.set_debug_buffer(dbg)
     z.set_variant(v)

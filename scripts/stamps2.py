@@ -1,4 +1,4 @@
-"""Residency/clock check for the stamped pipelined variant (120)."""
+"""Residency/clock check for the stamped pipelined variant (24)."""
 import os
 import sys
 
@@ -16,7 +16,7 @@ sums = torch.empty(nobj * (k + m) * 32, dtype=torch.uint8, device="cuda")
 z.fill_batch(buf, stride, blen, nobj, seed=5)
 dbg = torch.zeros(nobj // 4 * 8 * 5, dtype=torch.int64, device="cuda")
 z.set_debug_buffer(dbg)
-z.set_variant(120)
+z.set_variant(24)
 for _ in range(3):
     codec.encode_batch(buf, stride, blen, nobj, parity=buf, parity_offset=k * S, parity_stride=stride, sums=sums)
 torch.cuda.synchronize()

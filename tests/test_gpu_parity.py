@@ -300,11 +300,12 @@ def test_full_size_rs84_properties(oracle):
     torch.cuda.empty_cache()
 
 
-def test_full_size_rs42_config2(oracle):
-    """BASELINE config 2 at full size: RS(4+2), 1024 x 1 MiB through the default launch
-    (warp-specialised small-batch kernel); sampled blocks against the oracle, every sum
-    against the standalone hash kernel."""
-    k, m, blen, nb = 4, 2, 1 << 20, 1024
+@pytest.mark.parametrize("k,m,nb", [(4, 2, 1024), (16, 4, 2048)])
+def test_full_size_ws_defaults(oracle, k, m, nb):
+    """BASELINE config 2 (RS(4+2), 1024 x 1 MiB) and RS(16+4) 2048 x 1 MiB at full size
+    through the default launches (warp-specialised kernels); sampled blocks against the
+    oracle, every sum against the standalone hash kernel."""
+    blen = 1 << 20
     S = blen // k
     stride = (k + m) * S
     codec = z.Codec(k, m)
@@ -316,7 +317,7 @@ def test_full_size_rs42_config2(oracle):
     v = d.view(nb, k + m, S)
     hs = sums.view(nb, k + m, 32)
     mat = oracle.build_matrix(k, m)
-    for b in (0, 3, 511, 1023):
+    for b in (0, 3, nb // 2 - 1, nb - 1):
         want = oracle.encode_data(k, m, oracle.fill(42, b, blen), mat)
         assert np.array_equal(v[b].cpu().numpy(), want)
         assert np.array_equal(hs[b].cpu().numpy(), oracle.hh256_rows(KEY, want))

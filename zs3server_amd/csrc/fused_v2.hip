@@ -415,7 +415,8 @@ constexpr int ws_cwe() {
     return K > 8 ? 8 : 16;
 }
 
-template <int K, int M, int G, int T, int PF, bool BUF = false, bool HQ = false>
+// WT (diagnostic): per-wave shader cycles spent waiting at barriers, into the dbg stamps.
+template <int K, int M, int G, int T, int PF, bool BUF = false, bool HQ = false, bool WT = false>
 __global__ void __launch_bounds__((ws_nh<K, M, G, T, HQ>() + G * (T / ws_cwe<K>()))) __attribute__((amdgpu_waves_per_eu(3)))
 k_ehx_ws(EncArgs a) {
     constexpr int R = K + M;
@@ -452,6 +453,16 @@ k_ehx_ws(EncArgs a) {
         rt0 = __builtin_amdgcn_s_memrealtime();
         ct0 = __builtin_amdgcn_s_memtime();
     }
+    uint64_t wsum = 0;
+    auto bar = [&]() {
+        if constexpr (WT) {
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            lds_barrier2();
+            wsum += __builtin_amdgcn_s_memtime() - t;
+        } else {
+            lds_barrier2();
+        }
+    };
     auto stamp = [&]() {
         if (a.dbg && (tid & 63) == 0) {
             const uint64_t rt1 = __builtin_amdgcn_s_memrealtime();
@@ -461,7 +472,7 @@ k_ehx_ws(EncArgs a) {
             d[1] = rt1;
             d[2] = ct1 - ct0;
             d[3] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
-            d[4] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+            d[4] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) | (wsum << 8);  // XCC_ID | wait
         }
     };
 
@@ -473,8 +484,8 @@ k_ehx_ws(EncArgs a) {
         const int row_off = crow * TS + 8 * lane;
         const uint32_t sel = zipper_sel(lane);
         HHLane st = hh_init(lane, a.key[0], a.key[1], a.key[2], a.key[3]);
-        lds_barrier2();  // tables (matches the encode role)
-        lds_barrier2();  // step 0: tile 0 being encoded
+        bar();  // tables (matches the encode role)
+        bar();  // step 0: tile 0 being encoded
         for (int64_t s = 1; s <= nfull; ++s) {
             const uint64_t* p = reinterpret_cast<const uint64_t*>(tile[(s - 1) & 1] + row_off);
             uint64_t w[NPK];
@@ -482,14 +493,14 @@ k_ehx_ws(EncArgs a) {
             for (int i = 0; i < NPK; ++i) w[i] = p[4 * i];
 #pragma unroll
             for (int i = 0; i < NPK; ++i) hh_update(st, w[i], sel);
-            lds_barrier2();
+            bar();
         }
         if (tail) {
             const uint8_t* row = tile[nfull & 1] + crow * TS;
             hh_packets(st, row, tail >> 5, lane, sel);
             if (tail & 31) hh_remainder(st, row + (tail & ~31), (uint32_t)(tail & 31), lane, sel);
         }
-        for (int64_t s = nfull + 1; s < total; ++s) lds_barrier2();
+        for (int64_t s = nfull + 1; s < total; ++s) bar();
         const uint64_t h = hh_finalize256(st, lane, sel);
         if (live) {
             const int64_t bb = blk0 + chain / R;
@@ -503,8 +514,8 @@ k_ehx_ws(EncArgs a) {
         const int chain = tid >> 1, hh = tid & 1;
         const int row_off = chain * TS;
         HHPair st = hh2_init(hh, a.key[0], a.key[1], a.key[2], a.key[3]);
-        lds_barrier2();  // tables (matches the encode role)
-        lds_barrier2();  // step 0: tile 0 being encoded
+        bar();  // tables (matches the encode role)
+        bar();  // step 0: tile 0 being encoded
         for (int64_t s = 1; s <= nfull; ++s) {
             const uint4* p = reinterpret_cast<const uint4*>(tile[(s - 1) & 1] + row_off) + hh;
             uint4 w[NPK];
@@ -513,14 +524,14 @@ k_ehx_ws(EncArgs a) {
 #pragma unroll
             for (int i = 0; i < NPK; ++i)
                 hh2_update(st, ((uint64_t)w[i].y << 32) | w[i].x, ((uint64_t)w[i].w << 32) | w[i].z);
-            lds_barrier2();
+            bar();
         }
         if (tail) {
             const uint8_t* row = tile[nfull & 1] + row_off;
             hh2_packets(st, row, tail >> 5, hh);
             if (tail & 31) hh2_remainder(st, row + (tail & ~31), (uint32_t)(tail & 31), hh);
         }
-        for (int64_t s = nfull + 1; s < total; ++s) lds_barrier2();
+        for (int64_t s = nfull + 1; s < total; ++s) bar();
         uint64_t d0, d1;
         hh2_finalize256(st, d0, d1);
         if (blk0 + chain / R < a.n_blocks) {
@@ -618,7 +629,7 @@ k_ehx_ws(EncArgs a) {
         encode(xs, tile[ti & 1], par);
         load(xs, (ti + PF) * T);
         store_par(par, ti * T);
-        lds_barrier2();
+        bar();
     };
     auto edge = [&](VT (&xs)[K], int64_t ti) {
         const bool full = ti < nfull, part = ti == nfull && tail;
@@ -627,9 +638,9 @@ k_ehx_ws(EncArgs a) {
         if (full || part) encode(xs, tile[ti & 1], par);
         prefetch_any(xs, ti + PF);
         if (full || (part && o < tail)) store_par(par, ti * T);
-        lds_barrier2();
+        bar();
     };
-    lds_barrier2();  // tables visible
+    bar();  // tables visible
 #pragma unroll
     for (int p = 0; p < PF; ++p) prefetch_any(x[p], p);
 #pragma unroll
@@ -643,13 +654,13 @@ k_ehx_ws(EncArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
     for (int p = 0; p < 2 * PF; ++p) edge(x[p % PF], i + p);
-    lds_barrier2();  // the hash-only step
+    bar();  // the hash-only step
 #pragma unroll
     for (int p = 0; p < PF; ++p) vm_wait<0>(x[p]);
     stamp();
 }
 
-template <int K, int M, int G, int T, int PF, bool BUF = false, bool HQ = false, int LDSMIN = 0>
+template <int K, int M, int G, int T, int PF, bool BUF = false, bool HQ = false, int LDSMIN = 0, bool WT = false>
 static bool launch_ws_t(const EncArgs& a, hipStream_t s) {
     constexpr int R = K + M;
     constexpr int NT = ws_nh<K, M, G, T, HQ>() + G * (T / ws_cwe<K>());
@@ -662,7 +673,7 @@ static bool launch_ws_t(const EncArgs& a, hipStream_t s) {
         if (BUF && ((G - 1) * a.data_stride + K * a.S > 0x7FFFFFFF ||
                     (G - 1) * a.parity_stride + M * a.S > 0x7FFFFFFF || a.data_stride < 0 || a.parity_stride < 0))
             return false;
-        auto kern = k_ehx_ws<K, M, G, T, PF, BUF, HQ>;
+        auto kern = k_ehx_ws<K, M, G, T, PF, BUF, HQ, WT>;
         static bool attr = false;
         if (!attr) {
             if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn) !=
@@ -738,8 +749,9 @@ static bool launch_ehx_km(int v, const EncArgs& a, hipStream_t s) {
         case 87: if constexpr (deep) return launch_ehx_t<K, M, 8, 1, 2, false, 2, false, 4>(a, s); else return false;
         case 88: if constexpr (deep) return launch_ehx_t<K, M, 8, 1, 2, false, 3, false, 4>(a, s); else return false;
         case 100: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1>(a, s); else return false;
-        case 101: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 2>(a, s); else return false;
         case 103: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 2, true>(a, s); else return false;
+        case 102: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, true>(a, s); else return false;
+        case 104: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, true>(a, s); else return false;
         case 120: if constexpr (K == 16 && M == 4) return launch_ws_t<K, M, 8, 384, 1, true>(a, s); else return false;
         case 110: if constexpr (few) return launch_ws_t<K, M, 4, 512, 2, false, true, 83968>(a, s); else return false;
         case 111: if constexpr (few) return launch_ws_t<K, M, 4, 512, 4, false, true, 83968>(a, s); else return false;

@@ -1042,7 +1042,7 @@ static bool launch_variant(int v, const EncArgs& a, hipStream_t s) {
         case 21: launch_pipe<K, M, G, 192, 4>(a, s); return true;
         case 22: launch_pipe<K, M, G, 256, 8>(a, s); return true;
         case 23: launch_pipe<K, M, G, 320, 8>(a, s); return true;
-        case 120: launch_pipe<K, M, G, 384, 8, true>(a, s); return true;
+        case 24: launch_pipe<K, M, G, 384, 8, true>(a, s); return true;
         case 30: launch_pair<K, M, 384, 1, 16>(a, s); return true;
         case 31: launch_pair<K, M, 384, 2, 16>(a, s); return true;
         case 32: launch_pair<K, M, 192, 2, 8>(a, s); return true;
@@ -1056,8 +1056,8 @@ static bool launch_variant(int v, const EncArgs& a, hipStream_t s) {
         case 46: launch_ablation<K, M, 1, 384, 8, 1, 2>(a, s); return true;
         case 47: launch_ablation<K, M, 3, 768, 16>(a, s); return true;
         case 48: launch_ablation<K, M, 4, 768, 16>(a, s); return true;
-        case 101: launch_fused<K, M, G, 384, 1, 8, 1, false, true>(a, s); return true;
-        case 102: launch_fused<K, M, G, 256, 2, 16, 1, false, true>(a, s); return true;
+        case 17: launch_fused<K, M, G, 384, 1, 8, 1, false, true>(a, s); return true;
+        case 18: launch_fused<K, M, G, 256, 2, 16, 1, false, true>(a, s); return true;
         default: return launch_ehx(v, a, s);
     }
 }
@@ -1086,6 +1086,12 @@ static hipError_t run_encode_fast(const EncArgs& a, hipStream_t s) {
             // (L2-resident alias runs 1.08 -> 0.96 ms) and 3 % off the HBM launch.
             if (!done && a.dyb == M && a.n_blocks >= 16 * 256) done = launch_ehx(100, a, s);
             if (!done && a.dyb == M && a.n_blocks >= 16 * 256) done = launch_ehx(80, a, s);
+        }
+        if constexpr (K == 16 && M == 4) {
+            // RS(16+4), one 8-stripe workgroup per CU or more: k_ehx_ws variant 120 (5
+            // pair-form hash waves + 6 encode waves with 8-byte columns, buffer-addressed
+            // loads/stores): 0.81 -> 0.62 ms on 2048 x 1 MiB.
+            if (!done && a.dyb == M && a.n_blocks >= 8 * 256) done = launch_ehx(120, a, s);
         }
         if constexpr (K == 4 && M == 2) {
             // Default RS(4+2) for batches of at most one 8-stripe workgroup per CU

@@ -53,8 +53,37 @@ CASES = [
 @pytest.mark.parametrize("k,m,blen,erased", CASES)
 @pytest.mark.parametrize("data_only", [True, False])
 @pytest.mark.parametrize("heal", [False, True])
-def test_verify_reconstruct(oracle, k, m, blen, erased, data_only, heal):
-    nb = 3
+@pytest.mark.parametrize("variant", [0, 200])
+def test_verify_reconstruct(oracle, k, m, blen, erased, data_only, heal, variant):
+    """variant 0 = default dispatch (k_vr_ws for RS(8+4)-shaped verify / rebuild-2),
+    200 = k_verify_reconstruct for every shape."""
+    z.set_variant(variant)
+    try:
+        run_verify_case(oracle, k, m, blen, erased, data_only, heal)
+    finally:
+        z.set_variant(0)
+
+
+# warp-specialised GET / heal kernel (fused_v2.hip k_vr_ws, RS(8+4)-shaped, e = 0 or 2):
+# tile edges (no full tile, one tile, ragged tails) and dead stripes of the 16-stripe
+# workgroup
+WS_CASES = [(8, 4, 1 << 16, []), (8, 4, 1 << 16, [0, 5]), (8, 4, 1 << 16, [3, 9]), (8, 4, 8 * 48, [2, 11]),
+            (8, 4, 8 * 256, [1, 4]), (8, 4, 8 * (256 * 3 + 16), [0, 7]), (8, 4, 8 * (256 * 2 + 48), [])]
+
+
+@pytest.mark.parametrize("k,m,blen,erased", WS_CASES)
+@pytest.mark.parametrize("data_only", [True, False])
+@pytest.mark.parametrize("heal", [False, True])
+@pytest.mark.parametrize("variant", [210, 211])
+def test_verify_reconstruct_ws(oracle, k, m, blen, erased, data_only, heal, variant):
+    z.set_variant(variant)
+    try:
+        run_verify_case(oracle, k, m, blen, erased, data_only, heal, nb=17)
+    finally:
+        z.set_variant(0)
+
+
+def run_verify_case(oracle, k, m, blen, erased, data_only, heal, nb=3):
     sh, sums = stripes(oracle, k, m, blen, nb)
     S = sh.shape[2]
     R = k + m
@@ -152,11 +181,12 @@ def test_fused_kernel_selected():
 @pytest.mark.parametrize("k,m,blen,erased,heal", [(8, 4, 8 * 640, [], False), (8, 4, 8 * 640, [0, 5], False),
                                                   (8, 4, 8 * 640, [2, 10], True), (4, 2, 4 * 512, [1], True),
                                                   (16, 4, 16 * 256, [3, 17], False)])
-@pytest.mark.parametrize("variant", [0, 201])
+@pytest.mark.parametrize("variant", [0, 200, 201, 211])
 def test_verify_reconstruct_large_batch(oracle, k, m, blen, erased, heal, variant):
-    """4096 stripes through the default launch and the one-workgroup-per-CU launch
-    (variant 201, 16 stripes per workgroup); every stripe checked against the oracle,
-    one corrupt survivor flagged."""
+    """4096 stripes through the default launch (k_vr_ws where it applies), the
+    first-generation kernel (200), its one-workgroup-per-CU launch (201) and k_vr_ws
+    with one tile of prefetch (211); every stripe checked against the oracle, one
+    corrupt survivor flagged."""
     nb = 4096
     R = k + m
     S = -(-blen // k)

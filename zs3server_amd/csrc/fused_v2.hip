@@ -416,7 +416,10 @@ constexpr int ws_cwe() {
 }
 
 // WT (diagnostic): per-wave shader cycles spent waiting at barriers, into the dbg stamps.
-template <int K, int M, int G, int T, int PF, bool BUF = false, bool HQ = false, bool WT = false>
+// PM (issue-priority experiments): 1 = encode waves s_setprio 1 over hash waves; 2 = as 1
+// plus the younger encode wave of each SIMD-sharing pair (waves w, w+4) at 2; 3 = hash
+// waves at 1.
+template <int K, int M, int G, int T, int PF, bool BUF = false, bool HQ = false, bool WT = false, int PM = 0>
 __global__ void __launch_bounds__((ws_nh<K, M, G, T, HQ>() + G * (T / ws_cwe<K>()))) __attribute__((amdgpu_waves_per_eu(3)))
 k_ehx_ws(EncArgs a) {
     constexpr int R = K + M;
@@ -508,6 +511,16 @@ k_ehx_ws(EncArgs a) {
         }
         stamp();
         return;
+    }
+    if constexpr (PM == 3) {
+        if (__builtin_amdgcn_readfirstlane(tid) < NH) __builtin_amdgcn_s_setprio(1);
+    } else if constexpr (PM == 1 || PM == 2) {
+        if (__builtin_amdgcn_readfirstlane(tid) >= NH) {
+            if (PM == 2 && __builtin_amdgcn_readfirstlane(tid) >= NH + 256)
+                __builtin_amdgcn_s_setprio(2);
+            else
+                __builtin_amdgcn_s_setprio(1);
+        }
     }
     if (!HQ && __builtin_amdgcn_readfirstlane(tid) < NH) {
         // ---- hash role: lanes (2hh, 2hh+1) of chain `chain` = shard row s of stripe g
@@ -660,7 +673,8 @@ k_ehx_ws(EncArgs a) {
     stamp();
 }
 
-template <int K, int M, int G, int T, int PF, bool BUF = false, bool HQ = false, int LDSMIN = 0, bool WT = false>
+template <int K, int M, int G, int T, int PF, bool BUF = false, bool HQ = false, int LDSMIN = 0, bool WT = false,
+          int PM = 0>
 static bool launch_ws_t(const EncArgs& a, hipStream_t s) {
     constexpr int R = K + M;
     constexpr int NT = ws_nh<K, M, G, T, HQ>() + G * (T / ws_cwe<K>());
@@ -673,7 +687,7 @@ static bool launch_ws_t(const EncArgs& a, hipStream_t s) {
         if (BUF && ((G - 1) * a.data_stride + K * a.S > 0x7FFFFFFF ||
                     (G - 1) * a.parity_stride + M * a.S > 0x7FFFFFFF || a.data_stride < 0 || a.parity_stride < 0))
             return false;
-        auto kern = k_ehx_ws<K, M, G, T, PF, BUF, HQ, WT>;
+        auto kern = k_ehx_ws<K, M, G, T, PF, BUF, HQ, WT, PM>;
         static bool attr = false;
         if (!attr) {
             if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn) !=
@@ -751,6 +765,9 @@ static bool launch_ehx_km(int v, const EncArgs& a, hipStream_t s) {
         case 100: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1>(a, s); else return false;
         case 103: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 2, true>(a, s); else return false;
         case 102: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, true>(a, s); else return false;
+        case 105: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1>(a, s); else return false;
+        case 106: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 2>(a, s); else return false;
+        case 107: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 3>(a, s); else return false;
         case 104: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, true>(a, s); else return false;
         case 120: if constexpr (K == 16 && M == 4) return launch_ws_t<K, M, 8, 384, 1, true>(a, s); else return false;
         case 110: if constexpr (few) return launch_ws_t<K, M, 4, 512, 2, false, true, 83968>(a, s); else return false;
@@ -759,6 +776,234 @@ static bool launch_ehx_km(int v, const EncArgs& a, hipStream_t s) {
         case 61: if constexpr (deep) return launch_ehx_t<K, M, 8, 1, 2, false, 1>(a, s); else return false;
         case 64: if constexpr (deep) return launch_ehx_t<K, M, 8, 2, 2, false, 1>(a, s); else return false;
         default: return false;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// GET / heal pass, warp-specialised (replaces the arithmetic of
+// streamingBitrotReader.ReadAt's verify, bitrot-streaming.go:171-186, and
+// Erasure.DecodeDataBlocks, erasure-coding.go:96-109, for one batch of stripes).
+// Same contract as k_verify_reconstruct (kernels.hip) for exactly EX missing rows:
+// the k survivor rows are hashed and compared with their stored sums, the EX missing
+// rows rebuilt from the same loads (one HBM read per survivor), HOUT also hashes the
+// rebuilt rows.  Layout as k_ehx_ws: one workgroup per CU (LDS padded), G stripes;
+// the first 2*G*RH threads hash (pair form, RH = hashed rows per stripe), the other
+// G*T/16 rebuild (16-byte columns, untracked loads PF tiles ahead, exact vmcnt waits).
+template <int K, int EX, bool HOUT, int G, int T, int PF>
+__global__ void __launch_bounds__((2 * G * (K + (HOUT ? EX : 0)) + G * (T / 16))) __attribute__((amdgpu_waves_per_eu(2)))
+k_vr_ws(VrArgs a) {
+    constexpr int RH = K + (HOUT ? EX : 0);
+    constexpr int NH = 2 * G * RH;
+    constexpr int CPS = T / 16;
+    constexpr int NE = G * CPS;
+    constexpr int NT = NH + NE;
+    constexpr int TS = T + 16;
+    constexpr int NPK = T / 32;
+    constexpr int NTAB = (EX > 0 ? EX : 1) * K * 8;
+    static_assert(NH % 64 == 0 && NE % 64 == 0 && T % 32 == 0, "whole wavefronts per role");
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem_dyn[];
+    uint8_t(*tile)[G * RH * TS] = reinterpret_cast<uint8_t(*)[G * RH * TS]>(smem_dyn);
+    __shared__ __attribute__((aligned(16))) uint32_t tabs[NTAB];
+    __shared__ int32_t srows[K + EX];
+
+    const int tid = threadIdx.x;
+    const int64_t blk0 = (int64_t)blockIdx.x * G;
+    const int64_t S = a.S;
+    const int R = a.k + a.m;
+    if (EX > 0)
+        for (int i = tid; i < EX * K * 8; i += NT) tabs[i] = a.tables[i];
+    for (int i = tid; i < K + EX; i += NT) srows[i] = a.rows[i];
+    const int64_t nfull = S / T;
+    const int tail = (int)(S - nfull * T);
+    int64_t iend = PF;
+    if (nfull >= 3 * PF) iend = PF + ((nfull - 3 * PF) / PF + 1) * PF;
+    const int64_t total = iend + 2 * PF + 1;
+
+    if (__builtin_amdgcn_readfirstlane(tid) < NH) {
+        // ---- hash role (pair form): hashed row cj of stripe g
+        const int chain = tid >> 1, hh = tid & 1;
+        const int g = chain / RH, cj = chain % RH;
+        const int row_off = chain * TS;
+        HHPair st = hh2_init(hh, a.key[0], a.key[1], a.key[2], a.key[3]);
+        lds_barrier2();  // tables / rows (matches the rebuild role)
+        lds_barrier2();  // step 0
+        for (int64_t s = 1; s <= nfull; ++s) {
+            const uint4* p = reinterpret_cast<const uint4*>(tile[(s - 1) & 1] + row_off) + hh;
+            uint4 w[NPK];
+#pragma unroll
+            for (int i = 0; i < NPK; ++i) w[i] = p[2 * i];
+#pragma unroll
+            for (int i = 0; i < NPK; ++i)
+                hh2_update(st, ((uint64_t)w[i].y << 32) | w[i].x, ((uint64_t)w[i].w << 32) | w[i].z);
+            lds_barrier2();
+        }
+        if (tail) {
+            const uint8_t* row = tile[nfull & 1] + row_off;
+            hh2_packets(st, row, tail >> 5, hh);
+            if (tail & 31) hh2_remainder(st, row + (tail & ~31), (uint32_t)(tail & 31), hh);
+        }
+        for (int64_t s = nfull + 1; s < total; ++s) lds_barrier2();
+        uint64_t d0, d1;
+        hh2_finalize256(st, d0, d1);
+        const bool live = blk0 + g < a.n_blocks;
+        const int64_t b = blk0 + g;
+        const int srow = srows[cj];
+        if (cj < K) {
+            // errFileCorrupt per (stripe, survivor): either half of the digest differs
+            bool mis = false;
+            if (live) {
+                uint64_t e0, e1;
+                __builtin_memcpy(&e0, a.expect + (b * R + srow) * 32 + 16 * hh, 8);
+                __builtin_memcpy(&e1, a.expect + (b * R + srow) * 32 + 16 * hh + 8, 8);
+                mis = e0 != d0 || e1 != d1;
+            }
+            const unsigned long long m = __ballot(mis);
+            const bool bad = ((m >> (tid & 62)) & 3ull) != 0;
+            if (live && hh == 0) a.bad[b * R + srow] = bad ? 1 : 0;
+        } else if (HOUT && live && a.sums_out) {
+            uint64_t* out = reinterpret_cast<uint64_t*>(a.sums_out + (b * R + srow) * 32 + 16 * hh);
+            out[0] = d0;
+            out[1] = d1;
+        }
+        return;
+    }
+
+    // ---- rebuild role: 16-byte column o of stripe g
+    constexpr int NWd = 4;
+    typedef typename VecOf<NWd>::type VT;
+    const int e = tid - NH;
+    const int g = e / CPS, o = (e % CPS) * 16;
+    const int64_t b = (blk0 + g) < a.n_blocks ? (blk0 + g) : (a.n_blocks - 1);
+    uint8_t* blk = a.shards + b * a.block_stride + o;
+    const int col_off = g * RH * TS + o;
+    lds_barrier2();  // tables / rows visible
+    int64_t roff[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) roff[j] = (int64_t)__builtin_amdgcn_readfirstlane(srows[j]) * S;
+    int64_t ooff[EX > 0 ? EX : 1];
+#pragma unroll
+    for (int r = 0; r < EX; ++r) ooff[r] = (int64_t)__builtin_amdgcn_readfirstlane(srows[K + r]) * S;
+
+    VT x[PF][K];
+    auto load = [&](VT (&xs)[K], int64_t t0) {
+#pragma unroll
+        for (int j = 0; j < K; ++j) ld_async<NWd>(xs[j], blk + roff[j] + t0);
+    };
+    auto prefetch_any = [&](VT (&xs)[K], int64_t tn) {
+        const bool ok = tn < nfull || (tn == nfull && o < tail);
+        load(xs, ok ? tn * T : 0);
+    };
+    // survivors to LDS, rebuilt rows into y (and LDS when hashed)
+    auto rebuild = [&](VT (&xr)[K], uint8_t* tl, Col<NWd> (&y)[EX > 0 ? EX : 1]) {
+        Col<NWd> xs[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) xs[j] = to_col<NWd>(xr[j]);
+        if constexpr (EX > 0) {
+            const uint32_t* tb = tabs + opaque_zero();
+#pragma unroll
+            for (int r = 0; r < EX; ++r) {
+                GfAcc acc[NWd];
+#pragma unroll
+                for (int w = 0; w < NWd; ++w) acc_init(acc[w]);
+#pragma unroll
+                for (int j = 0; j < K; ++j) {
+                    const CoefTab t = load_coef(tb, r * K + j);
+#pragma unroll
+                    for (int w = 0; w < NWd; ++w) acc_add(acc[w], gf_lookup(split_nibbles(xs[j].w[w]), t));
+                }
+#pragma unroll
+                for (int w = 0; w < NWd; ++w) y[r].w[w] = acc_done(acc[w]);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < K; ++j) st_col<NWd>(tl + col_off + j * TS, xs[j]);
+        if constexpr (HOUT) {
+#pragma unroll
+            for (int r = 0; r < EX; ++r) st_col<NWd>(tl + col_off + (K + r) * TS, y[r]);
+        }
+    };
+    auto store_rows = [&](const Col<NWd> (&y)[EX > 0 ? EX : 1], int64_t t0) {
+#pragma unroll
+        for (int r = 0; r < EX; ++r) st_col<NWd>(blk + ooff[r] + t0, y[r]);
+    };
+    auto step = [&](VT (&xs)[K], int64_t ti) {
+        Col<NWd> y[EX > 0 ? EX : 1];
+        vm_wait<EX + (PF - 1) * (K + EX)>(xs);
+        rebuild(xs, tile[ti & 1], y);
+        load(xs, (ti + PF) * T);
+        store_rows(y, ti * T);
+        lds_barrier2();
+    };
+    auto edge = [&](VT (&xs)[K], int64_t ti) {
+        const bool full = ti < nfull, part = ti == nfull && tail;
+        vm_wait<0>(xs);
+        Col<NWd> y[EX > 0 ? EX : 1];
+        if (full || part) rebuild(xs, tile[ti & 1], y);
+        prefetch_any(xs, ti + PF);
+        if (full || (part && o < tail)) store_rows(y, ti * T);
+        lds_barrier2();
+    };
+#pragma unroll
+    for (int p = 0; p < PF; ++p) prefetch_any(x[p], p);
+    // edge(0) is step 0: its barrier pairs with the hash role's second barrier
+#pragma unroll
+    for (int p = 0; p < PF; ++p) edge(x[p], p);
+    int64_t i = PF;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (; i + 2 * PF <= nfull; i += PF) {
+#pragma unroll
+        for (int p = 0; p < PF; ++p) step(x[p], i + p);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int p = 0; p < 2 * PF; ++p) edge(x[p % PF], i + p);
+    lds_barrier2();  // the hash-only step
+#pragma unroll
+    for (int p = 0; p < PF; ++p) vm_wait<0>(x[p]);
+}
+
+template <int K, int EX, bool HOUT, int G, int T, int PF>
+static bool launch_vr_ws_t(const VrArgs& a, hipStream_t s) {
+    constexpr int RH = K + (HOUT ? EX : 0);
+    constexpr int NT = 2 * G * RH + G * (T / 16);
+    constexpr size_t tiles = (size_t)2 * G * RH * (T + 16);
+    constexpr size_t dyn = tiles > 83968 ? tiles : 83968;  // one workgroup per CU
+    if constexpr (dyn + (size_t)(EX > 0 ? EX : 1) * K * 32 + 4 * (K + EX) > 163840 || NT > 1024 ||
+                  (2 * G * RH) % 64 != 0 || (G * (T / 16)) % 64 != 0) {
+        return false;
+    } else {
+        if (a.e != EX || (a.S % 16) != 0 || a.k != K || (HOUT != (a.sums_out != nullptr) && EX > 0)) return false;
+        auto kern = k_vr_ws<K, EX, HOUT, G, T, PF>;
+        static bool attr = false;
+        if (!attr) {
+            if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn) !=
+                hipSuccess)
+                return false;
+            attr = true;
+        }
+        const int64_t grid = (a.n_blocks + G - 1) / G;
+        hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), dyn, s, a);
+        return true;
+    }
+}
+
+// RS(8+4)-shaped GET: 16 stripes, 256-byte tiles, verify-only or rebuild 2.  Heal
+// (HOUT: 10 hashed rows, 9 waves, 168 VGPRs) spills in this form and stays on
+// k_verify_reconstruct (measured 4.7 / 1.9 ms vs 1.5 ms).
+bool launch_vr_ws(int v, const VrArgs& a, hipStream_t s) {
+    if (a.k != 8 || a.sums_out != nullptr) return false;
+    switch (v) {
+        case 0:
+        case 210:
+            if (a.e == 0) return launch_vr_ws_t<8, 0, false, 16, 256, 2>(a, s);
+            if (a.e == 2) return launch_vr_ws_t<8, 2, false, 16, 256, 2>(a, s);
+            return false;
+        case 211:
+            if (a.e == 0) return launch_vr_ws_t<8, 0, false, 16, 256, 1>(a, s);
+            if (a.e == 2) return launch_vr_ws_t<8, 2, false, 16, 256, 1>(a, s);
+            return false;
+        default:
+            return false;
     }
 }
 

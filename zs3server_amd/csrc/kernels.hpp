@@ -99,6 +99,8 @@ bool has_fast_encode(int k, int m);
 // Second-generation fused encode+hash kernel (fused_v2.hip), variant numbers 50+.
 // Returns false when the variant does not apply to a.k/a.m (caller falls back).
 bool launch_ehx(int v, const EncArgs& a, hipStream_t s);
+// Warp-specialised GET / heal pass (fused_v2.hip); false if the shape has no instance.
+bool launch_vr_ws(int v, const VrArgs& a, hipStream_t s);
 
 // Tuning knob for experiments: 0 = default variant.
 void set_variant(int v);

@@ -74,7 +74,7 @@ WS_CASES = [(8, 4, 1 << 16, []), (8, 4, 1 << 16, [0, 5]), (8, 4, 1 << 16, [3, 9]
 @pytest.mark.parametrize("k,m,blen,erased", WS_CASES)
 @pytest.mark.parametrize("data_only", [True, False])
 @pytest.mark.parametrize("heal", [False, True])
-@pytest.mark.parametrize("variant", [210, 211])
+@pytest.mark.parametrize("variant", [210, 211, 212, 213])
 def test_verify_reconstruct_ws(oracle, k, m, blen, erased, data_only, heal, variant):
     z.set_variant(variant)
     try:
@@ -181,7 +181,7 @@ def test_fused_kernel_selected():
 @pytest.mark.parametrize("k,m,blen,erased,heal", [(8, 4, 8 * 640, [], False), (8, 4, 8 * 640, [0, 5], False),
                                                   (8, 4, 8 * 640, [2, 10], True), (4, 2, 4 * 512, [1], True),
                                                   (16, 4, 16 * 256, [3, 17], False)])
-@pytest.mark.parametrize("variant", [0, 200, 201, 211])
+@pytest.mark.parametrize("variant", [0, 200, 201, 211, 212])
 def test_verify_reconstruct_large_batch(oracle, k, m, blen, erased, heal, variant):
     """4096 stripes through the default launch (k_vr_ws where it applies), the
     first-generation kernel (200), its one-workgroup-per-CU launch (201) and k_vr_ws

@@ -789,12 +789,12 @@ static bool launch_ehx_km(int v, const EncArgs& a, hipStream_t s) {
 // rebuilt rows.  Layout as k_ehx_ws: one workgroup per CU (LDS padded), G stripes;
 // the first 2*G*RH threads hash (pair form, RH = hashed rows per stripe), the other
 // G*T/16 rebuild (16-byte columns, untracked loads PF tiles ahead, exact vmcnt waits).
-template <int K, int EX, bool HOUT, int G, int T, int PF>
-__global__ void __launch_bounds__((2 * G * (K + (HOUT ? EX : 0)) + G * (T / 16))) __attribute__((amdgpu_waves_per_eu(2)))
+template <int K, int EX, bool HOUT, int G, int T, int PF, int CW = 16>
+__global__ void __launch_bounds__((2 * G * (K + (HOUT ? EX : 0)) + G * (T / CW))) __attribute__((amdgpu_waves_per_eu(2)))
 k_vr_ws(VrArgs a) {
     constexpr int RH = K + (HOUT ? EX : 0);
     constexpr int NH = 2 * G * RH;
-    constexpr int CPS = T / 16;
+    constexpr int CPS = T / CW;
     constexpr int NE = G * CPS;
     constexpr int NT = NH + NE;
     constexpr int TS = T + 16;
@@ -868,11 +868,11 @@ k_vr_ws(VrArgs a) {
         return;
     }
 
-    // ---- rebuild role: 16-byte column o of stripe g
-    constexpr int NWd = 4;
+    // ---- rebuild role: CW-byte column o of stripe g
+    constexpr int NWd = CW / 4;
     typedef typename VecOf<NWd>::type VT;
     const int e = tid - NH;
-    const int g = e / CPS, o = (e % CPS) * 16;
+    const int g = e / CPS, o = (e % CPS) * CW;
     const int64_t b = (blk0 + g) < a.n_blocks ? (blk0 + g) : (a.n_blocks - 1);
     uint8_t* blk = a.shards + b * a.block_stride + o;
     const int col_off = g * RH * TS + o;
@@ -913,6 +913,8 @@ k_vr_ws(VrArgs a) {
                 }
 #pragma unroll
                 for (int w = 0; w < NWd; ++w) y[r].w[w] = acc_done(acc[w]);
+                // one rebuilt row at a time: its K coefficient tables, not all E*K, live
+                __builtin_amdgcn_sched_barrier(0);
             }
         }
 #pragma unroll
@@ -962,18 +964,18 @@ k_vr_ws(VrArgs a) {
     for (int p = 0; p < PF; ++p) vm_wait<0>(x[p]);
 }
 
-template <int K, int EX, bool HOUT, int G, int T, int PF>
+template <int K, int EX, bool HOUT, int G, int T, int PF, int CW = 16>
 static bool launch_vr_ws_t(const VrArgs& a, hipStream_t s) {
     constexpr int RH = K + (HOUT ? EX : 0);
-    constexpr int NT = 2 * G * RH + G * (T / 16);
+    constexpr int NT = 2 * G * RH + G * (T / CW);
     constexpr size_t tiles = (size_t)2 * G * RH * (T + 16);
     constexpr size_t dyn = tiles > 83968 ? tiles : 83968;  // one workgroup per CU
     if constexpr (dyn + (size_t)(EX > 0 ? EX : 1) * K * 32 + 4 * (K + EX) > 163840 || NT > 1024 ||
-                  (2 * G * RH) % 64 != 0 || (G * (T / 16)) % 64 != 0) {
+                  (2 * G * RH) % 64 != 0 || (G * (T / CW)) % 64 != 0) {
         return false;
     } else {
         if (a.e != EX || (a.S % 16) != 0 || a.k != K || (HOUT != (a.sums_out != nullptr) && EX > 0)) return false;
-        auto kern = k_vr_ws<K, EX, HOUT, G, T, PF>;
+        auto kern = k_vr_ws<K, EX, HOUT, G, T, PF, CW>;
         static bool attr = false;
         if (!attr) {
             if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn) !=
@@ -987,11 +989,18 @@ static bool launch_vr_ws_t(const VrArgs& a, hipStream_t s) {
     }
 }
 
-// RS(8+4)-shaped GET: 16 stripes, 256-byte tiles, verify-only or rebuild 2.  Heal
-// (HOUT: 10 hashed rows, 9 waves, 168 VGPRs) spills in this form and stays on
-// k_verify_reconstruct (measured 4.7 / 1.9 ms vs 1.5 ms).
+// RS(8+4)-shaped GET: 16 stripes, 256-byte tiles, verify-only or rebuild 2; heal with
+// 8-byte columns (16-byte columns spill at the heal's 168-VGPR budget: 4.7 ms).
 bool launch_vr_ws(int v, const VrArgs& a, hipStream_t s) {
-    if (a.k != 8 || a.sums_out != nullptr) return false;
+    if (a.k != 8) return false;
+    if (a.sums_out != nullptr) {
+        // heal (10 hashed rows): 8-byte rebuild columns and 128-byte tiles keep the
+        // 9-wave workgroup inside 168 VGPRs (1.50 -> 1.25 ms, 1 data + 1 parity)
+        if (a.e != 2) return false;
+        if (v == 0 || v == 212) return launch_vr_ws_t<8, 2, true, 16, 128, 2, 8>(a, s);
+        if (v == 213) return launch_vr_ws_t<8, 2, true, 16, 256, 1, 8>(a, s);
+        return false;
+    }
     switch (v) {
         case 0:
         case 210:

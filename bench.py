@@ -101,8 +101,8 @@ def committed_traffic(k: int, m: int, nobj: int, blen: int):
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--objects", type=int, default=4096, help="1 MiB blocks per GPU per step")
     ap.add_argument("--k", type=int, default=8)
     ap.add_argument("--m", type=int, default=4)

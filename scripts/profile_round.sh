@@ -7,7 +7,7 @@ ROUND=${ROUND:-r01}
 OUT=gpurun_out; P=$OUT/profile/$ROUND; mkdir -p $OUT $P; export TMPDIR=/tmp
 echo "=== trace $(date +%T)"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- \
-    python bench.py --steps 20 --warmup 3 --no-cpu > $OUT/trace.log 2>&1 || { tail -20 $OUT/trace.log; exit 5; }
+    python bench.py --no-cpu > $OUT/trace.log 2>&1 || { tail -20 $OUT/trace.log; exit 5; }
 cp $(find $OUT/trace -name '*kernel_stats.csv' | head -1) $P/kernel_stats.csv
 grep '"metric"' $OUT/trace.log > $P/bench_under_rocprof.json
 cat $P/kernel_stats.csv

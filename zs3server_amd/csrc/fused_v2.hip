@@ -534,9 +534,21 @@ k_ehx_ws(EncArgs a) {
             uint4 w[NPK];
 #pragma unroll
             for (int i = 0; i < NPK; ++i) w[i] = p[2 * i];
+            if constexpr (PM == 4) __builtin_amdgcn_s_setprio(3);
 #pragma unroll
-            for (int i = 0; i < NPK; ++i)
+            for (int i = 0; i < NPK; ++i) {
+                if constexpr (PM == 4) {
+                    // progress-equalising priority: 3, 2, 1, 0 over the quarters of the tile
+                    if (i > 0 && (4 * i) % NPK == 0) {
+                        __builtin_amdgcn_sched_barrier(0);
+                        if (4 * i / NPK == 1) __builtin_amdgcn_s_setprio(2);
+                        if (4 * i / NPK == 2) __builtin_amdgcn_s_setprio(1);
+                        if (4 * i / NPK == 3) __builtin_amdgcn_s_setprio(0);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                }
                 hh2_update(st, ((uint64_t)w[i].y << 32) | w[i].x, ((uint64_t)w[i].w << 32) | w[i].z);
+            }
             bar();
         }
         if (tail) {
@@ -612,7 +624,14 @@ k_ehx_ws(EncArgs a) {
         Col<NWd> xs[K];
 #pragma unroll
         for (int j = 0; j < K; ++j) xs[j] = to_col<NWd>(xr[j]);
-        encode_dyadic<NWd, K, M>(xs, par, tabs);
+        if constexpr (PM == 4) {
+            __builtin_amdgcn_s_setprio(3);
+            encode_dyadic<NWd, K, M, true, true>(xs, par, tabs);
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_setprio(K / M >= 3 ? 0 : 1);
+        } else {
+            encode_dyadic<NWd, K, M>(xs, par, tabs);
+        }
 #pragma unroll
         for (int j = 0; j < K; ++j) st_col<NWd>(tl + col_off + j * TS, xs[j]);
 #pragma unroll
@@ -765,6 +784,7 @@ static bool launch_ehx_km(int v, const EncArgs& a, hipStream_t s) {
         case 100: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1>(a, s); else return false;
         case 103: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 2, true>(a, s); else return false;
         case 102: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, true>(a, s); else return false;
+        case 108: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 4>(a, s); else return false;
         case 105: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1>(a, s); else return false;
         case 106: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 2>(a, s); else return false;
         case 107: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 3>(a, s); else return false;

@@ -141,13 +141,20 @@ __device__ __forceinline__ int opaque_zero() {
 // y0 = Y0+Y1, y1 = Y1.
 // SB: a scheduling barrier per block keeps each block's table reads local (fewer
 // VGPRs); without it the scheduler may interleave the encode with other work.
-template <int NWd, int K, int M, bool SB = true>
+// PRS: lower the wave's issue priority by one after each block (progress-equalising
+// priority, fused_v2.hip PM = 4; the caller sets the starting priority).
+template <int NWd, int K, int M, bool SB = true, bool PRS = false>
 __device__ __forceinline__ void encode_dyadic(const Col<NWd> (&x)[K], Col<NWd> (&out)[M], const uint32_t* dtabs) {
     static_assert(M == 2 || M == 4, "dyadic block");
     uint32_t Y[M][NWd];
 #pragma unroll
     for (int q = 0; q < K / M; ++q) {
         if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
+        if constexpr (PRS) {
+            if (q == 1) __builtin_amdgcn_s_setprio(2);
+            if (q == 2) __builtin_amdgcn_s_setprio(1);
+            if (q > 0) __builtin_amdgcn_sched_barrier(0);
+        }
         const uint32_t* tq = dtabs + opaque_zero() + q * M * 8;
         CoefTab t[M];
 #pragma unroll

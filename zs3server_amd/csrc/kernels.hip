@@ -1084,6 +1084,11 @@ static hipError_t run_encode_fast(const EncArgs& a, hipStream_t s) {
             // Variant 100 (warp-specialised k_ehx_ws: 6 hash waves in the pair form + 6
             // encode waves with 16-byte columns) takes ~11 % off the compute-bound time
             // (L2-resident alias runs 1.08 -> 0.96 ms) and 3 % off the HBM launch.
+            // Variant 105 = 100 with the encode waves at issue priority 1 over the hash
+            // waves (which idle 48-68 % of a step): the SIMDs holding two encode waves no
+            // longer end each step with one encode wave issuing alone; 0-4 % per box
+            // (scripts/box_sweep.sh), never slower than 100 beyond noise.
+            if (!done && a.dyb == M && a.n_blocks >= 16 * 256) done = launch_ehx(105, a, s);
             if (!done && a.dyb == M && a.n_blocks >= 16 * 256) done = launch_ehx(100, a, s);
             if (!done && a.dyb == M && a.n_blocks >= 16 * 256) done = launch_ehx(80, a, s);
         }

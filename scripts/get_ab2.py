@@ -1,0 +1,54 @@
+"""A/B of the GET / heal launches for the RS(4+2) and RS(16+4) shapes (variant 0 =
+default dispatch, 200 = first-generation kernel), interleaved rounds."""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import zs3server_amd as z  # noqa: E402
+
+
+def timeit(fn, steps=10):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(steps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / steps
+
+
+variants = [int(v) for v in os.environ.get("VARIANTS", "0,200").split(",")]
+for k, m, nobj, cases in ((4, 2, 2048, (("verify 4", [], False), ("verify + rebuild 2", [0, 3], False),
+                                        ("verify + rebuild 1", [1], False), ("heal 2", [1, 5], True))),
+                          (16, 4, 2048, (("verify 16", [], False),))):
+    blen = 1 << 20
+    S = blen // k
+    R = k + m
+    stride = R * S
+    codec = z.Codec(k, m)
+    buf = torch.empty(nobj * stride, dtype=torch.uint8, device="cuda")
+    z.fill_batch(buf, stride, blen, nobj, seed=3)
+    sums = torch.zeros(nobj * R * 32, dtype=torch.uint8, device="cuda")
+    codec.encode_batch(buf, stride, blen, nobj, parity=buf, parity_offset=k * S, parity_stride=stride, sums=sums)
+    bad = torch.zeros((nobj, R), dtype=torch.int32, device="cuda")
+    out = torch.zeros_like(sums)
+    for rnd in range(2):
+        for name, erased, heal in cases:
+            present = [i not in erased for i in range(R)]
+            for v in variants:
+                z.set_variant(v)
+                ms = timeit(lambda: codec.verify_reconstruct_batch(buf, stride, S, nobj, present, not heal, sums, bad,
+                                                                   sums_out=out if heal else None))
+                nre = len([e for e in erased if e < k or heal])
+                nbytes = nobj * (k + nre) * S
+                print(json.dumps({"round": rnd, "k": k, "case": name, "variant": v, "ms": round(ms, 4),
+                                  "hbm_frac": round(nbytes / ms / 1e-3 / 8e12, 3),
+                                  "bad": int(bad.sum())}), flush=True)
+    del buf, sums, bad, out
+    torch.cuda.empty_cache()
+z.set_variant(0)

@@ -105,7 +105,17 @@ RECON_PATTERNS = [
 
 @pytest.mark.parametrize("k,m,erased", RECON_PATTERNS)
 @pytest.mark.parametrize("data_only", [True, False])
-def test_reconstruct_batch(oracle, k, m, erased, data_only):
+@pytest.mark.parametrize("variant", [0, 220, 221])
+def test_reconstruct_batch(oracle, k, m, erased, data_only, variant):
+    """variant 220/221: the reconstruct kernel with 2/4 columns per thread (e <= 2)."""
+    z.set_variant(variant)
+    try:
+        run_reconstruct_case(oracle, k, m, erased, data_only)
+    finally:
+        z.set_variant(0)
+
+
+def run_reconstruct_case(oracle, k, m, erased, data_only):
     blen = 1 << 16 if k in (4, 8, 16) else 4099
     nb = 3
     codec = z.Codec(k, m)

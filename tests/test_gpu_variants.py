@@ -18,7 +18,7 @@ DEV = "cuda:0"
 
 # RS(8+4) fused_v2 tile = 384 B per shard row
 SIZES_84 = [8 * 16, 8 * 384, 8 * 384 * 3, 8 * (384 * 2 + 32), 8 * (384 * 5 + 16), 1 << 20]
-VARIANTS = [0, 50, 51, 52, 53, 55, 70, 71, 80, 81, 82, 83, 84, 100, 102, 103, 104, 105, 106, 107, 108]
+VARIANTS = [0, 50, 51, 52, 53, 55, 70, 71, 80, 81, 82, 83, 84, 100, 102, 103, 104, 105, 106, 107, 108, 109]
 
 
 @pytest.fixture(scope="module", autouse=True)

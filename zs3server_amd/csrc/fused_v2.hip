@@ -784,6 +784,7 @@ static bool launch_ehx_km(int v, const EncArgs& a, hipStream_t s) {
         case 100: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1>(a, s); else return false;
         case 103: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 2, true>(a, s); else return false;
         case 102: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, true>(a, s); else return false;
+        case 109: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, true, false, 0, false, 1>(a, s); else return false;
         case 108: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 4>(a, s); else return false;
         case 105: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1>(a, s); else return false;
         case 106: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 2>(a, s); else return false;
@@ -1012,6 +1013,21 @@ static bool launch_vr_ws_t(const VrArgs& a, hipStream_t s) {
 // RS(8+4)-shaped GET: 16 stripes, 256-byte tiles, verify-only or rebuild 2; heal with
 // 8-byte columns (16-byte columns spill at the heal's 168-VGPR budget: 4.7 ms).
 bool launch_vr_ws(int v, const VrArgs& a, hipStream_t s) {
+    if (a.k == 4 && (v == 0 || v == 210)) {
+        // RS(4+2)-shaped GET / heal: 16 stripes, 256-byte tiles
+        if (a.sums_out != nullptr)
+            return a.e == 2 && launch_vr_ws_t<4, 2, true, 16, 256, 2>(a, s);
+        if (a.e == 0) return launch_vr_ws_t<4, 0, false, 16, 256, 2>(a, s);
+        if (a.e == 1) return launch_vr_ws_t<4, 1, false, 16, 256, 2>(a, s);
+        if (a.e == 2) return launch_vr_ws_t<4, 2, false, 16, 256, 2>(a, s);
+        return false;
+    }
+    if (a.k == 16 && (v == 0 || v == 210)) {
+        // RS(16+4)-shaped verify-only GET: 8 stripes, 256-byte tiles (the rebuild
+        // instances spill: 16 survivors x 16 B x 2 tiles beside 32-64 generic products)
+        if (a.sums_out != nullptr || a.e != 0) return false;
+        return launch_vr_ws_t<16, 0, false, 8, 256, 2>(a, s);
+    }
     if (a.k != 8) return false;
     if (a.sums_out != nullptr) {
         // heal (10 hashed rows): 8-byte rebuild columns and 128-byte tiles keep the

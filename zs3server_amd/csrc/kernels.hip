@@ -545,8 +545,10 @@ __global__ void __launch_bounds__(256) k_encode_only(EncArgs a) {
 
 // ---------------------------------------------------------------------------
 // Reconstruct: E_MAX output rows, each a GF combination of the K valid rows.
-template <int K, int EMAX>
+template <int K, int EMAX, int NC = 1>
 __global__ void __launch_bounds__(256) k_reconstruct(RecArgs a) {
+    // NC columns per thread (256 apart, so every load instruction stays coalesced): all
+    // NC*K survivor loads are issued before the first product (more bytes in flight).
     __shared__ __attribute__((aligned(16))) uint32_t tabs[EMAX * K * 8];
     __shared__ int32_t rows[K + EMAX];
     for (int i = threadIdx.x; i < a.e * K * 8; i += 256) tabs[i] = a.tables[i];
@@ -557,38 +559,48 @@ __global__ void __launch_bounds__(256) k_reconstruct(RecArgs a) {
     const int E = a.e;
     for (int64_t b = blockIdx.y; b < a.n_blocks; b += gridDim.y) {
         uint8_t* blk = a.shards + b * a.block_stride;
-        for (int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x; c < cols; c += (int64_t)gridDim.x * 256) {
-            const int64_t o = c * 16;
+        for (int64_t c0 = (int64_t)blockIdx.x * 256 * NC + threadIdx.x; c0 < cols; c0 += (int64_t)gridDim.x * 256 * NC) {
             const uint32_t* tbl = tabs + opaque_zero();
-            uint4 x[K];
+            uint4 x[NC][K];
 #pragma unroll
-            for (int t = 0; t < K; ++t) x[t] = ld16(blk + (int64_t)rows[t] * S + o);
-            GfAcc acc[EMAX][4];
+            for (int i = 0; i < NC; ++i) {
+                const int64_t c = c0 + 256 * i;
+                const int64_t o = (c < cols ? c : c0) * 16;
 #pragma unroll
-            for (int r = 0; r < EMAX; ++r)
+                for (int t = 0; t < K; ++t) x[i][t] = ld16(blk + (int64_t)rows[t] * S + o);
+            }
 #pragma unroll
-                for (int w = 0; w < 4; ++w) acc_init(acc[r][w]);
+            for (int i = 0; i < NC; ++i) {
+                const int64_t c = c0 + 256 * i;
+                if (c >= cols) continue;
+                const int64_t o = c * 16;
+                GfAcc acc[EMAX][4];
 #pragma unroll
-            for (int t = 0; t < K; ++t) {
-                const Nib n0 = split_nibbles(x[t].x), n1 = split_nibbles(x[t].y);
-                const Nib n2 = split_nibbles(x[t].z), n3 = split_nibbles(x[t].w);
+                for (int r = 0; r < EMAX; ++r)
+#pragma unroll
+                    for (int w = 0; w < 4; ++w) acc_init(acc[r][w]);
+#pragma unroll
+                for (int t = 0; t < K; ++t) {
+                    const Nib n0 = split_nibbles(x[i][t].x), n1 = split_nibbles(x[i][t].y);
+                    const Nib n2 = split_nibbles(x[i][t].z), n3 = split_nibbles(x[i][t].w);
+#pragma unroll
+                    for (int r = 0; r < EMAX; ++r) {
+                        if (r < E) {
+                            const CoefTab tb = load_coef(tbl, r * K + t);
+                            acc_add(acc[r][0], gf_lookup(n0, tb));
+                            acc_add(acc[r][1], gf_lookup(n1, tb));
+                            acc_add(acc[r][2], gf_lookup(n2, tb));
+                            acc_add(acc[r][3], gf_lookup(n3, tb));
+                        }
+                    }
+                }
 #pragma unroll
                 for (int r = 0; r < EMAX; ++r) {
                     if (r < E) {
-                        const CoefTab tb = load_coef(tbl, r * K + t);
-                        acc_add(acc[r][0], gf_lookup(n0, tb));
-                        acc_add(acc[r][1], gf_lookup(n1, tb));
-                        acc_add(acc[r][2], gf_lookup(n2, tb));
-                        acc_add(acc[r][3], gf_lookup(n3, tb));
+                        const uint4 p = make_uint4(acc_done(acc[r][0]), acc_done(acc[r][1]),
+                                                   acc_done(acc[r][2]), acc_done(acc[r][3]));
+                        st16(blk + (int64_t)rows[K + r] * S + o, p);
                     }
-                }
-            }
-#pragma unroll
-            for (int r = 0; r < EMAX; ++r) {
-                if (r < E) {
-                    const uint4 p = make_uint4(acc_done(acc[r][0]), acc_done(acc[r][1]),
-                                               acc_done(acc[r][2]), acc_done(acc[r][3]));
-                    st16(blk + (int64_t)rows[K + r] * S + o, p);
                 }
             }
         }
@@ -1176,6 +1188,15 @@ static hipError_t run_rec_fast(const RecArgs& a, hipStream_t s) {
     const int64_t cols = (a.S + 15) >> 4;
     const unsigned gx = (unsigned)((cols + 255) / 256);
     const unsigned gy = (unsigned)(a.n_blocks < 65535 ? a.n_blocks : 65535);
+    if (a.e <= 2 && (g_variant == 220 || g_variant == 221)) {
+        const int nc = g_variant == 220 ? 2 : 4;
+        const unsigned gx2 = (unsigned)((cols + 256 * nc - 1) / (256 * nc));
+        if (nc == 2)
+            hipLaunchKernelGGL((k_reconstruct<K, 2, 2>), dim3(gx2, gy), dim3(256), 0, s, a);
+        else
+            hipLaunchKernelGGL((k_reconstruct<K, 2, 4>), dim3(gx2, gy), dim3(256), 0, s, a);
+        return hipGetLastError();
+    }
     if (a.e <= 2)
         hipLaunchKernelGGL((k_reconstruct<K, 2>), dim3(gx, gy), dim3(256), 0, s, a);
     else

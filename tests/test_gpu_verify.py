@@ -83,6 +83,24 @@ def test_verify_reconstruct_ws(oracle, k, m, blen, erased, data_only, heal, vari
         z.set_variant(0)
 
 
+WS4_CASES = [(4, 2, 1 << 16, []), (4, 2, 1 << 16, [1]), (4, 2, 1 << 16, [0, 5]), (4, 2, 4 * 48, [2, 3]),
+             (4, 2, 4 * (256 * 3 + 16), [1, 4]), (4, 2, 4 * 256, [0])]
+
+
+@pytest.mark.parametrize("k,m,blen,erased", WS4_CASES)
+@pytest.mark.parametrize("data_only", [True, False])
+@pytest.mark.parametrize("heal", [False, True])
+@pytest.mark.parametrize("variant", [0, 210])
+def test_verify_reconstruct_ws_rs42(oracle, k, m, blen, erased, data_only, heal, variant):
+    """RS(4+2)-shaped GET / heal on k_vr_ws: quad-form (default) and pair-form (210)
+    hash waves, tile edges and dead stripes."""
+    z.set_variant(variant)
+    try:
+        run_verify_case(oracle, k, m, blen, erased, data_only, heal, nb=11)
+    finally:
+        z.set_variant(0)
+
+
 def run_verify_case(oracle, k, m, blen, erased, data_only, heal, nb=3):
     sh, sums = stripes(oracle, k, m, blen, nb)
     S = sh.shape[2]
@@ -181,7 +199,7 @@ def test_fused_kernel_selected():
 @pytest.mark.parametrize("k,m,blen,erased,heal", [(8, 4, 8 * 640, [], False), (8, 4, 8 * 640, [0, 5], False),
                                                   (8, 4, 8 * 640, [2, 10], True), (4, 2, 4 * 512, [1], True),
                                                   (16, 4, 16 * 256, [3, 17], False)])
-@pytest.mark.parametrize("variant", [0, 200, 201, 211, 212])
+@pytest.mark.parametrize("variant", [0, 200, 201, 210, 211, 212])
 def test_verify_reconstruct_large_batch(oracle, k, m, blen, erased, heal, variant):
     """4096 stripes through the default launch (k_vr_ws where it applies), the
     first-generation kernel (200), its one-workgroup-per-CU launch (201) and k_vr_ws

@@ -810,15 +810,22 @@ static bool launch_ehx_km(int v, const EncArgs& a, hipStream_t s) {
 // rebuilt rows.  Layout as k_ehx_ws: one workgroup per CU (LDS padded), G stripes;
 // the first 2*G*RH threads hash (pair form, RH = hashed rows per stripe), the other
 // G*T/16 rebuild (16-byte columns, untracked loads PF tiles ahead, exact vmcnt waits).
-template <int K, int EX, bool HOUT, int G, int T, int PF, int CW = 16>
-__global__ void __launch_bounds__((2 * G * (K + (HOUT ? EX : 0)) + G * (T / CW))) __attribute__((amdgpu_waves_per_eu(2)))
+template <int G, int RH, bool HQ>
+constexpr int vr_nh() {
+    return HQ ? ((4 * G * RH + 63) / 64) * 64 : 2 * G * RH;
+}
+
+// HQ: quad-form hash waves (one HH lane per thread; pad quads hash a real row and
+// discard the digest) for chain-latency-bound shapes (few chains per CU, e.g. RS(4+2)).
+template <int K, int EX, bool HOUT, int G, int T, int PF, int CW = 16, bool HQ = false>
+__global__ void __launch_bounds__((vr_nh<G, K + (HOUT ? EX : 0), HQ>() + G * (T / CW))) __attribute__((amdgpu_waves_per_eu(2)))
 k_vr_ws(VrArgs a) {
     constexpr int RH = K + (HOUT ? EX : 0);
-    constexpr int NH = 2 * G * RH;
+    constexpr int NH = vr_nh<G, RH, HQ>();
     constexpr int CPS = T / CW;
     constexpr int NE = G * CPS;
     constexpr int NT = NH + NE;
-    constexpr int TS = T + 16;
+    constexpr int TS = HQ ? T + 32 : T + 16;
     constexpr int NPK = T / 32;
     constexpr int NTAB = (EX > 0 ? EX : 1) * K * 8;
     static_assert(NH % 64 == 0 && NE % 64 == 0 && T % 32 == 0, "whole wavefronts per role");
@@ -840,7 +847,51 @@ k_vr_ws(VrArgs a) {
     if (nfull >= 3 * PF) iend = PF + ((nfull - 3 * PF) / PF + 1) * PF;
     const int64_t total = iend + 2 * PF + 1;
 
-    if (__builtin_amdgcn_readfirstlane(tid) < NH) {
+    if (HQ && __builtin_amdgcn_readfirstlane(tid) < NH) {
+        // ---- hash role (quad form): lane `lane` of hashed row cj of stripe g
+        const int chain = tid >> 2, lane = tid & 3;
+        const int crow = chain < G * RH ? chain : chain - G * RH;
+        const int g = crow / RH, cj = crow % RH;
+        const int row_off = crow * TS + 8 * lane;
+        const uint32_t sel = zipper_sel(lane);
+        HHLane st = hh_init(lane, a.key[0], a.key[1], a.key[2], a.key[3]);
+        lds_barrier2();  // tables / rows (matches the rebuild role)
+        lds_barrier2();  // step 0
+        for (int64_t s = 1; s <= nfull; ++s) {
+            const uint64_t* p = reinterpret_cast<const uint64_t*>(tile[(s - 1) & 1] + row_off);
+            uint64_t w[NPK];
+#pragma unroll
+            for (int i = 0; i < NPK; ++i) w[i] = p[4 * i];
+#pragma unroll
+            for (int i = 0; i < NPK; ++i) hh_update(st, w[i], sel);
+            lds_barrier2();
+        }
+        if (tail) {
+            const uint8_t* row = tile[nfull & 1] + crow * TS;
+            hh_packets(st, row, tail >> 5, lane, sel);
+            if (tail & 31) hh_remainder(st, row + (tail & ~31), (uint32_t)(tail & 31), lane, sel);
+        }
+        for (int64_t s = nfull + 1; s < total; ++s) lds_barrier2();
+        const uint64_t h = hh_finalize256(st, lane, sel);
+        const bool live = chain < G * RH && blk0 + g < a.n_blocks;
+        const int64_t b = blk0 + g;
+        const int srow = srows[cj];
+        if (cj < K) {
+            bool mis = false;
+            if (live) {
+                uint64_t want;
+                __builtin_memcpy(&want, a.expect + (b * R + srow) * 32 + 8 * lane, 8);
+                mis = want != h;
+            }
+            const unsigned long long m = __ballot(mis);
+            const bool bad = ((m >> (tid & 60)) & 0xFull) != 0;
+            if (live && lane == 0) a.bad[b * R + srow] = bad ? 1 : 0;
+        } else if (HOUT && live && a.sums_out) {
+            *reinterpret_cast<uint64_t*>(a.sums_out + (b * R + srow) * 32 + 8 * lane) = h;
+        }
+        return;
+    }
+    if (!HQ && __builtin_amdgcn_readfirstlane(tid) < NH) {
         // ---- hash role (pair form): hashed row cj of stripe g
         const int chain = tid >> 1, hh = tid & 1;
         const int g = chain / RH, cj = chain % RH;
@@ -985,18 +1036,18 @@ k_vr_ws(VrArgs a) {
     for (int p = 0; p < PF; ++p) vm_wait<0>(x[p]);
 }
 
-template <int K, int EX, bool HOUT, int G, int T, int PF, int CW = 16>
+template <int K, int EX, bool HOUT, int G, int T, int PF, int CW = 16, bool HQ = false>
 static bool launch_vr_ws_t(const VrArgs& a, hipStream_t s) {
     constexpr int RH = K + (HOUT ? EX : 0);
-    constexpr int NT = 2 * G * RH + G * (T / CW);
-    constexpr size_t tiles = (size_t)2 * G * RH * (T + 16);
+    constexpr int NT = vr_nh<G, RH, HQ>() + G * (T / CW);
+    constexpr size_t tiles = (size_t)2 * G * RH * (HQ ? T + 32 : T + 16);
     constexpr size_t dyn = tiles > 83968 ? tiles : 83968;  // one workgroup per CU
     if constexpr (dyn + (size_t)(EX > 0 ? EX : 1) * K * 32 + 4 * (K + EX) > 163840 || NT > 1024 ||
-                  (2 * G * RH) % 64 != 0 || (G * (T / CW)) % 64 != 0) {
+                  vr_nh<G, RH, HQ>() % 64 != 0 || (G * (T / CW)) % 64 != 0) {
         return false;
     } else {
         if (a.e != EX || (a.S % 16) != 0 || a.k != K || (HOUT != (a.sums_out != nullptr) && EX > 0)) return false;
-        auto kern = k_vr_ws<K, EX, HOUT, G, T, PF, CW>;
+        auto kern = k_vr_ws<K, EX, HOUT, G, T, PF, CW, HQ>;
         static bool attr = false;
         if (!attr) {
             if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn) !=
@@ -1013,8 +1064,19 @@ static bool launch_vr_ws_t(const VrArgs& a, hipStream_t s) {
 // RS(8+4)-shaped GET: 16 stripes, 256-byte tiles, verify-only or rebuild 2; heal with
 // 8-byte columns (16-byte columns spill at the heal's 168-VGPR budget: 4.7 ms).
 bool launch_vr_ws(int v, const VrArgs& a, hipStream_t s) {
-    if (a.k == 4 && (v == 0 || v == 210)) {
-        // RS(4+2)-shaped GET / heal: 16 stripes, 256-byte tiles
+    if (a.k == 4 && (v == 0 || v == 214)) {
+        // RS(4+2)-shaped GET / heal default: quad-form hash waves, 8 stripes, one wave
+        // of each kind per SIMD (the 8 192 chains of a 2048-object batch are
+        // latency-bound: verify 0.63 -> 0.44 ms over the pair form)
+        if (a.sums_out != nullptr)
+            return a.e == 2 && launch_vr_ws_t<4, 2, true, 8, 256, 4, 16, true>(a, s);
+        if (a.e == 0) return launch_vr_ws_t<4, 0, false, 8, 256, 4, 16, true>(a, s);
+        if (a.e == 1) return launch_vr_ws_t<4, 1, false, 8, 256, 4, 16, true>(a, s);
+        if (a.e == 2) return launch_vr_ws_t<4, 2, false, 8, 256, 4, 16, true>(a, s);
+        return false;
+    }
+    if (a.k == 4 && v == 210) {
+        // RS(4+2)-shaped GET / heal, pair-form hash waves: 16 stripes, 256-byte tiles
         if (a.sums_out != nullptr)
             return a.e == 2 && launch_vr_ws_t<4, 2, true, 16, 256, 2>(a, s);
         if (a.e == 0) return launch_vr_ws_t<4, 0, false, 16, 256, 2>(a, s);

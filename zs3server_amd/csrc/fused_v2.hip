@@ -410,21 +410,23 @@ constexpr int ws_nh() {
 }
 // Encode column width: 16 bytes, 8 for K > 8 (16 rows of 16-byte columns do not fit
 // the 168-VGPR budget beside the encode's working set).
-template <int K>
+template <int K, int CWX = 0>
 constexpr int ws_cwe() {
-    return K > 8 ? 8 : 16;
+    return CWX ? CWX : (K > 8 ? 8 : 16);
 }
 
 // WT (diagnostic): per-wave shader cycles spent waiting at barriers, into the dbg stamps.
 // PM (issue-priority experiments): 1 = encode waves s_setprio 1 over hash waves; 2 = as 1
 // plus the younger encode wave of each SIMD-sharing pair (waves w, w+4) at 2; 3 = hash
 // waves at 1.
-template <int K, int M, int G, int T, int PF, bool BUF = false, bool HQ = false, bool WT = false, int PM = 0>
-__global__ void __launch_bounds__((ws_nh<K, M, G, T, HQ>() + G * (T / ws_cwe<K>()))) __attribute__((amdgpu_waves_per_eu(3)))
+// CWX: encode column width override (0 = ws_cwe's default).
+template <int K, int M, int G, int T, int PF, bool BUF = false, bool HQ = false, bool WT = false, int PM = 0,
+          int CWX = 0>
+__global__ void __launch_bounds__((ws_nh<K, M, G, T, HQ>() + G * (T / ws_cwe<K, CWX>()))) __attribute__((amdgpu_waves_per_eu(3)))
 k_ehx_ws(EncArgs a) {
     constexpr int R = K + M;
     constexpr int NH = ws_nh<K, M, G, T, HQ>();  // hash threads
-    constexpr int CWE = ws_cwe<K>();
+    constexpr int CWE = ws_cwe<K, CWX>();
     constexpr int CPS = T / CWE;    // encode columns per stripe row
     constexpr int NE = G * CPS;     // encode threads
     constexpr int NT = NH + NE;
@@ -693,10 +695,10 @@ k_ehx_ws(EncArgs a) {
 }
 
 template <int K, int M, int G, int T, int PF, bool BUF = false, bool HQ = false, int LDSMIN = 0, bool WT = false,
-          int PM = 0>
+          int PM = 0, int CWX = 0>
 static bool launch_ws_t(const EncArgs& a, hipStream_t s) {
     constexpr int R = K + M;
-    constexpr int NT = ws_nh<K, M, G, T, HQ>() + G * (T / ws_cwe<K>());
+    constexpr int NT = ws_nh<K, M, G, T, HQ>() + G * (T / ws_cwe<K, CWX>());
     constexpr size_t tiles = (size_t)2 * G * R * (HQ ? T + 32 : T + 16);
     constexpr size_t dyn = tiles > (size_t)LDSMIN ? tiles : (size_t)LDSMIN;
     if constexpr (dyn + K * 32 > 163840 || NT > 1024) {
@@ -706,7 +708,7 @@ static bool launch_ws_t(const EncArgs& a, hipStream_t s) {
         if (BUF && ((G - 1) * a.data_stride + K * a.S > 0x7FFFFFFF ||
                     (G - 1) * a.parity_stride + M * a.S > 0x7FFFFFFF || a.data_stride < 0 || a.parity_stride < 0))
             return false;
-        auto kern = k_ehx_ws<K, M, G, T, PF, BUF, HQ, WT, PM>;
+        auto kern = k_ehx_ws<K, M, G, T, PF, BUF, HQ, WT, PM, CWX>;
         static bool attr = false;
         if (!attr) {
             if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn) !=

@@ -1087,10 +1087,14 @@ bool launch_vr_ws(int v, const VrArgs& a, hipStream_t s) {
         return false;
     }
     if (a.k == 16 && (v == 0 || v == 210)) {
-        // RS(16+4)-shaped verify-only GET: 8 stripes, 256-byte tiles (the rebuild
-        // instances spill: 16 survivors x 16 B x 2 tiles beside 32-64 generic products)
-        if (a.sums_out != nullptr || a.e != 0) return false;
-        return launch_vr_ws_t<16, 0, false, 8, 256, 2>(a, s);
+        // RS(16+4)-shaped GET: 8 stripes, 256-byte tiles; rebuilds with 8-byte columns
+        // (16-byte columns spill: 16 survivors x 2 tiles beside 32-64 generic products);
+        // heal (18 hashed rows) keeps the first-generation kernel
+        if (a.sums_out != nullptr) return false;
+        if (a.e == 0) return launch_vr_ws_t<16, 0, false, 8, 256, 2>(a, s);
+        if (a.e == 2) return launch_vr_ws_t<16, 2, false, 8, 256, 1, 8>(a, s);
+        if (a.e == 4) return launch_vr_ws_t<16, 4, false, 8, 256, 1, 8>(a, s);
+        return false;
     }
     if (a.k != 8) return false;
     if (a.sums_out != nullptr) {

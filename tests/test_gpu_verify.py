@@ -101,6 +101,23 @@ def test_verify_reconstruct_ws_rs42(oracle, k, m, blen, erased, data_only, heal,
         z.set_variant(0)
 
 
+WS16_HEAL_CASES = [(16, 4, 1 << 16, [0, 5]), (16, 4, 1 << 16, [3, 17]), (16, 4, 16 * 48, [2, 19]),
+                   (16, 4, 16 * (256 * 3 + 16), [0, 1, 16, 19]), (16, 4, 16 * 256, [4, 5, 6, 7]),
+                   (16, 4, 16 * (256 * 2 + 48), [15, 18])]
+
+
+@pytest.mark.parametrize("k,m,blen,erased", WS16_HEAL_CASES)
+@pytest.mark.parametrize("variant", [0, 215])
+def test_heal_ws_rs164(oracle, k, m, blen, erased, variant):
+    """RS(16+4) heal (rebuild 2 or 4 shards and hash them) on k_vr_ws with quad-form
+    hash waves: tile edges, ragged tails and dead stripes of the 8-stripe workgroup."""
+    z.set_variant(variant)
+    try:
+        run_verify_case(oracle, k, m, blen, erased, False, True, nb=11)
+    finally:
+        z.set_variant(0)
+
+
 def run_verify_case(oracle, k, m, blen, erased, data_only, heal, nb=3):
     sh, sums = stripes(oracle, k, m, blen, nb)
     S = sh.shape[2]
@@ -198,7 +215,8 @@ def test_fused_kernel_selected():
 
 @pytest.mark.parametrize("k,m,blen,erased,heal", [(8, 4, 8 * 640, [], False), (8, 4, 8 * 640, [0, 5], False),
                                                   (8, 4, 8 * 640, [2, 10], True), (4, 2, 4 * 512, [1], True),
-                                                  (16, 4, 16 * 256, [3, 17], False)])
+                                                  (16, 4, 16 * 256, [3, 17], False),
+                                                  (16, 4, 16 * 256, [3, 17], True)])
 @pytest.mark.parametrize("variant", [0, 200, 201, 210, 211, 212])
 def test_verify_reconstruct_large_batch(oracle, k, m, blen, erased, heal, variant):
     """4096 stripes through the default launch (k_vr_ws where it applies), the

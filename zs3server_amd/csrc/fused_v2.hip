@@ -1088,9 +1088,16 @@ bool launch_vr_ws(int v, const VrArgs& a, hipStream_t s) {
     }
     if (a.k == 16 && (v == 0 || v == 210)) {
         // RS(16+4)-shaped GET: 8 stripes, 256-byte tiles; rebuilds with 8-byte columns
-        // (16-byte columns spill: 16 survivors x 2 tiles beside 32-64 generic products);
-        // heal (18 hashed rows) keeps the first-generation kernel
-        if (a.sums_out != nullptr) return false;
+        // (16-byte columns spill: 16 survivors x 2 tiles beside 32-64 generic products).
+        // Heal (18 / 20 hashed rows): 2*8*18 pair-form threads are not whole waves, so
+        // the hash role runs in quad form (padded to 9 / 10 waves) beside 4 rebuild waves
+        if (a.sums_out != nullptr) {
+            if (v == 0 || v == 215) {
+                if (a.e == 2) return launch_vr_ws_t<16, 2, true, 8, 256, 1, 8, true>(a, s);
+                if (a.e == 4) return launch_vr_ws_t<16, 4, true, 8, 256, 1, 8, true>(a, s);
+            }
+            return false;
+        }
         if (a.e == 0) return launch_vr_ws_t<16, 0, false, 8, 256, 2>(a, s);
         if (a.e == 2) return launch_vr_ws_t<16, 2, false, 8, 256, 1, 8>(a, s);
         if (a.e == 4) return launch_vr_ws_t<16, 4, false, 8, 256, 1, 8>(a, s);

@@ -1268,7 +1268,7 @@ static hipError_t run_vr_k(const VrArgs& a, hipStream_t s) {
     // Default for RS(8+4)-shaped verify-only / rebuild-2 GETs: the warp-specialised
     // k_vr_ws (fused_v2.hip): verify 0.85 -> 0.70 ms, verify + rebuild 2 1.41 -> 1.13 ms
     // on 4096 x 1 MiB (scripts/get_ab.py).  Variant 200-209 keep this kernel.
-    if (g_variant == 0 || (g_variant >= 210 && g_variant <= 214))
+    if (g_variant == 0 || (g_variant >= 210 && g_variant <= 215))
         if (launch_vr_ws(g_variant, a, s)) return hipGetLastError();
     const bool hout = a.sums_out != nullptr;
     if (a.e == 0) return run_vr<K, 0, false>(a, s);

@@ -26,7 +26,8 @@ variants = [int(v) for v in os.environ.get("VARIANTS", "0,200").split(",")]
 for k, m, nobj, cases in ((4, 2, 2048, (("verify 4", [], False), ("verify + rebuild 2", [0, 3], False),
                                         ("verify + rebuild 1", [1], False), ("heal 2", [1, 5], True))),
                           (16, 4, 2048, (("verify 16", [], False), ("verify + rebuild 2", [0, 9], False),
-                                         ("verify + rebuild 4", [1, 7, 15, 19], False)))):
+                                         ("verify + rebuild 4", [1, 7, 15, 19], False),
+                                         ("heal 2", [0, 17], True), ("heal 4", [1, 7, 15, 19], True)))):
     blen = 1 << 20
     S = blen // k
     R = k + m

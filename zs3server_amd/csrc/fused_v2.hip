@@ -1090,9 +1090,11 @@ bool launch_vr_ws(int v, const VrArgs& a, hipStream_t s) {
         // RS(16+4)-shaped GET: 8 stripes, 256-byte tiles; rebuilds with 8-byte columns
         // (16-byte columns spill: 16 survivors x 2 tiles beside 32-64 generic products).
         // Heal (18 / 20 hashed rows): 2*8*18 pair-form threads are not whole waves, so
-        // the hash role runs in quad form (padded to 9 / 10 waves) beside 4 rebuild waves
+        // the hash role runs in quad form (padded to 9 / 10 waves) beside 4 rebuild waves.
+        // Measured slower than the first-generation kernel on 2048 x 1 MiB (heal 2: 1.29
+        // vs 0.95 ms, heal 4: 2.86 vs 1.31 ms; 13 waves leave 128 VGPRs), so opt-in only
         if (a.sums_out != nullptr) {
-            if (v == 0 || v == 215) {
+            if (v == 215) {
                 if (a.e == 2) return launch_vr_ws_t<16, 2, true, 8, 256, 1, 8, true>(a, s);
                 if (a.e == 4) return launch_vr_ws_t<16, 4, true, 8, 256, 1, 8, true>(a, s);
             }

@@ -74,6 +74,8 @@ typedef struct zs3_codec zs3_codec;
 int zs3_codec_new(int k, int m, int64_t block_size, zs3_codec** out);
 void zs3_codec_free(zs3_codec* c);
 int zs3_codec_matrix(const zs3_codec* c, uint8_t* h_out /* (k+m)*k bytes */);
+/* The codec's dataBlocks, parityBlocks and blockSize (any pointer may be NULL). */
+int zs3_codec_params(const zs3_codec* c, int* k, int* m, int64_t* block_size);
 
 /* Size arithmetic, exact Go semantics (int64, -1 = unknown length). */
 int64_t zs3_shard_size(const zs3_codec* c);                       /* Erasure.ShardSize      :122 */
@@ -143,6 +145,48 @@ int zs3_hh256_verify_batch(const uint8_t* h_key, const uint8_t* d_msgs, int64_t 
                            int64_t msg_len, int64_t n_msgs, const uint8_t* d_want,
                            int32_t* d_bad, void* stream);
 
+/* ---- per-block erasure patterns ---------------------------------------------
+ * In the reference every block is decoded with its own shard set: parallelReader
+ * nils a reader that failed or returned errFileCorrupt and reads the next shard
+ * (cmd/erasure-decode.go:166-179), so the pattern can change from one block to the
+ * next.  These take h_present as n_blocks rows of k+m bytes (row b = block b's
+ * present flags, as zs3_reconstruct_batch's h_present) and serve every block with
+ * its own (cached) decode plan; blocks sharing a pattern run in one launch.
+ * h_status (optional, host, n_blocks int32) receives each block's status (the
+ * reedsolomon error of its pattern, e.g. ZS3_ERR_TOO_FEW_SHARDS; failed blocks are
+ * not touched).  Returns ZS3_OK when every block is OK, else the first block error;
+ * the other blocks are still served.  Asynchronous on `stream` like the single-
+ * pattern calls (the patterns are read before return). */
+int zs3_reconstruct_batch_masks(const zs3_codec* c, uint8_t* d_shards, int64_t block_stride,
+                                int64_t shard_len, int64_t n_blocks, const uint8_t* h_present,
+                                int data_only, int32_t* h_status, void* stream);
+int zs3_verify_reconstruct_batch_masks(const zs3_codec* c, uint8_t* d_shards, int64_t block_stride,
+                                       int64_t shard_len, int64_t n_blocks, const uint8_t* h_present,
+                                       int data_only, const uint8_t* d_expect, int32_t* d_bad,
+                                       uint8_t* d_sums_out, int32_t* h_status, void* stream);
+
+/* HighwayHash-256 of n_msgs messages of different lengths (SURVEY.md §8b
+ * zs3_hh256_batch(key, msgs**, lens*, n)): message i is d_lens[i] bytes at
+ * d_ptrs[i] (both DEVICE arrays; the pointers are device pointers).  A reader's last
+ * chunk is shorter than the shard size (cmd/erasure-decode.go:112-114).  Digest i at
+ * d_sums + 32*i. */
+int zs3_hh256_batch_ragged(const uint8_t* h_key, const uint8_t* const* d_ptrs, const int64_t* d_lens,
+                           int64_t n_msgs, uint8_t* d_sums, void* stream);
+
+/* Deep-scan bitrotVerify for HighwayHash256S (cmd/bitrot.go:158-210, called by
+ * xlStorage.VerifyFile cmd/xl-storage.go:2386-2404): n_files shard files resident on
+ * the device in their on-disk layout [32-byte sum][chunk]* (file f at
+ * d_files + f*file_stride, file_size bytes), the sums read in place.  want_size must
+ * equal bitrotShardFileSize(part_size, shard_size), else ZS3_ERR_FILE_CORRUPT with
+ * nothing launched (bitrot.go:159-162).  Chunks: ceil(part_size/shard_size), the last
+ * one part_size - (chunks-1)*shard_size bytes.  d_bad (device, n_files*chunks int32)
+ * receives 1 for every chunk whose HighwayHash-256 differs from its stored sum;
+ * d_file_bad (optional device, n_files int32) receives 1 for every file with a bad
+ * chunk (bitrotVerify's errFileCorrupt).  *chunks_out (optional) = chunks per file. */
+int zs3_bitrot_verify_file_batch(const uint8_t* h_key, const uint8_t* d_files, int64_t file_stride,
+                                 int64_t n_files, int64_t want_size, int64_t part_size, int64_t shard_size,
+                                 int32_t* d_bad, int32_t* d_file_bad, int64_t* chunks_out, void* stream);
+
 /* ---- PUT-stream object digests ------------------------------- */
 
 /* S3 ETag of n_msgs objects: MD5 (RFC 1321, Go crypto/md5) of message i = d_msgs +
@@ -204,21 +248,81 @@ int zs3_hh256(const uint8_t* h_key, const uint8_t* h_msg, int64_t len, uint8_t* 
 int64_t zs3_stream_encode(const zs3_codec* c, const uint8_t* h_src, int64_t total_len,
                           uint8_t* h_parity, uint8_t* h_sums, int64_t batch_blocks);
 
+/* ---- cross-request batching queue (SURVEY.md §8b Threading, §7 iv) ----------------
+ * The reference calls EncodeData / DecodeDataBlocks once per 1 MiB block per request
+ * (cmd/erasure-encode.go:83-111, cmd/erasure-decode.go:230-276); one block is far too
+ * little work for one device round trip.  A queue gathers the blocks that concurrent
+ * callers (OS threads: every goroutine inside cgo holds one) submit into device
+ * batches on its own streams and pinned staging:
+ *   - a block is copied into the queue's pinned staging by its submitting thread;
+ *   - a batch is launched when it is full, when the device has nothing in flight
+ *     (batch while busy), when its oldest block has waited max_wait_us, or on flush;
+ *   - zs3_req_wait blocks until the batch is done and copies this block's results
+ *     back into the caller's buffers (again on the caller's thread).
+ * All entry points are thread-safe.  Every submitted request must be waited for
+ * exactly once (before zs3_queue_free).  A submit may block while every staging slot
+ * is busy, until earlier requests are waited for. */
+typedef struct zs3_queue zs3_queue;
+typedef struct zs3_req zs3_req;
+typedef struct {
+    int device;       /* HIP device ordinal; -1 = the calling thread's current device */
+    int max_batch;    /* blocks per device batch (0 = 128) */
+    int max_wait_us;  /* longest a block waits for its batch to fill (0 = 200) */
+    int slots;        /* pinned staging slots per lane (0 = 3; at least 2) */
+} zs3_queue_opts;
+
+int zs3_queue_new(const zs3_codec* c, const zs3_queue_opts* opts /* NULL = defaults */, zs3_queue** out);
+void zs3_queue_free(zs3_queue* q);
+
+/* EncodeData (erasure-coding.go:77-91) of one block plus the k+m bitrot sums
+ * (bitrot-streaming.go:47-49), exactly as zs3_encode_data: h_buf holds len data
+ * bytes and has capacity cap >= (k+m)*S'; after zs3_req_wait bytes [len, k*S') are
+ * zero, parity row r is at h_buf + (k+r)*S' and h_sums (optional) holds the (k+m)
+ * digests.  len == 0 (the empty object) returns ZS3_OK and *req = NULL.  The buffers
+ * must stay valid until zs3_req_wait returns. */
+int zs3_queue_submit_encode(zs3_queue* q, uint8_t* h_buf, int64_t len, int64_t cap, uint8_t* h_sums,
+                            zs3_req** req);
+
+/* One block of k+m rows of shard_len bytes at h_shards (row i at h_shards +
+ * i*shard_len; missing rows hold anything) with its own h_present[k+m].
+ * data_only != 0: DecodeDataBlocks (missing data rows rebuilt); 0: Erasure.Heal's
+ * DecodeDataAndParityBlocks (all missing rows rebuilt; h_sums_out, if given, receives
+ * the HighwayHash-256 of every rebuilt row at i*32).  With h_expect ([k+m][32], the
+ * sums stored in front of each chunk) the k survivors are verified in the same pass:
+ * zs3_req_wait then returns ZS3_ERR_FILE_CORRUPT when any failed and h_bad (optional,
+ * k+m int32) flags which (parallelReader drops that shard and reads the next,
+ * erasure-decode.go:166-179; the rebuilt rows are invalid then).  zs3_req_wait
+ * returns ZS3_OK or the block's reedsolomon error (e.g. ZS3_ERR_TOO_FEW_SHARDS). */
+int zs3_queue_submit_decode(zs3_queue* q, uint8_t* h_shards, int64_t shard_len, const uint8_t* h_present,
+                            int data_only, const uint8_t* h_expect, int32_t* h_bad, uint8_t* h_sums_out,
+                            zs3_req** req);
+
+/* Wait for one request, copy its results out, free the handle.  Returns S' for an
+ * encode request, ZS3_OK for a decode request, or an error. */
+int64_t zs3_req_wait(zs3_req* req);
+int zs3_queue_flush(zs3_queue* q);   /* launch the open batches now */
+int zs3_queue_stats(const zs3_queue* q, int64_t* batches, int64_t* blocks);
+
+/* Synchronous conveniences (submit + wait): what the cgo shim calls per block. */
+int64_t zs3_queue_encode_data(zs3_queue* q, uint8_t* h_buf, int64_t len, int64_t cap, uint8_t* h_sums);
+int zs3_queue_decode_data_blocks(zs3_queue* q, uint8_t* h_shards, int64_t shard_len, const uint8_t* h_present,
+                                 int data_only, const uint8_t* h_expect, int32_t* h_bad);
+
 /* Startup self-tests through the device path: erasureSelfTest
  * (erasure-coding.go:158-216, 60 (k, m) xxhash64 KATs + shard-0 rebuild) and
  * bitrotSelfTest (bitrot.go:218-249).  Returns ZS3_OK or ZS3_ERR_FILE_CORRUPT. */
 int zs3_selftest(void);
 
-/* Which kernel served the last batch call on this thread: 1 = specialised
- * (k, m) kernel, 0 = generic byte kernel. */
+/* Which kernel family served the last batch call on this thread (ZS3_PATH_*):
+ * 0 = generic byte kernel, 1 = first-generation specialised (k, m) kernel,
+ * 2 = warp-specialised kernel (k_ehx_ws / k_vr_ws), 3 = mixed-wave second-generation
+ * encode (k_ehx); -1 = nothing launched. */
+#define ZS3_PATH_NONE      -1
+#define ZS3_PATH_GENERIC    0
+#define ZS3_PATH_FIRSTGEN   1
+#define ZS3_PATH_WS         2
+#define ZS3_PATH_PIPE       3
 int zs3_last_path(void);
-
-/* Diagnostics: select an experimental tile/column variant of the fused encode
- * kernel for the headline shapes (0 = tuned default).  Not for production use. */
-int zs3_debug_set_variant(int variant);
-/* Diagnostics: device buffer receiving per-wave phase cycle sums from the
- * stamped variants (NULL = off). */
-int zs3_debug_set_buffer(void* d_dbg);
 
 #ifdef __cplusplus
 }

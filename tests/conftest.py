@@ -18,3 +18,11 @@ def oracle():
     from oracle import oracle_c
     oracle_c.lib()
     return oracle_c
+
+
+def variant_ctx(v: int):
+    """Variant 0 runs on the product library; any other variant on the diagnostics
+    build (libzs3gpu_diag.so), selected for this thread only."""
+    import contextlib
+    import zs3server_amd as z
+    return contextlib.nullcontext() if v == 0 else z.diag(v)

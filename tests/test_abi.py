@@ -14,8 +14,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "zs3gpu.h")
 
 
-def header_functions():
-    src = open(HEADER).read()
+DIAG_HEADER = os.path.join(ROOT, "include", "zs3gpu_diag.h")
+
+
+def header_functions(path=HEADER):
+    src = open(path).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(zs3_[a-z0-9_]+)\s*\(", src)))
 
@@ -31,11 +34,25 @@ def test_header_matches_python_export_list():
     assert header_functions() == sorted(z.EXPORTS)
 
 
+def _exports(path):
+    out = subprocess.check_output(["nm", "-D", "--defined-only", path]).decode()
+    return {line.split()[-1] for line in out.splitlines() if line.strip()}
+
+
 def test_library_exports_every_header_symbol():
-    out = subprocess.check_output(["nm", "-D", "--defined-only", z.LIB_PATH]).decode()
-    syms = {line.split()[-1] for line in out.splitlines() if line.strip()}
+    syms = _exports(z.LIB_PATH)
     missing = [f for f in header_functions() if f not in syms]
     assert not missing, missing
+
+
+def test_product_library_has_no_diagnostics():
+    """The experimental variants and the zs3_debug_* calls live only in the
+    diagnostics build; the product library exports exactly include/zs3gpu.h."""
+    assert header_functions(DIAG_HEADER) == sorted(z.DIAG_EXPORTS)
+    zs3 = {s for s in _exports(z.LIB_PATH) if s.startswith("zs3_")}
+    assert zs3 == set(header_functions())
+    dsyms = _exports(z.DIAG_LIB_PATH)
+    assert set(header_functions()) | set(z.DIAG_EXPORTS) <= dsyms
 
 
 def test_version_and_strerror():

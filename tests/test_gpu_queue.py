@@ -1,0 +1,216 @@
+"""GPU parity of the cross-request batching queue (zs3_queue_*, SURVEY.md §8b
+Threading): concurrent submitter threads — the stand-in for goroutines calling
+Erasure.EncodeData / DecodeDataBlocks per 1 MiB block inside cgo
+(cmd/erasure-encode.go:83-111, cmd/erasure-decode.go:230-276) — get bit-exact results
+while the queue gathers their blocks into shared device batches.
+
+Every expected value comes from the scalar oracle (oracle/zs3_oracle.c).
+"""
+import threading
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+import zs3server_amd as z  # noqa: E402
+
+KEY = z.MAGIC_HH256_KEY
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    z.lib()
+
+
+def run_threads(n, fn):
+    errs = []
+
+    def wrap(t):
+        try:
+            fn(t)
+        except BaseException as e:  # noqa: BLE001 - re-raised in the main thread
+            errs.append((t, e))
+
+    th = [threading.Thread(target=wrap, args=(t,)) for t in range(n)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    if errs:
+        raise errs[0][1]
+
+
+@pytest.mark.parametrize("k,m,bs", [(8, 4, 1 << 20), (4, 2, 1 << 16), (16, 4, 1 << 16), (5, 3, 100000)])
+def test_queue_encode_8_threads(oracle, k, m, bs):
+    """8 threads each push an 'object' (full blocks + a ragged last block, as the
+    Erasure.Encode block loop does) through the queue: parity in place in the caller's
+    buffer, Split zero-fill, bitrot sums, all vs the oracle; the queue batched them."""
+    codec = z.Codec(k, m, bs)
+    q = z.Queue(codec, max_batch=16, max_wait_us=300)
+    R = k + m
+    mat = oracle.build_matrix(k, m)
+    nblocks = 3 if bs >= 1 << 20 else 6
+    tails = [0, 1, 17, bs // 3 + 5, bs - 1, 33, 1000, 7]
+
+    def obj(t):
+        lens = [bs] * nblocks + ([tails[t]] if tails[t] else [])
+        for i, ln in enumerate(lens):
+            data = oracle.fill(100 + t, i, ln)
+            S = -(-ln // k)
+            buf = np.full(R * S + 64, 0xEE, dtype=np.uint8)  # capacity > (k+m)*S, junk after len
+            buf[:ln] = data
+            got_S, sums = q.encode_data(buf, ln)
+            assert got_S == S
+            want = oracle.encode_data(k, m, data, mat)
+            assert np.array_equal(buf[:R * S].reshape(R, S), want), (t, i)
+            assert np.array_equal(sums, oracle.hh256_rows(KEY, want)), (t, i)
+
+    run_threads(8, obj)
+    batches, blocks = q.stats()
+    assert blocks == sum(nblocks + (1 if tails[t] else 0) for t in range(8))
+    q.close()
+
+
+def test_queue_encode_empty_block():
+    codec = z.Codec(8, 4, 1 << 16)
+    q = z.Queue(codec)
+    S, _ = q.encode_data(np.zeros(16, np.uint8), 0)
+    assert S == 0  # EncodeData of 0 bytes: nothing to do
+    q.close()
+
+
+def _stripe(oracle, k, m, bs, seed, b, ln=None):
+    ln = bs if ln is None else ln
+    mat = oracle.build_matrix(k, m)
+    sh = oracle.encode_data(k, m, oracle.fill(seed, b, ln), mat)
+    return sh, oracle.hh256_rows(KEY, sh)
+
+
+@pytest.mark.parametrize("k,m,bs", [(8, 4, 1 << 20), (4, 2, 1 << 16), (16, 4, 1 << 16), (5, 3, 100000)])
+def test_queue_decode_mixed_patterns_8_threads(oracle, k, m, bs):
+    """8 threads decode blocks with per-block erasure patterns (GET: DecodeDataBlocks
+    with the survivors verified; HEAL: all missing rows + their sums), including a
+    rotted survivor (errFileCorrupt + its flag), too few shards (ErrTooFewShards) and a
+    short last block; every block vs the oracle."""
+    codec = z.Codec(k, m, bs)
+    q = z.Queue(codec, max_batch=8, max_wait_us=300)
+    R = k + m
+    rng_master = np.random.default_rng(k * 31 + m)
+    seeds = rng_master.integers(0, 1 << 30, size=8)
+
+    def worker(t):
+        rng = np.random.default_rng(int(seeds[t]))
+        for i in range(5):
+            short = i == 4
+            ln = (bs // 2 + 3) if short else bs
+            sh, sums = _stripe(oracle, k, m, bs, 200 + t, i, ln)
+            S = sh.shape[1]
+            heal = bool(rng.integers(0, 2))
+            e = int(rng.integers(0, m + 1))
+            missing = rng.choice(R, size=e, replace=False)
+            present = np.ones(R, bool)
+            present[missing] = False
+            work = sh.copy()
+            work[~present] = 0x5A
+            kind = int(rng.integers(0, 5))
+            if kind == 0 and e < m:  # one survivor rotted on disk
+                j = [x for x in range(R) if present[x]][0]
+                work[j, S // 2] ^= 1
+                bad = np.zeros(R, np.int32)
+                rc = q.decode(work, present, not heal, expect=sums, bad=bad)
+                assert rc == -7, (t, i, rc)
+                want = np.zeros(R, np.int32)
+                want[j] = 1
+                assert np.array_equal(bad, want), (t, i)
+                continue
+            if kind == 1:  # more than m lost
+                lost = rng.choice(R, size=m + 1, replace=False)
+                present2 = np.ones(R, bool)
+                present2[lost] = False
+                assert q.decode(work.copy(), present2, True, expect=sums) == -3
+                continue
+            out = np.zeros((R, 32), np.uint8) if heal else None
+            bad = np.full(R, 9, np.int32)
+            rc = q.decode(work, present, not heal, expect=sums, bad=bad, sums_out=out)
+            assert rc == 0, (t, i, rc)
+            assert not bad.any()
+            for r in range(R):
+                if present[r] or r < k or heal:
+                    assert np.array_equal(work[r], sh[r]), (t, i, r)
+                else:
+                    assert (work[r] == 0x5A).all(), "DecodeDataBlocks leaves missing parity alone"
+            if heal:
+                for r in np.nonzero(~present)[0]:
+                    assert np.array_equal(out[r], sums[r]), (t, i, r)
+
+    run_threads(8, worker)
+    q.close()
+
+
+def test_queue_mixed_encode_and_decode_concurrently(oracle):
+    """Encoders and decoders share one queue (separate lanes, same device)."""
+    k, m, bs = 8, 4, 1 << 16
+    codec = z.Codec(k, m, bs)
+    q = z.Queue(codec, max_batch=32)
+    R = k + m
+    mat = oracle.build_matrix(k, m)
+
+    def worker(t):
+        for i in range(12):
+            if t % 2 == 0:
+                data = oracle.fill(300 + t, i, bs)
+                buf = np.zeros(R * (bs // k), np.uint8)
+                buf[:bs] = data
+                S, sums = q.encode_data(buf, bs)
+                want = oracle.encode_data(k, m, data, mat)
+                assert np.array_equal(buf.reshape(R, S), want)
+                assert np.array_equal(sums, oracle.hh256_rows(KEY, want))
+            else:
+                sh, sums = _stripe(oracle, k, m, bs, 400 + t, i)
+                present = np.ones(R, bool)
+                present[[i % k, (i + 5) % R]] = False
+                work = sh.copy()
+                work[~present] = 0
+                assert q.decode(work, present, True, expect=sums) == 0
+                assert np.array_equal(work[:k], sh[:k])
+
+    run_threads(8, worker)
+    batches, blocks = q.stats()
+    assert blocks == 8 * 12
+    q.close()
+
+
+def test_queue_batches_concurrent_blocks(oracle):
+    """Under concurrency the queue forms multi-block batches (fewer launches than
+    blocks): 16 threads x 8 blocks, async submits, then waits."""
+    k, m, bs = 8, 4, 1 << 16
+    codec = z.Codec(k, m, bs)
+    q = z.Queue(codec, max_batch=64, max_wait_us=2000)
+    R = k + m
+    mat = oracle.build_matrix(k, m)
+    S = bs // k
+
+    def worker(t):
+        bufs, reqs, sums = [], [], []
+        for i in range(8):
+            b = np.zeros(R * S, np.uint8)
+            b[:bs] = oracle.fill(500 + t, i, bs)
+            s = np.zeros(R * 32, np.uint8)
+            bufs.append(b)
+            sums.append(s)
+            reqs.append(q.submit_encode(b, bs, s))
+        for i, r in enumerate(reqs):
+            assert q.wait(r) == S
+            want = oracle.encode_data(k, m, oracle.fill(500 + t, i, bs), mat)
+            assert np.array_equal(bufs[i].reshape(R, S), want)
+            assert np.array_equal(sums[i].reshape(R, 32), oracle.hh256_rows(KEY, want))
+
+    run_threads(16, worker)
+    batches, blocks = q.stats()
+    assert blocks == 128 and batches < blocks
+    q.close()

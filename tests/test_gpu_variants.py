@@ -12,6 +12,7 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 import zs3server_amd as z  # noqa: E402
+from conftest import variant_ctx  # noqa: E402
 
 KEY = z.MAGIC_HH256_KEY
 DEV = "cuda:0"
@@ -27,10 +28,14 @@ def gpu():
         pytest.skip("no GPU")
     z.lib()
     yield
-    z.set_variant(0)
 
 
 def run_case(oracle, k, m, blen, nb, variant, seed):
+    with variant_ctx(variant):
+        _run_case(oracle, k, m, blen, nb, variant, seed)
+
+
+def _run_case(oracle, k, m, blen, nb, variant, seed):
     codec = z.Codec(k, m, 1 << 20)
     S = -(-blen // k)
     stride = (k + m) * S
@@ -39,12 +44,8 @@ def run_case(oracle, k, m, blen, nb, variant, seed):
         host[b * stride: b * stride + blen] = oracle.fill(seed, b, blen)
     d = torch.from_numpy(host).to(DEV)
     sums = torch.zeros(nb * (k + m) * 32, dtype=torch.uint8, device=DEV)
-    z.set_variant(variant)
-    try:
-        codec.encode_batch(d, stride, blen, nb, parity=d, parity_offset=k * S, parity_stride=stride, sums=sums)
-        torch.cuda.synchronize()
-    finally:
-        z.set_variant(0)
+    codec.encode_batch(d, stride, blen, nb, parity=d, parity_offset=k * S, parity_stride=stride, sums=sums)
+    torch.cuda.synchronize()
     out = d.cpu().numpy().reshape(nb, k + m, S)
     hs = sums.cpu().numpy().reshape(nb, k + m, 32)
     mat = oracle.build_matrix(k, m)

@@ -15,6 +15,7 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 import zs3server_amd as z  # noqa: E402
+from conftest import variant_ctx  # noqa: E402
 from zs3server_amd import erasure as ze  # noqa: E402
 
 KEY = z.MAGIC_HH256_KEY
@@ -57,11 +58,8 @@ CASES = [
 def test_verify_reconstruct(oracle, k, m, blen, erased, data_only, heal, variant):
     """variant 0 = default dispatch (k_vr_ws for RS(8+4)-shaped verify / rebuild-2),
     200 = k_verify_reconstruct for every shape."""
-    z.set_variant(variant)
-    try:
+    with variant_ctx(variant):
         run_verify_case(oracle, k, m, blen, erased, data_only, heal)
-    finally:
-        z.set_variant(0)
 
 
 # warp-specialised GET / heal kernel (fused_v2.hip k_vr_ws, RS(8+4)-shaped, e = 0 or 2):
@@ -76,11 +74,8 @@ WS_CASES = [(8, 4, 1 << 16, []), (8, 4, 1 << 16, [0, 5]), (8, 4, 1 << 16, [3, 9]
 @pytest.mark.parametrize("heal", [False, True])
 @pytest.mark.parametrize("variant", [210, 211, 212, 213])
 def test_verify_reconstruct_ws(oracle, k, m, blen, erased, data_only, heal, variant):
-    z.set_variant(variant)
-    try:
+    with variant_ctx(variant):
         run_verify_case(oracle, k, m, blen, erased, data_only, heal, nb=17)
-    finally:
-        z.set_variant(0)
 
 
 WS4_CASES = [(4, 2, 1 << 16, []), (4, 2, 1 << 16, [1]), (4, 2, 1 << 16, [0, 5]), (4, 2, 4 * 48, [2, 3]),
@@ -94,11 +89,8 @@ WS4_CASES = [(4, 2, 1 << 16, []), (4, 2, 1 << 16, [1]), (4, 2, 1 << 16, [0, 5]),
 def test_verify_reconstruct_ws_rs42(oracle, k, m, blen, erased, data_only, heal, variant):
     """RS(4+2)-shaped GET / heal on k_vr_ws: quad-form (default) and pair-form (210)
     hash waves, tile edges and dead stripes."""
-    z.set_variant(variant)
-    try:
+    with variant_ctx(variant):
         run_verify_case(oracle, k, m, blen, erased, data_only, heal, nb=11)
-    finally:
-        z.set_variant(0)
 
 
 WS16_HEAL_CASES = [(16, 4, 1 << 16, [0, 5]), (16, 4, 1 << 16, [3, 17]), (16, 4, 16 * 48, [2, 19]),
@@ -109,16 +101,30 @@ WS16_HEAL_CASES = [(16, 4, 1 << 16, [0, 5]), (16, 4, 1 << 16, [3, 17]), (16, 4, 
 @pytest.mark.parametrize("k,m,blen,erased", WS16_HEAL_CASES)
 @pytest.mark.parametrize("variant", [0, 215])
 def test_heal_ws_rs164(oracle, k, m, blen, erased, variant):
-    """RS(16+4) heal (rebuild 2 or 4 shards and hash them) on k_vr_ws with quad-form
-    hash waves: tile edges, ragged tails and dead stripes of the 8-stripe workgroup."""
-    z.set_variant(variant)
-    try:
-        run_verify_case(oracle, k, m, blen, erased, False, True, nb=11)
-    finally:
-        z.set_variant(0)
+    """RS(16+4) heal (rebuild 2 or 4 shards and hash them): the default (first-
+    generation kernel) and k_vr_ws with quad-form hash waves (diagnostics variant 215,
+    asserted to have run): tile edges, ragged tails and dead stripes of the 8-stripe
+    workgroup."""
+    with variant_ctx(variant):
+        run_verify_case(oracle, k, m, blen, erased, False, True, nb=11, want_path=2 if variant == 215 else None)
 
 
-def run_verify_case(oracle, k, m, blen, erased, data_only, heal, nb=3):
+# RS(16+4) GET on the default k_vr_ws (8-byte rebuild columns, e = 2 and e = 4): tile
+# edges, ragged tails and dead stripes of the 8-stripe workgroup (nb = 11)
+WS16_GET_CASES = [(16, 4, blen, erased, data_only)
+                  for blen in (1 << 16, 16 * 48, 16 * (256 * 3 + 16), 16 * (256 * 2 + 48))
+                  for erased, data_only in (([0, 5], True), ([4, 15], True), ([3, 17], False),
+                                            ([0, 1, 16, 19], False), ([2, 7, 9, 12], True))]
+
+
+@pytest.mark.parametrize("k,m,blen,erased,data_only", WS16_GET_CASES)
+def test_verify_reconstruct_ws_rs164(oracle, k, m, blen, erased, data_only):
+    """The RS(16+4) rebuild-2 / rebuild-4 defaults run the warp-specialised kernel
+    (asserted through zs3_last_path) and are bit-exact vs the oracle."""
+    run_verify_case(oracle, k, m, blen, erased, data_only, False, nb=11, want_path=2)
+
+
+def run_verify_case(oracle, k, m, blen, erased, data_only, heal, nb=3, want_path=None):
     sh, sums = stripes(oracle, k, m, blen, nb)
     S = sh.shape[2]
     R = k + m
@@ -132,6 +138,8 @@ def run_verify_case(oracle, k, m, blen, erased, data_only, heal, nb=3):
     present = [i not in erased for i in range(R)]
     codec.verify_reconstruct_batch(d, R * S, S, nb, present, data_only, exp, bad, sums_out=out)
     torch.cuda.synchronize()
+    if want_path is not None:
+        assert z.last_path() == want_path, f"kernel family {z.last_path()} ran, expected {want_path}"
     got = d.cpu().numpy()
     assert not bad.cpu().numpy().any(), "no survivor is corrupt"
     rebuilt = [i for i in erased if i < k or not data_only]
@@ -210,7 +218,7 @@ def test_fused_kernel_selected():
     bad = torch.zeros(R, dtype=torch.int32, device=DEV)
     codec.verify_reconstruct_batch(d, R * S, S, 1, [i != 2 for i in range(R)], True, exp, bad)
     torch.cuda.synchronize()
-    assert z.last_path() == 1
+    assert z.last_path() >= 1
 
 
 @pytest.mark.parametrize("k,m,blen,erased,heal", [(8, 4, 8 * 640, [], False), (8, 4, 8 * 640, [0, 5], False),
@@ -231,7 +239,6 @@ def test_verify_reconstruct_large_batch(oracle, k, m, blen, erased, heal, varian
     sh = np.concatenate([base] * (nb // 64))  # 64 distinct stripes, repeated
     sums = np.stack([oracle.hh256_rows(KEY, s) for s in base])
     sums = np.concatenate([sums] * (nb // 64))
-    codec = z.Codec(k, m)
     d = torch.from_numpy(sh.copy()).to(DEV)
     for e in erased:
         d[:, e, :] = 0x5A
@@ -242,12 +249,10 @@ def test_verify_reconstruct_large_batch(oracle, k, m, blen, erased, heal, varian
     bad = torch.full((nb, R), 7, dtype=torch.int32, device=DEV)
     out = torch.zeros((nb, R, 32), dtype=torch.uint8, device=DEV) if heal else None
     present = [i not in erased for i in range(R)]
-    z.set_variant(variant)
-    try:
+    with variant_ctx(variant):
+        codec = z.Codec(k, m)
         codec.verify_reconstruct_batch(d, R * S, S, nb, present, not heal, exp, bad, sums_out=out)
         torch.cuda.synchronize()
-    finally:
-        z.set_variant(0)
     b = bad.cpu().numpy()
     want_bad = np.zeros((nb, R), dtype=np.int32)
     want_bad[bad_blk, bad_row] = 1
@@ -262,3 +267,96 @@ def test_verify_reconstruct_large_batch(oracle, k, m, blen, erased, heal, varian
         o = out.cpu().numpy()
         for i in rebuilt:
             assert np.array_equal(o[ok, i], sums[ok, i]), f"heal sums of shard {i}"
+
+
+# ---- per-block erasure patterns (zs3_*_batch_masks) ---------------------------------
+
+MASK_SHAPES = [(8, 4, 1 << 16), (4, 2, 4 * (256 * 3 + 16)), (16, 4, 16 * 256), (5, 3, 1000)]
+
+
+def random_patterns(rng, nb, k, m, allow_fail=False):
+    R = k + m
+    pats = np.ones((nb, R), dtype=bool)
+    for b in range(nb):
+        e = int(rng.integers(0, m + (2 if allow_fail else 1)))
+        pats[b, rng.choice(R, size=min(e, R), replace=False)] = False
+    return pats
+
+
+@pytest.mark.parametrize("k,m,blen", MASK_SHAPES)
+@pytest.mark.parametrize("data_only", [True, False])
+def test_reconstruct_batch_masks(oracle, k, m, blen, data_only):
+    """Every block of one batch decoded with its own erasure pattern (the reference
+    decodes each block with the shards its readers returned, erasure-decode.go:166-179),
+    including patterns with too few shards: those blocks get ErrTooFewShards in their
+    status and are left untouched, the others are rebuilt bit-exact."""
+    nb = 37
+    rng = np.random.default_rng(k * 100 + m)
+    sh, _ = stripes(oracle, k, m, blen, nb, seed=9)
+    S = sh.shape[2]
+    R = k + m
+    pats = random_patterns(rng, nb, k, m, allow_fail=True)
+    d = torch.from_numpy(sh.copy()).to(DEV)
+    dv = d.view(nb, R, S)
+    for b in range(nb):
+        for i in np.nonzero(~pats[b])[0]:
+            dv[b, int(i)] = 0x3C
+    codec = z.Codec(k, m)
+    status = np.full(nb, 99, np.int32)
+    rc = codec.reconstruct_batch_masks(d, R * S, S, nb, pats, data_only, status=status)
+    torch.cuda.synchronize()
+    got = d.cpu().numpy().reshape(nb, R, S)
+    fail = pats.sum(axis=1) < k
+    assert rc == (-3 if fail.any() else 0)
+    assert np.array_equal(status, np.where(fail, -3, 0).astype(np.int32))
+    for b in range(nb):
+        for i in range(R):
+            if pats[b, i]:
+                assert np.array_equal(got[b, i], sh[b, i])
+            elif fail[b] or (data_only and i >= k):
+                assert (got[b, i] == 0x3C).all(), (b, i)
+            else:
+                assert np.array_equal(got[b, i], sh[b, i]), (b, i)
+
+
+@pytest.mark.parametrize("k,m,blen", MASK_SHAPES)
+@pytest.mark.parametrize("heal", [False, True])
+def test_verify_reconstruct_batch_masks(oracle, k, m, blen, heal):
+    """GET / heal pass with per-block patterns: survivors verified per block (one rotted
+    survivor flagged exactly), missing shards rebuilt, heal sums of the rebuilt shards."""
+    nb = 41
+    rng = np.random.default_rng(k * 7 + m)
+    sh, sums = stripes(oracle, k, m, blen, nb, seed=13)
+    S = sh.shape[2]
+    R = k + m
+    pats = random_patterns(rng, nb, k, m)
+    bad_sh = sh.copy()
+    rb = 5
+    surv = [i for i in range(R) if pats[rb, i]][:k]
+    bad_sh[rb, surv[0], S - 1] ^= 0x80
+    d = torch.from_numpy(bad_sh).to(DEV)
+    dv = d.view(nb, R, S)
+    for b in range(nb):
+        for i in np.nonzero(~pats[b])[0]:
+            dv[b, int(i)] = 0x77
+    codec = z.Codec(k, m)
+    exp = torch.from_numpy(sums).to(DEV)
+    bad = torch.full((nb, R), 9, dtype=torch.int32, device=DEV)
+    out = torch.zeros((nb, R, 32), dtype=torch.uint8, device=DEV) if heal else None
+    status = np.full(nb, 99, np.int32)
+    rc = codec.verify_reconstruct_batch_masks(d, R * S, S, nb, pats, not heal, exp, bad, sums_out=out,
+                                              status=status)
+    torch.cuda.synchronize()
+    assert rc == 0 and not status.any()
+    want_bad = np.zeros((nb, R), np.int32)
+    want_bad[rb, surv[0]] = 1
+    assert np.array_equal(bad.cpu().numpy(), want_bad)
+    got = d.cpu().numpy().reshape(nb, R, S)
+    for b in range(nb):
+        if b == rb:
+            continue  # rebuilt from a rotted survivor: garbage by design (re-issued by the caller)
+        for i in range(R):
+            if pats[b, i] or i < k or heal:
+                assert np.array_equal(got[b, i], sh[b, i]), (b, i)
+            if heal and not pats[b, i]:
+                assert np.array_equal(out.cpu().numpy()[b, i], sums[b, i]), (b, i)

@@ -23,12 +23,16 @@ def _hipcc():
 
 
 @pytest.mark.skipif(_hipcc() is None, reason="hipcc not available")
-def test_untracked_loads_never_touched_in_flight(tmp_path):
+@pytest.mark.parametrize("diag", [False, True], ids=["product", "diag"])
+def test_untracked_loads_never_touched_in_flight(tmp_path, diag):
+    """Both builds: the product library's instances and the diagnostics build's
+    experimental ones."""
     import check_async_loads as cal
 
     asm = tmp_path / "fused_v2.s"
-    subprocess.check_call([_hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "--cuda-device-only", "-S",
-                           "-o", str(asm), os.path.join(ROOT, "zs3server_amd", "csrc", "fused_v2.hip"),
+    subprocess.check_call([_hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "--cuda-device-only", "-S"]
+                          + (["-DZS3_DIAG=1"] if diag else []) +
+                          ["-o", str(asm), os.path.join(ROOT, "zs3server_amd", "csrc", "fused_v2.hip"),
                            "-I", os.path.join(ROOT, "include")], stderr=subprocess.DEVNULL)
     text = asm.read_text().split("\n")
     funcs, cur = [], None

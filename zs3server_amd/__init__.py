@@ -8,11 +8,18 @@ streaming bitrot format in `bitrot.py`.
 There is no CPU fallback: if libzs3gpu.so is missing or fails to load, import of
 `lib()` raises.  Device buffers are torch tensors on a ROCm device (or raw
 device pointers as ints).
+
+Two builds of the same ABI: libzs3gpu.so (the product: tuned default kernels and the
+generic fallbacks) and libzs3gpu_diag.so (the same plus experimental kernel variants
+and the zs3_debug_* calls of include/zs3gpu_diag.h).  Everything here runs on the
+product library unless a `diag()` context is active in this thread.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 import os
+import threading
 
 try:  # load torch's HIP runtime first so the library binds to the same one
     import torch  # noqa: F401
@@ -21,6 +28,7 @@ except Exception:  # pragma: no cover - torch is always present in this image
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libzs3gpu.so")
+DIAG_LIB_PATH = os.path.join(_HERE, "libzs3gpu_diag.so")
 
 ZS3_OK = 0
 ERRORS = {
@@ -42,8 +50,13 @@ EXPORTS = [
     "zs3_hh256_verify_batch",
     "zs3_fill_batch", "zs3_encode_data", "zs3_decode_data_blocks", "zs3_hh256", "zs3_selftest",
     "zs3_stream_encode", "zs3_md5_batch", "zs3_sha256_batch", "zs3_etag_multipart",
-    "zs3_last_path", "zs3_debug_set_variant", "zs3_debug_set_buffer",
+    "zs3_last_path", "zs3_reconstruct_batch_masks", "zs3_verify_reconstruct_batch_masks",
+    "zs3_hh256_batch_ragged", "zs3_bitrot_verify_file_batch", "zs3_codec_params",
+    "zs3_queue_new", "zs3_queue_free", "zs3_queue_submit_encode", "zs3_queue_submit_decode", "zs3_req_wait",
+    "zs3_queue_flush", "zs3_queue_stats", "zs3_queue_encode_data", "zs3_queue_decode_data_blocks",
 ]
+# include/zs3gpu_diag.h: exported by the diagnostics build only
+DIAG_EXPORTS = ["zs3_debug_set_variant", "zs3_debug_set_buffer"]
 
 
 class ZS3Error(Exception):
@@ -53,17 +66,54 @@ class ZS3Error(Exception):
         super().__init__(f"{what}: {self.name} ({code})" if what else f"{self.name} ({code})")
 
 
-_L = None
+_L = None        # product library
+_LD = None       # diagnostics library
+_tls = threading.local()
 
 
 def lib():
-    """Load libzs3gpu.so (raises if absent: the product path has no fallback)."""
+    """The library this thread uses: the product libzs3gpu.so, or the diagnostics
+    build inside a `diag()` context.  Raises if absent: there is no fallback."""
+    d = getattr(_tls, "diag", None)
+    return d if d is not None else product_lib()
+
+
+def product_lib():
     global _L
-    if _L is not None:
-        return _L
-    if not os.path.exists(LIB_PATH):
-        raise ImportError(f"{LIB_PATH} not built — run __graft_entry__.build()")
-    L = C.CDLL(LIB_PATH)
+    if _L is None:
+        _L = _load(LIB_PATH)
+    return _L
+
+
+def diag_lib():
+    """libzs3gpu_diag.so: the product ABI plus the experimental kernel variants."""
+    global _LD
+    if _LD is None:
+        _LD = _load(DIAG_LIB_PATH)
+        _LD.zs3_debug_set_variant.argtypes = [C.c_int]
+        _LD.zs3_debug_set_buffer.argtypes = [C.c_void_p]
+    return _LD
+
+
+@contextlib.contextmanager
+def diag(variant: int = 0):
+    """Run this thread's calls on the diagnostics build with fused-kernel `variant`
+    (thread-local in the library too: other threads are unaffected)."""
+    prev = getattr(_tls, "diag", None)
+    L = diag_lib()
+    _tls.diag = L
+    L.zs3_debug_set_variant(variant)
+    try:
+        yield L
+    finally:
+        L.zs3_debug_set_variant(0)
+        _tls.diag = prev
+
+
+def _load(path):
+    if not os.path.exists(path):
+        raise ImportError(f"{path} not built — run __graft_entry__.build()")
+    L = C.CDLL(path)
     vp, i64, u8p = C.c_void_p, C.c_int64, C.POINTER(C.c_uint8)
     L.zs3_strerror.restype = C.c_char_p
     L.zs3_strerror.argtypes = [C.c_int]
@@ -99,8 +149,29 @@ def lib():
     L.zs3_etag_multipart.argtypes = [vp, vp, vp, i64, vp]
     L.zs3_host_alloc.argtypes = [C.POINTER(vp), C.c_size_t]
     L.zs3_host_free.argtypes = [vp]
-    _L = L
+    L.zs3_reconstruct_batch_masks.argtypes = [vp, vp, i64, i64, i64, vp, C.c_int, vp, vp]
+    L.zs3_verify_reconstruct_batch_masks.argtypes = [vp, vp, i64, i64, i64, vp, C.c_int, vp, vp, vp, vp, vp]
+    L.zs3_hh256_batch_ragged.argtypes = [vp, vp, vp, i64, vp, vp]
+    L.zs3_bitrot_verify_file_batch.argtypes = [vp, vp, i64, i64, i64, i64, i64, vp, vp, C.POINTER(C.c_int64), vp]
+    L.zs3_codec_params.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(i64)]
+    L.zs3_queue_new.argtypes = [vp, C.POINTER(QueueOpts), C.POINTER(vp)]
+    L.zs3_queue_free.argtypes = [vp]
+    L.zs3_queue_free.restype = None
+    L.zs3_queue_submit_encode.argtypes = [vp, vp, i64, i64, vp, C.POINTER(vp)]
+    L.zs3_queue_submit_decode.argtypes = [vp, vp, i64, vp, C.c_int, vp, vp, vp, C.POINTER(vp)]
+    L.zs3_req_wait.argtypes = [vp]
+    L.zs3_req_wait.restype = i64
+    L.zs3_queue_flush.argtypes = [vp]
+    L.zs3_queue_stats.argtypes = [vp, C.POINTER(i64), C.POINTER(i64)]
+    L.zs3_queue_encode_data.argtypes = [vp, vp, i64, i64, vp]
+    L.zs3_queue_encode_data.restype = i64
+    L.zs3_queue_decode_data_blocks.argtypes = [vp, vp, i64, vp, C.c_int, vp, vp]
     return L
+
+
+class QueueOpts(C.Structure):
+    """zs3_queue_opts (include/zs3gpu.h)."""
+    _fields_ = [("device", C.c_int), ("max_batch", C.c_int), ("max_wait_us", C.c_int), ("slots", C.c_int)]
 
 
 def _check(rc: int, what: str = "") -> int:
@@ -142,43 +213,45 @@ class Codec:
         L = lib()
         h = C.c_void_p()
         _check(L.zs3_codec_new(k, m, block_size, C.byref(h)), "NewErasure")
+        self._L = L  # a codec belongs to the library that made it
         self._h = h
         self.k, self.m, self.block_size = k, m, block_size
 
     def __del__(self):
         h = getattr(self, "_h", None)
-        if h is not None and h.value and _L is not None:
-            _L.zs3_codec_free(h)
+        L = getattr(self, "_L", None)
+        if h is not None and h.value and L is not None:
+            L.zs3_codec_free(h)
             self._h = None
 
     # ---- size arithmetic (erasure-coding.go:122-150) ----
     def shard_size(self) -> int:
-        return lib().zs3_shard_size(self._h)
+        return self._L.zs3_shard_size(self._h)
 
     def shard_file_size(self, total: int) -> int:
-        return lib().zs3_shard_file_size(self._h, total)
+        return self._L.zs3_shard_file_size(self._h, total)
 
     def shard_file_offset(self, start: int, length: int, total: int) -> int:
-        return lib().zs3_shard_file_offset(self._h, start, length, total)
+        return self._L.zs3_shard_file_offset(self._h, start, length, total)
 
     def matrix(self):
         import numpy as np
         out = np.zeros((self.k + self.m) * self.k, dtype=np.uint8)
-        _check(lib().zs3_codec_matrix(self._h, out.ctypes.data_as(C.POINTER(C.c_uint8))))
+        _check(self._L.zs3_codec_matrix(self._h, out.ctypes.data_as(C.POINTER(C.c_uint8))))
         return out.reshape(self.k + self.m, self.k)
 
     # ---- device-resident batches ----
     def encode_batch(self, data, data_stride: int, block_len: int, n_blocks: int, parity,
                      parity_stride: int, sums=None, parity_offset: int = 0, data_offset: int = 0,
                      stream=None) -> None:
-        _check(lib().zs3_encode_batch(self._h, _ptr(data, data_offset), data_stride, block_len, n_blocks,
+        _check(self._L.zs3_encode_batch(self._h, _ptr(data, data_offset), data_stride, block_len, n_blocks,
                                       _ptr(parity, parity_offset), parity_stride, _ptr(sums),
                                       _stream(stream)), "encode_batch")
 
     def reconstruct_batch(self, shards, block_stride: int, shard_len: int, n_blocks: int, present,
                           data_only: bool, stream=None, offset: int = 0) -> None:
         pres = (C.c_uint8 * (self.k + self.m))(*[1 if p else 0 for p in present])
-        _check(lib().zs3_reconstruct_batch(self._h, _ptr(shards, offset), block_stride, shard_len, n_blocks,
+        _check(self._L.zs3_reconstruct_batch(self._h, _ptr(shards, offset), block_stride, shard_len, n_blocks,
                                            pres, 1 if data_only else 0, _stream(stream)), "reconstruct_batch")
 
     def verify_reconstruct_batch(self, shards, block_stride: int, shard_len: int, n_blocks: int, present,
@@ -189,9 +262,33 @@ class Codec:
         int32 device), rebuild the missing shards in place, optionally hash them
         into `sums_out`."""
         pres = (C.c_uint8 * (self.k + self.m))(*[1 if p else 0 for p in present])
-        _check(lib().zs3_verify_reconstruct_batch(self._h, _ptr(shards, offset), block_stride, shard_len,
+        _check(self._L.zs3_verify_reconstruct_batch(self._h, _ptr(shards, offset), block_stride, shard_len,
                                                   n_blocks, pres, 1 if data_only else 0, _ptr(expect), _ptr(bad),
                                                   _ptr(sums_out), _stream(stream)), "verify_reconstruct_batch")
+
+    def reconstruct_batch_masks(self, shards, block_stride: int, shard_len: int, n_blocks: int, present,
+                                data_only: bool, status=None, stream=None, offset: int = 0) -> int:
+        """Per-block erasure patterns (zs3_reconstruct_batch_masks): `present` is an
+        (n_blocks, k+m) array of flags.  Returns ZS3_OK or the first block's error;
+        `status` (numpy int32, n_blocks) receives every block's status."""
+        import numpy as np
+        pres = np.ascontiguousarray(np.asarray(present, dtype=bool).astype(np.uint8).reshape(n_blocks, self.k + self.m))
+        st = status if status is not None else np.zeros(n_blocks, np.int32)
+        return int(self._L.zs3_reconstruct_batch_masks(self._h, _ptr(shards, offset), block_stride, shard_len,
+                                                        n_blocks, pres.ctypes.data, 1 if data_only else 0,
+                                                        st.ctypes.data, _stream(stream)))
+
+    def verify_reconstruct_batch_masks(self, shards, block_stride: int, shard_len: int, n_blocks: int, present,
+                                       data_only: bool, expect, bad, sums_out=None, status=None, stream=None,
+                                       offset: int = 0) -> int:
+        """GET / heal pass with per-block erasure patterns
+        (zs3_verify_reconstruct_batch_masks); returns ZS3_OK or the first block error."""
+        import numpy as np
+        pres = np.ascontiguousarray(np.asarray(present, dtype=bool).astype(np.uint8).reshape(n_blocks, self.k + self.m))
+        st = status if status is not None else np.zeros(n_blocks, np.int32)
+        return int(self._L.zs3_verify_reconstruct_batch_masks(
+            self._h, _ptr(shards, offset), block_stride, shard_len, n_blocks, pres.ctypes.data,
+            1 if data_only else 0, _ptr(expect), _ptr(bad), _ptr(sums_out), st.ctypes.data, _stream(stream)))
 
     # ---- host-pointer calls ----
     def encode_data(self, buf, length: int, sums: bool = False):
@@ -200,7 +297,7 @@ class Codec:
         import numpy as np
         arr = _u8buf(buf)
         out = np.zeros((self.k + self.m) * 32, dtype=np.uint8) if sums else None
-        S = lib().zs3_encode_data(self._h, arr.ctypes.data, length, arr.nbytes,
+        S = self._L.zs3_encode_data(self._h, arr.ctypes.data, length, arr.nbytes,
                                   out.ctypes.data if sums else None)
         _check(S, "EncodeData")
         return S, (out.reshape(self.k + self.m, 32) if sums else None)
@@ -210,14 +307,84 @@ class Codec:
         src/parity/sums are host buffers (numpy arrays or pinned HostBuffer)."""
         def addr(x):
             return x.ptr if isinstance(x, HostBuffer) else x.ctypes.data
-        n = lib().zs3_stream_encode(self._h, addr(src), total_len, addr(parity), addr(sums), batch_blocks)
+        n = self._L.zs3_stream_encode(self._h, addr(src), total_len, addr(parity), addr(sums), batch_blocks)
         return _check(n, "stream_encode")
 
     def decode_data_blocks(self, shards, present, data_only: bool) -> None:
         """Reconstruct in place on a (k+m, S) C-contiguous numpy uint8 array."""
         pres = (C.c_uint8 * (self.k + self.m))(*[1 if p else 0 for p in present])
-        _check(lib().zs3_decode_data_blocks(self._h, shards.ctypes.data, shards.shape[1], pres,
+        _check(self._L.zs3_decode_data_blocks(self._h, shards.ctypes.data, shards.shape[1], pres,
                                             1 if data_only else 0), "DecodeDataBlocks")
+
+
+class Queue:
+    """Cross-request batching queue (zs3_queue_*): concurrent callers' blocks are
+    gathered into device batches.  Each call below blocks the calling thread only
+    (ctypes releases the GIL), so N Python threads behave like N goroutines in cgo."""
+
+    def __init__(self, codec: Codec, device: int = -1, max_batch: int = 0, max_wait_us: int = 0, slots: int = 0):
+        self._L = codec._L
+        self.codec = codec
+        self.k, self.m = codec.k, codec.m
+        opts = QueueOpts(device, max_batch, max_wait_us, slots)
+        h = C.c_void_p()
+        _check(self._L.zs3_queue_new(codec._h, C.byref(opts), C.byref(h)), "queue_new")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._L.zs3_queue_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def encode_data(self, buf, length: int, sums: bool = True):
+        """EncodeData in place on a host buffer through the queue; returns (S, sums)."""
+        import numpy as np
+        arr = _u8buf(buf)
+        out = np.zeros((self.k + self.m) * 32, dtype=np.uint8) if sums else None
+        S = self._L.zs3_queue_encode_data(self._h, arr.ctypes.data, length, arr.nbytes,
+                                          out.ctypes.data if sums else None)
+        _check(S, "queue EncodeData")
+        return S, (out.reshape(self.k + self.m, 32) if sums else None)
+
+    def submit_encode(self, buf, length: int, sums=None):
+        """Asynchronous form: returns a request handle for wait()."""
+        arr = _u8buf(buf)
+        r = C.c_void_p()
+        _check(self._L.zs3_queue_submit_encode(self._h, arr.ctypes.data, length, arr.nbytes,
+                                               sums.ctypes.data if sums is not None else None, C.byref(r)),
+               "queue submit")
+        return r
+
+    def wait(self, req) -> int:
+        return int(self._L.zs3_req_wait(req))
+
+    def decode(self, shards, present, data_only: bool, expect=None, bad=None, sums_out=None) -> int:
+        """DecodeDataBlocks (data_only) / heal Reconstruct on one (k+m, S) host stripe
+        (numpy uint8, C-contiguous), survivors verified against `expect` ((k+m, 32))
+        when given.  Returns the status: 0, errFileCorrupt (-7, see `bad`), or the
+        reedsolomon error of the pattern."""
+        import numpy as np
+        pres = np.asarray([1 if p else 0 for p in present], dtype=np.uint8)
+        r = C.c_void_p()
+        rc = self._L.zs3_queue_submit_decode(self._h, shards.ctypes.data, shards.shape[1], pres.ctypes.data,
+                                             1 if data_only else 0,
+                                             expect.ctypes.data if expect is not None else None,
+                                             bad.ctypes.data if bad is not None else None,
+                                             sums_out.ctypes.data if sums_out is not None else None, C.byref(r))
+        if rc:
+            return int(rc)
+        return int(self._L.zs3_req_wait(r))
+
+    def flush(self) -> None:
+        _check(self._L.zs3_queue_flush(self._h))
+
+    def stats(self) -> tuple[int, int]:
+        b, n = C.c_int64(0), C.c_int64(0)
+        _check(self._L.zs3_queue_stats(self._h, C.byref(b), C.byref(n)))
+        return b.value, n.value
 
 
 class HostBuffer:
@@ -286,6 +453,29 @@ def etag_multipart(etags) -> bytes:
     return out[:r].tobytes()
 
 
+def hh256_batch_ragged(ptrs, lens, n_msgs: int, sums, key: bytes | None = None, stream=None) -> None:
+    """HighwayHash-256 of messages of different lengths (zs3_hh256_batch_ragged):
+    `ptrs` / `lens` are device int64 tensors of message addresses / lengths."""
+    kb = C.create_string_buffer(key, 32) if key else None
+    _check(lib().zs3_hh256_batch_ragged(kb, _ptr(ptrs), _ptr(lens), n_msgs, _ptr(sums), _stream(stream)),
+           "hh256_batch_ragged")
+
+
+def bitrot_verify_file_batch(files, file_stride: int, n_files: int, want_size: int, part_size: int,
+                             shard_size: int, bad, file_bad=None, key: bytes | None = None, stream=None) -> int:
+    """Deep-scan bitrotVerify of n device-resident shard files in the on-disk
+    [sum][chunk]* layout (zs3_bitrot_verify_file_batch).  Raises errFileCorrupt when
+    want_size is not bitrotShardFileSize(part_size, shard_size); returns chunks per
+    file.  `bad` (device int32, n_files*chunks) flags corrupt chunks, `file_bad`
+    (optional, n_files) corrupt files."""
+    kb = C.create_string_buffer(key, 32) if key else None
+    chunks = C.c_int64(0)
+    _check(lib().zs3_bitrot_verify_file_batch(kb, _ptr(files), file_stride, n_files, want_size, part_size,
+                                               shard_size, _ptr(bad), _ptr(file_bad), C.byref(chunks),
+                                               _stream(stream)), "bitrotVerify")
+    return chunks.value
+
+
 def fill_batch(out, stride: int, length: int, n_blocks: int, seed: int = 0, obj0: int = 0,
                stream=None, offset: int = 0) -> None:
     _check(lib().zs3_fill_batch(_ptr(out, offset), stride, length, n_blocks, seed, obj0, _stream(stream)),
@@ -311,15 +501,9 @@ def last_path() -> int:
     return lib().zs3_last_path()
 
 
-def set_variant(v: int) -> None:
-    """Diagnostics: experimental fused-kernel variant (0 = tuned default)."""
-    lib().zs3_debug_set_variant(v)
-
-
 def set_debug_buffer(t) -> None:
-    L = lib()
-    L.zs3_debug_set_buffer.argtypes = [C.c_void_p]
-    L.zs3_debug_set_buffer(_ptr(t))
+    """Diagnostics build only: per-wave stamp buffer for this thread (None = off)."""
+    diag_lib().zs3_debug_set_buffer(_ptr(t))
 
 
 def device_count() -> int:

@@ -69,20 +69,39 @@ class StreamingBitrotReader:
 
 
 def bitrot_verify(stream: bytes, want_size: int, part_size: int, shard_size: int) -> None:
-    """bitrotVerify for HighwayHash256S (cmd/bitrot.go:158-210): raises errFileCorrupt."""
+    """bitrotVerify for HighwayHash256S (cmd/bitrot.go:158-210): raises errFileCorrupt.
+
+    The whole shard file goes to the device once and every chunk is verified in one
+    launch against the sum stored in front of it (zs3_bitrot_verify_file_batch)."""
+    bitrot_verify_files([stream], want_size, part_size, shard_size, raise_first=True)
+
+
+def bitrot_verify_files(files, want_size: int, part_size: int, shard_size: int, raise_first: bool = False):
+    """Deep scan of several shard files of one part (xlStorage.VerifyFile,
+    cmd/xl-storage.go:2386-2404) in one device launch.  Returns the list of file
+    indices that fail (errFileCorrupt); with raise_first, raises for the first one.
+    A file shorter than want_size fails like the reference's short read."""
+    import numpy as np
+    import torch
+
+    from . import bitrot_verify_file_batch
+
     if want_size != bitrot_shard_file_size(part_size, shard_size):
         raise ZS3Error(ERR_FILE_CORRUPT, "bitrotVerify: size")
-    r = io.BytesIO(stream)
-    left = want_size
-    while left > 0:
-        h = r.read(HASH_SIZE)
-        if len(h) != HASH_SIZE:
-            raise ZS3Error(ERR_FILE_CORRUPT, "bitrotVerify: short hash")
-        left -= HASH_SIZE
-        if left < shard_size:
-            shard_size = left
-        chunk = r.read(shard_size)
-        left -= len(chunk)
-        if hh256(chunk, MAGIC_HH256_KEY) != h:
-            raise ZS3Error(ERR_FILE_CORRUPT, "bitrotVerify: hash mismatch")
-    return None
+    short = [i for i, f in enumerate(files) if len(f) < want_size]
+    n = len(files)
+    stride = max(16, (want_size + 15) // 16 * 16)
+    host = np.zeros(n * stride, dtype=np.uint8)
+    for i, f in enumerate(files):
+        b = np.frombuffer(bytes(f[:want_size]), dtype=np.uint8)
+        host[i * stride: i * stride + len(b)] = b
+    dev = torch.from_numpy(host).to("cuda")
+    chunks = -(-part_size // shard_size) if part_size else 0
+    bad = torch.zeros(max(1, n * chunks), dtype=torch.int32, device="cuda")
+    file_bad = torch.zeros(max(1, n), dtype=torch.int32, device="cuda")
+    bitrot_verify_file_batch(dev, stride, n, want_size, part_size, shard_size, bad, file_bad, key=MAGIC_HH256_KEY)
+    torch.cuda.synchronize()
+    failed = sorted(set(short) | {int(i) for i in np.nonzero(file_bad.cpu().numpy()[:n])[0]})
+    if raise_first and failed:
+        raise ZS3Error(ERR_FILE_CORRUPT, f"bitrotVerify: file {failed[0]} hash mismatch")
+    return failed

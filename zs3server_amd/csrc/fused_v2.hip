@@ -709,13 +709,7 @@ static bool launch_ws_t(const EncArgs& a, hipStream_t s) {
                     (G - 1) * a.parity_stride + M * a.S > 0x7FFFFFFF || a.data_stride < 0 || a.parity_stride < 0))
             return false;
         auto kern = k_ehx_ws<K, M, G, T, PF, BUF, HQ, WT, PM, CWX>;
-        static bool attr = false;
-        if (!attr) {
-            if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn) !=
-                hipSuccess)
-                return false;
-            attr = true;
-        }
+        if (ensure_dyn_lds((const void*)kern, dyn) != hipSuccess) return false;
         const int64_t grid = (a.n_blocks + G - 1) / G;
         hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), dyn, s, a);
         return true;
@@ -741,13 +735,7 @@ static bool launch_ehx_t(const EncArgs& a, hipStream_t s) {
     } else {
         if (a.dyb != M) return false;
         auto kern = k_ehx<K, M, G, CW, PF, NBUF, NTS, ABL, PIPE, PRIO>;
-        static bool attr = false;
-        if (!attr) {
-            if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn) !=
-                hipSuccess)
-                return false;
-            attr = true;
-        }
+        if (ensure_dyn_lds((const void*)kern, dyn) != hipSuccess) return false;
         const int64_t grid = (a.n_blocks + G - 1) / G;
         hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), dyn, s, a);
         return true;
@@ -757,6 +745,40 @@ static bool launch_ehx_t(const EncArgs& a, hipStream_t s) {
 // Only instances that scripts/check_async_loads.py proves clean are compiled (wider
 // columns and deeper prefetch on the other shapes make hipcc copy or re-use
 // registers of in-flight loads).
+//
+// Product defaults (variant 0), by shape and batch size n (scripts/sweep_sizes.py,
+// profiles/r02/sweep_sizes_rs84.txt: the fastest launch at each n, so throughput grows
+// monotonically with the batch):
+//  RS(8+4)  n >= 4096: k_ehx_ws G = 16 (variant 105: 6 pair-form hash waves + 6 encode
+//                      waves with 16-byte columns, encode waves at s_setprio 1; one
+//                      workgroup of 12 waves per CU)
+//           2048 <= n <= 2304: G = 8 (variant 130: 256-288 workgroups, one per CU)
+//           2304 < n < 4096: G = 16 again (a G = 8 grid of 289-511 workgroups doubles
+//                      up on some CUs and runs slower than 145-255 G = 16 workgroups)
+//           n < 2048:  PATH_NONE -> the first-generation kernel (4 stripes per
+//                      workgroup, quad-form hash lanes: more threads per stripe when
+//                      there are too few stripes to fill 256 CUs with 16 each)
+//  RS(16+4) n >= 2048: k_ehx_ws G = 8 (variant 120)
+//  RS(4+2)  n <= 1024: k_ehx_ws G = 4, quad-form hash waves (variant 111; BASELINE config 2)
+//           n <= 2048: k_ehx mixed waves, pipelined body (variant 91)
+template <int K, int M>
+static int launch_ehx_default(const EncArgs& a, hipStream_t s) {
+    const int64_t n = a.n_blocks;
+    if constexpr (K == 8 && M == 4) {
+        if (n >= 2048 && n <= 2304)
+            return launch_ws_t<K, M, 8, 384, 1, false, false, 0, false, 1>(a, s) ? PATH_WS : PATH_NONE;
+        if (n >= 2048) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1>(a, s) ? PATH_WS : PATH_NONE;
+    } else if constexpr (K == 16 && M == 4) {
+        if (n >= 8 * 256) return launch_ws_t<K, M, 8, 384, 1, true>(a, s) ? PATH_WS : PATH_NONE;
+    } else if constexpr (K == 4 && M == 2) {
+        if (n <= 4 * 256) return launch_ws_t<K, M, 4, 512, 4, false, true, 83968>(a, s) ? PATH_WS : PATH_NONE;
+        if (n <= 8 * 256)
+            return launch_ehx_t<K, M, 8, 4, 2, false, 0, true, 1, false, 83968>(a, s) ? PATH_PIPE : PATH_NONE;
+    }
+    return PATH_NONE;
+}
+
+#if ZS3_DIAG
 template <int K, int M>
 static bool launch_ehx_km(int v, const EncArgs& a, hipStream_t s) {
     constexpr bool deep = K == 8 && M == 4;
@@ -792,15 +814,21 @@ static bool launch_ehx_km(int v, const EncArgs& a, hipStream_t s) {
         case 106: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 2>(a, s); else return false;
         case 107: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 3>(a, s); else return false;
         case 104: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, true>(a, s); else return false;
+        case 130: if constexpr (deep) return launch_ws_t<K, M, 8, 384, 1, false, false, 0, false, 1>(a, s); else return false;
+        case 131: if constexpr (deep) return launch_ws_t<K, M, 4, 512, 2, false, true>(a, s); else return false;
+        case 132: if constexpr (deep) return launch_ws_t<K, M, 2, 512, 2, false, true>(a, s); else return false;
         case 120: if constexpr (K == 16 && M == 4) return launch_ws_t<K, M, 8, 384, 1, true>(a, s); else return false;
+        case 121: if constexpr (K == 16 && M == 4) return launch_ws_t<K, M, 4, 512, 1, true, true>(a, s); else return false;
         case 110: if constexpr (few) return launch_ws_t<K, M, 4, 512, 2, false, true, 83968>(a, s); else return false;
         case 111: if constexpr (few) return launch_ws_t<K, M, 4, 512, 4, false, true, 83968>(a, s); else return false;
         case 112: if constexpr (few) return launch_ws_t<K, M, 4, 256, 4, false, true, 83968>(a, s); else return false;
+        case 113: if constexpr (few) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1>(a, s); else return false;
         case 61: if constexpr (deep) return launch_ehx_t<K, M, 8, 1, 2, false, 1>(a, s); else return false;
         case 64: if constexpr (deep) return launch_ehx_t<K, M, 8, 2, 2, false, 1>(a, s); else return false;
         default: return false;
     }
 }
+#endif  // ZS3_DIAG
 
 // ---------------------------------------------------------------------------
 // GET / heal pass, warp-specialised (replaces the arithmetic of
@@ -876,7 +904,7 @@ k_vr_ws(VrArgs a) {
         for (int64_t s = nfull + 1; s < total; ++s) lds_barrier2();
         const uint64_t h = hh_finalize256(st, lane, sel);
         const bool live = chain < G * RH && blk0 + g < a.n_blocks;
-        const int64_t b = blk0 + g;
+        const int64_t b = live && a.ids ? (int64_t)a.ids[blk0 + g] : blk0 + g;
         const int srow = srows[cj];
         if (cj < K) {
             bool mis = false;
@@ -920,7 +948,7 @@ k_vr_ws(VrArgs a) {
         uint64_t d0, d1;
         hh2_finalize256(st, d0, d1);
         const bool live = blk0 + g < a.n_blocks;
-        const int64_t b = blk0 + g;
+        const int64_t b = live && a.ids ? (int64_t)a.ids[blk0 + g] : blk0 + g;
         const int srow = srows[cj];
         if (cj < K) {
             // errFileCorrupt per (stripe, survivor): either half of the digest differs
@@ -947,7 +975,8 @@ k_vr_ws(VrArgs a) {
     typedef typename VecOf<NWd>::type VT;
     const int e = tid - NH;
     const int g = e / CPS, o = (e % CPS) * CW;
-    const int64_t b = (blk0 + g) < a.n_blocks ? (blk0 + g) : (a.n_blocks - 1);
+    const int64_t bl = (blk0 + g) < a.n_blocks ? (blk0 + g) : (a.n_blocks - 1);
+    const int64_t b = a.ids ? (int64_t)a.ids[bl] : bl;
     uint8_t* blk = a.shards + b * a.block_stride + o;
     const int col_off = g * RH * TS + o;
     lds_barrier2();  // tables / rows visible
@@ -1050,22 +1079,18 @@ static bool launch_vr_ws_t(const VrArgs& a, hipStream_t s) {
     } else {
         if (a.e != EX || (a.S % 16) != 0 || a.k != K || (HOUT != (a.sums_out != nullptr) && EX > 0)) return false;
         auto kern = k_vr_ws<K, EX, HOUT, G, T, PF, CW, HQ>;
-        static bool attr = false;
-        if (!attr) {
-            if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn) !=
-                hipSuccess)
-                return false;
-            attr = true;
-        }
+        if (ensure_dyn_lds((const void*)kern, dyn) != hipSuccess) return false;
         const int64_t grid = (a.n_blocks + G - 1) / G;
         hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), dyn, s, a);
         return true;
     }
 }
 
+// GET / heal defaults (variant 0) and diagnostics variants 210-215.
 // RS(8+4)-shaped GET: 16 stripes, 256-byte tiles, verify-only or rebuild 2; heal with
 // 8-byte columns (16-byte columns spill at the heal's 168-VGPR budget: 4.7 ms).
 bool launch_vr_ws(int v, const VrArgs& a, hipStream_t s) {
+    if (!ZS3_DIAG && v != 0) return false;
     if (a.k == 4 && (v == 0 || v == 214)) {
         // RS(4+2)-shaped GET / heal default: quad-form hash waves, 8 stripes, one wave
         // of each kind per SIMD (the 8 192 chains of a 2048-object batch are
@@ -1077,6 +1102,7 @@ bool launch_vr_ws(int v, const VrArgs& a, hipStream_t s) {
         if (a.e == 2) return launch_vr_ws_t<4, 2, false, 8, 256, 4, 16, true>(a, s);
         return false;
     }
+#if ZS3_DIAG
     if (a.k == 4 && v == 210) {
         // RS(4+2)-shaped GET / heal, pair-form hash waves: 16 stripes, 256-byte tiles
         if (a.sums_out != nullptr)
@@ -1086,20 +1112,25 @@ bool launch_vr_ws(int v, const VrArgs& a, hipStream_t s) {
         if (a.e == 2) return launch_vr_ws_t<4, 2, false, 16, 256, 2>(a, s);
         return false;
     }
-    if (a.k == 16 && (v == 0 || v == 210)) {
+#endif
+    if (a.k == 16 && (v == 0 || v == 210 || v == 215)) {
         // RS(16+4)-shaped GET: 8 stripes, 256-byte tiles; rebuilds with 8-byte columns
         // (16-byte columns spill: 16 survivors x 2 tiles beside 32-64 generic products).
-        // Heal (18 / 20 hashed rows): 2*8*18 pair-form threads are not whole waves, so
-        // the hash role runs in quad form (padded to 9 / 10 waves) beside 4 rebuild waves.
-        // Measured slower than the first-generation kernel on 2048 x 1 MiB (heal 2: 1.29
-        // vs 0.95 ms, heal 4: 2.86 vs 1.31 ms; 13 waves leave 128 VGPRs), so opt-in only
         if (a.sums_out != nullptr) {
+#if ZS3_DIAG
+            // Heal (18 / 20 hashed rows): 2*8*18 pair-form threads are not whole waves,
+            // so the hash role runs in quad form (padded to 9 / 10 waves) beside 4
+            // rebuild waves.  Measured slower than the first-generation kernel on
+            // 2048 x 1 MiB (heal 2: 1.29 vs 0.95 ms, heal 4: 2.86 vs 1.31 ms; 13 waves
+            // leave 128 VGPRs), so opt-in only (variant 215).
             if (v == 215) {
                 if (a.e == 2) return launch_vr_ws_t<16, 2, true, 8, 256, 1, 8, true>(a, s);
                 if (a.e == 4) return launch_vr_ws_t<16, 4, true, 8, 256, 1, 8, true>(a, s);
             }
+#endif
             return false;
         }
+        if (v == 215) return false;
         if (a.e == 0) return launch_vr_ws_t<16, 0, false, 8, 256, 2>(a, s);
         if (a.e == 2) return launch_vr_ws_t<16, 2, false, 8, 256, 1, 8>(a, s);
         if (a.e == 4) return launch_vr_ws_t<16, 4, false, 8, 256, 1, 8>(a, s);
@@ -1111,7 +1142,9 @@ bool launch_vr_ws(int v, const VrArgs& a, hipStream_t s) {
         // 9-wave workgroup inside 168 VGPRs (1.50 -> 1.25 ms, 1 data + 1 parity)
         if (a.e != 2) return false;
         if (v == 0 || v == 212) return launch_vr_ws_t<8, 2, true, 16, 128, 2, 8>(a, s);
+#if ZS3_DIAG
         if (v == 213) return launch_vr_ws_t<8, 2, true, 16, 256, 1, 8>(a, s);
+#endif
         return false;
     }
     switch (v) {
@@ -1120,20 +1153,32 @@ bool launch_vr_ws(int v, const VrArgs& a, hipStream_t s) {
             if (a.e == 0) return launch_vr_ws_t<8, 0, false, 16, 256, 2>(a, s);
             if (a.e == 2) return launch_vr_ws_t<8, 2, false, 16, 256, 2>(a, s);
             return false;
+#if ZS3_DIAG
         case 211:
             if (a.e == 0) return launch_vr_ws_t<8, 0, false, 16, 256, 1>(a, s);
             if (a.e == 2) return launch_vr_ws_t<8, 2, false, 16, 256, 1>(a, s);
             return false;
+#endif
         default:
             return false;
     }
 }
 
-bool launch_ehx(int v, const EncArgs& a, hipStream_t s) {
-    if (a.k == 8 && a.m == 4) return launch_ehx_km<8, 4>(v, a, s);
-    if (a.k == 4 && a.m == 2) return launch_ehx_km<4, 2>(v, a, s);
-    if (a.k == 16 && a.m == 4) return launch_ehx_km<16, 4>(v, a, s);
-    return false;
+int launch_ehx(int v, const EncArgs& a, hipStream_t s) {
+    if (v == 0) {
+        if (a.k == 8 && a.m == 4) return launch_ehx_default<8, 4>(a, s);
+        if (a.k == 4 && a.m == 2) return launch_ehx_default<4, 2>(a, s);
+        if (a.k == 16 && a.m == 4) return launch_ehx_default<16, 4>(a, s);
+        return PATH_NONE;
+    }
+#if ZS3_DIAG
+    bool ok = false;
+    if (a.k == 8 && a.m == 4) ok = launch_ehx_km<8, 4>(v, a, s);
+    if (a.k == 4 && a.m == 2) ok = launch_ehx_km<4, 2>(v, a, s);
+    if (a.k == 16 && a.m == 4) ok = launch_ehx_km<16, 4>(v, a, s);
+    if (ok) return (v >= 100 && v < 200) ? PATH_WS : PATH_PIPE;
+#endif
+    return PATH_NONE;
 }
 
 }  // namespace zs3k

@@ -23,15 +23,28 @@
 
 #include <stdlib.h>
 
+#include <mutex>
+#include <set>
+#include <tuple>
 #include <type_traits>
 
 using namespace zs3dev;
 
 namespace zs3k {
 
-static int g_variant = 0;
-void set_variant(int v) { g_variant = v; }
-int get_variant() { return g_variant; }
+hipError_t ensure_dyn_lds(const void* kern, size_t bytes) {
+    static std::mutex mu;
+    static std::set<std::tuple<const void*, int, size_t>> done;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    const auto key = std::make_tuple(kern, dev, bytes);
+    std::lock_guard<std::mutex> g(mu);
+    if (done.count(key)) return hipSuccess;
+    e = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (e == hipSuccess) done.insert(key);
+    return e;
+}
 
 // Barrier that only drains LDS traffic: __syncthreads() would also wait for the
 // tile prefetch (vmcnt(0)) and serialise HBM latency with the hash phase.
@@ -318,8 +331,9 @@ __global__ void __launch_bounds__(NT) k_encode_hash(EncArgs a) {
     }
 }
 
+#if ZS3_DIAG
 // ---------------------------------------------------------------------------
-// Software-pipelined fused kernel: in step i every wave hashes tile i (LDS buffer
+// (diagnostics build) Software-pipelined fused kernel: in step i every wave hashes tile i (LDS buffer
 // i%2) AND encodes tile i+1 (into buffer (i+1)%2) in ONE basic block, so the
 // serial HighwayHash chain (~200 cycles of dependent latency per packet) is
 // filled with the independent GF(2^8) encode work instead of being serialised
@@ -495,6 +509,7 @@ __global__ void __launch_bounds__(NT) k_encode_hash_pipe(EncArgs a) {
         }
     }
 }
+#endif  // ZS3_DIAG
 
 // ---------------------------------------------------------------------------
 // Encode only (no hash): one thread per 16-byte column, K loads -> M stores.
@@ -558,7 +573,7 @@ __global__ void __launch_bounds__(256) k_reconstruct(RecArgs a) {
     const int64_t cols = (S + 15) >> 4;
     const int E = a.e;
     for (int64_t b = blockIdx.y; b < a.n_blocks; b += gridDim.y) {
-        uint8_t* blk = a.shards + b * a.block_stride;
+        uint8_t* blk = a.shards + (a.ids ? (int64_t)a.ids[b] : b) * a.block_stride;
         for (int64_t c0 = (int64_t)blockIdx.x * 256 * NC + threadIdx.x; c0 < cols; c0 += (int64_t)gridDim.x * 256 * NC) {
             const uint32_t* tbl = tabs + opaque_zero();
             uint4 x[NC][K];
@@ -696,7 +711,7 @@ __global__ void __launch_bounds__(256) k_reconstruct_generic(RecArgs a) {
     __syncthreads();
     const int64_t S = a.S;
     for (int64_t b = blockIdx.y; b < a.n_blocks; b += gridDim.y) {
-        uint8_t* blk = a.shards + b * a.block_stride;
+        uint8_t* blk = a.shards + (a.ids ? (int64_t)a.ids[b] : b) * a.block_stride;
         for (int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; o < S; o += (int64_t)gridDim.x * blockDim.x) {
             for (int r = 0; r < E; ++r) {
                 uint8_t acc = 0;
@@ -711,34 +726,80 @@ __global__ void __launch_bounds__(256) k_reconstruct_generic(RecArgs a) {
 // ---------------------------------------------------------------------------
 // HighwayHash-256 of n messages (64 chains = 256 threads per workgroup), with
 // optional compare against expected digests (streamingBitrotReader.ReadAt,
-// cmd/bitrot-streaming.go:180-186: per-shard errFileCorrupt, not whole-batch).
+// cmd/bitrot-streaming.go:180-186, and bitrotVerify, cmd/bitrot.go:158-210: a
+// per-chunk errFileCorrupt flag, never a whole-batch failure).
 // Double-buffered: the next tile's 16-byte pieces are loaded into registers while
 // the current tile is hashed from LDS, so HBM latency overlaps the hash chain.
+// Messages may differ in length (ragged mode, chunked-file mode): every chain runs
+// its own packets/remainder inside the shared tile loop, which runs to the longest
+// message of the workgroup; bytes past a message's end load as zero.
 constexpr int HB_CH = 64;
 constexpr int HB_T = 256;
 constexpr int HB_TS = HB_T + 32;
 constexpr int HB_PPT = HB_CH * (HB_T / 16) / 256;  // 16-byte pieces per thread per tile
 
+struct MsgGeom {
+    const uint8_t* p;    // message bytes
+    const uint8_t* exp;  // expected digest (or nullptr)
+    int64_t len;
+    int64_t slot;        // index into sums / bad
+};
+
+__device__ __forceinline__ MsgGeom msg_geom(const HashArgs& a, int64_t i) {
+    MsgGeom g;
+    g.slot = a.ids ? (int64_t)a.ids[i] : i;
+    const int64_t ss = a.sum_stride ? a.sum_stride : 32;
+    if (a.chunk > 0) {
+        // on-disk [sum][chunk]* shard file (bitrot-streaming.go:50-55)
+        const int64_t f = g.slot / a.nchunks, c = g.slot - f * a.nchunks;
+        const uint8_t* base = a.msgs + f * a.stride + c * (a.chunk + 32);
+        g.exp = base;
+        g.p = base + 32;
+        g.len = c == a.nchunks - 1 ? a.last_len : a.chunk;
+    } else {
+        g.p = a.ptrs ? a.ptrs[i] : a.msgs + g.slot * a.stride;
+        g.len = a.lens ? a.lens[i] : a.len;
+        g.exp = a.expect ? a.expect + g.slot * ss : nullptr;
+    }
+    return g;
+}
+
 __global__ void __launch_bounds__(256) k_hash_batch(HashArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t tile[2][HB_CH * HB_TS];
+    __shared__ int64_t s_len[HB_CH];
     const int tid = threadIdx.x;
     const int64_t m0 = (int64_t)blockIdx.x * HB_CH;
     const int chain = tid >> 2, lane = tid & 3;
     const uint32_t sel = zipper_sel(lane);
     HHLane st = hh_init(lane, a.key[0], a.key[1], a.key[2], a.key[3]);
-    const int64_t len = a.len;
-    const int64_t ntile = (len + HB_T - 1) / HB_T;
+    // geometry of this thread's hash chain and of the HB_PPT rows it loads
+    const bool live = m0 + chain < a.n;
+    const MsgGeom mine = live ? msg_geom(a, m0 + chain) : MsgGeom{nullptr, nullptr, 0, 0};
+    if (lane == 0) s_len[chain] = mine.len;
+    const uint8_t* rp[HB_PPT];
+    int64_t rl[HB_PPT];
+#pragma unroll
+    for (int q = 0; q < HB_PPT; ++q) {
+        const int r = (tid + q * 256) / (HB_T / 16);
+        const bool ok = m0 + r < a.n;
+        const MsgGeom g = ok ? msg_geom(a, m0 + r) : MsgGeom{nullptr, nullptr, 0, 0};
+        rp[q] = g.p;
+        rl[q] = g.len;
+    }
+    __syncthreads();
+    int64_t maxlen = 0;
+    for (int i = 0; i < HB_CH; ++i) maxlen = s_len[i] > maxlen ? s_len[i] : maxlen;
+    const int64_t ntile = (maxlen + HB_T - 1) / HB_T;
     uint4 v[HB_PPT];
     auto load = [&](int64_t t0) {
-        const int L = (int)((len - t0) < HB_T ? (len - t0) : HB_T);
 #pragma unroll
         for (int q = 0; q < HB_PPT; ++q) {
             const int i = tid + q * 256;
-            const int r = i / (HB_T / 16), o = (i % (HB_T / 16)) * 16;
-            const int64_t msg = m0 + r;
+            const int o = (i % (HB_T / 16)) * 16;
+            const int64_t L = rl[q] - t0;
             v[q] = make_uint4(0, 0, 0, 0);
-            if (msg < a.n && o < L) {
-                const uint8_t* src = a.msgs + msg * a.stride + t0 + o;
+            if (o < L) {
+                const uint8_t* src = rp[q] + t0 + o;
                 if (o + 16 <= L) {
                     v[q] = ld16(src);
                 } else {
@@ -767,32 +828,34 @@ __global__ void __launch_bounds__(256) k_hash_batch(HashArgs a) {
     lds_barrier();
     for (int64_t t = 0; t < ntile; ++t) {
         const int64_t t0 = t * HB_T;
-        const int L = (int)((len - t0) < HB_T ? (len - t0) : HB_T);
         uint8_t* cur = tile[t & 1];
         // stash tile t+1 (registers) into the other buffer, then prefetch t+2
         if (t + 1 < ntile) {
             stash(tile[(t + 1) & 1]);
             if (t + 2 < ntile) load(t0 + 2 * HB_T);
         }
+        const int64_t left = mine.len - t0;  // this chain's bytes from this tile on
         const uint8_t* row = cur + chain * HB_TS;
-        if (L == HB_T)
+        if (left >= HB_T) {
             hh_packets_n<HB_T / 32>(st, row, lane, sel);
-        else
+        } else if (left > 0) {
+            const int L = (int)left;
             hh_packets(st, row, L >> 5, lane, sel);
-        if (t + 1 >= ntile && (L & 31)) hh_remainder(st, row + (L & ~31), (uint32_t)(L & 31), lane, sel);
+            if (L & 31) hh_remainder(st, row + (L & ~31), (uint32_t)(L & 31), lane, sel);
+        }
         lds_barrier();
     }
     const uint64_t h = hh_finalize256(st, lane, sel);
-    const int64_t msg = m0 + chain;
-    if (msg < a.n) {
+    if (live) {
         const int64_t ss = a.sum_stride ? a.sum_stride : 32, bs = a.bad_stride ? a.bad_stride : 1;
-        if (a.sums) *reinterpret_cast<uint64_t*>(a.sums + msg * ss + 8 * lane) = h;
-        if (a.expect && a.bad) {
+        const int64_t out_i = a.chunk > 0 ? m0 + chain : mine.slot;
+        if (a.sums) *reinterpret_cast<uint64_t*>(a.sums + out_i * ss + 8 * lane) = h;
+        if (mine.exp && a.bad) {
             uint64_t want;
-            __builtin_memcpy(&want, a.expect + msg * ss + 8 * lane, 8);
+            __builtin_memcpy(&want, mine.exp + 8 * lane, 8);
             const unsigned long long mism = __ballot(want != h);
             const unsigned q = (unsigned)((mism >> (tid & 60)) & 0xFull);
-            if (lane == 0) a.bad[msg * bs] = q ? 1 : 0;
+            if (lane == 0) a.bad[out_i * bs] = q ? 1 : 0;
         }
     }
 }
@@ -858,7 +921,7 @@ __global__ void __launch_bounds__((VrShape<K, EMAX, HOUT, GX>::NT)) k_verify_rec
             const int o = (col % CPB) * CW;
             if (o >= L) continue;
             const int64_t b = (blk0 + g) < a.n_blocks ? (blk0 + g) : (a.n_blocks - 1);
-            uint8_t* blk = a.shards + b * a.block_stride + t0 + o;
+            uint8_t* blk = a.shards + (a.ids ? (int64_t)a.ids[b] : b) * a.block_stride + t0 + o;
             Col<NWd> x[K];
 #pragma unroll
             for (int j = 0; j < K; ++j) x[j] = ldcol<NWd>(blk + roff[j]);
@@ -899,7 +962,7 @@ __global__ void __launch_bounds__((VrShape<K, EMAX, HOUT, GX>::NT)) k_verify_rec
     }
     const uint64_t h = hh_finalize256(st, lane, sel);
     if (chain_live) {
-        const int64_t b = blk0 + chain / RH;
+        const int64_t b = a.ids ? (int64_t)a.ids[blk0 + chain / RH] : blk0 + chain / RH;
         const int64_t srow = srows[cj];
         if (cj < K) {
             uint64_t want;
@@ -958,6 +1021,8 @@ static void launch_fused(const EncArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((k_encode_hash<K, M, G, T, NBUF, NT, CW, PF, NTL, STAMP>), dim3((unsigned)grid), dim3(NT), 0, s, a);
 }
 
+#if ZS3_DIAG
+// ---- diagnostics build: experimental launch shapes of the first-generation kernels
 template <int K, int M, int G, int T, int CW, bool STAMP = false>
 static void launch_pipe(const EncArgs& a, hipStream_t s) {
     constexpr int R = K + M;
@@ -1019,115 +1084,74 @@ static void launch_ablation(const EncArgs& a, hipStream_t s) {
                        dim3(NT), 0, s, a);
 }
 
-static int env_variant() {
-    static int v = -2;
-    if (v == -2) {
-        const char* e = getenv("ZS3_VARIANT");
-        v = e ? atoi(e) : -1;
-    }
-    return g_variant > 0 ? g_variant : v;
-}
-
-// Experimental variants for the headline shapes (ZS3_VARIANT=n); -1/0 = default.
+// Experimental variants for the headline shapes; returns the path or PATH_NONE.
 template <int K, int M>
-static bool launch_variant(int v, const EncArgs& a, hipStream_t s) {
+static int launch_variant(int v, const EncArgs& a, hipStream_t s) {
     constexpr int R = K + M;
     constexpr int G = pick_G<R>();
     switch (v) {
-        case 1: launch_fused<K, M, G, 256, 2, 16>(a, s); return true;
-        case 2: launch_fused<K, M, G, 768, 1, 16>(a, s); return true;
-        case 3: launch_fused<K, M, G, 384, 2, 8>(a, s); return true;
-        case 4: launch_fused<K, M, G, 192, 2, 4>(a, s); return true;
-        case 5: launch_fused<K, M, G, 384, 1, 8>(a, s); return true;
-        case 6: launch_fused<K, M, G, 768, 2, 16>(a, s); return true;
-        case 7: launch_fused<K, M, G, 512, 2, 16>(a, s); return true;
-        case 8: launch_fused<K, M, G, 192, 1, 4>(a, s); return true;
-        case 9: launch_fused<K, M, G, 384, 1, 8, 2>(a, s); return true;
-        case 10: launch_fused<K, M, G, 384, 1, 8, 2, true>(a, s); return true;
-        case 11: launch_fused<K, M, G, 256, 2, 16, 2>(a, s); return true;
-        case 12: launch_fused<K, M, G, 192, 2, 4, 2>(a, s); return true;
-        case 13: launch_fused<K, M, G, 768, 1, 16, 2>(a, s); return true;
-        case 14: launch_fused<K, M, G, 384, 1, 8, 1, true>(a, s); return true;
-        case 15: launch_fused<K, M, G, 384, 1, 8, 3>(a, s); return true;
-        case 16: launch_fused<K, M, G, 192, 1, 4, 3>(a, s); return true;
-        case 20: launch_pipe<K, M, G, 384, 8>(a, s); return true;
-        case 21: launch_pipe<K, M, G, 192, 4>(a, s); return true;
-        case 22: launch_pipe<K, M, G, 256, 8>(a, s); return true;
-        case 23: launch_pipe<K, M, G, 320, 8>(a, s); return true;
-        case 24: launch_pipe<K, M, G, 384, 8, true>(a, s); return true;
-        case 30: launch_pair<K, M, 384, 1, 16>(a, s); return true;
-        case 31: launch_pair<K, M, 384, 2, 16>(a, s); return true;
-        case 32: launch_pair<K, M, 192, 2, 8>(a, s); return true;
-        case 33: launch_pair<K, M, 256, 1, 16>(a, s); return true;
-        case 34: launch_pair<K, M, 192, 1, 8>(a, s); return true;
-        case 41: launch_ablation<K, M, 1>(a, s); return true;
-        case 42: launch_ablation<K, M, 2>(a, s); return true;
-        case 43: launch_ablation<K, M, 3>(a, s); return true;
-        case 44: launch_ablation<K, M, 4>(a, s); return true;
-        case 45: launch_ablation<K, M, 1, 768, 16>(a, s); return true;
-        case 46: launch_ablation<K, M, 1, 384, 8, 1, 2>(a, s); return true;
-        case 47: launch_ablation<K, M, 3, 768, 16>(a, s); return true;
-        case 48: launch_ablation<K, M, 4, 768, 16>(a, s); return true;
-        case 17: launch_fused<K, M, G, 384, 1, 8, 1, false, true>(a, s); return true;
-        case 18: launch_fused<K, M, G, 256, 2, 16, 1, false, true>(a, s); return true;
+        case 1: launch_fused<K, M, G, 256, 2, 16>(a, s); return PATH_FIRSTGEN;
+        case 2: launch_fused<K, M, G, 768, 1, 16>(a, s); return PATH_FIRSTGEN;
+        case 3: launch_fused<K, M, G, 384, 2, 8>(a, s); return PATH_FIRSTGEN;
+        case 4: launch_fused<K, M, G, 192, 2, 4>(a, s); return PATH_FIRSTGEN;
+        case 5: launch_fused<K, M, G, 384, 1, 8>(a, s); return PATH_FIRSTGEN;
+        case 6: launch_fused<K, M, G, 768, 2, 16>(a, s); return PATH_FIRSTGEN;
+        case 7: launch_fused<K, M, G, 512, 2, 16>(a, s); return PATH_FIRSTGEN;
+        case 8: launch_fused<K, M, G, 192, 1, 4>(a, s); return PATH_FIRSTGEN;
+        case 9: launch_fused<K, M, G, 384, 1, 8, 2>(a, s); return PATH_FIRSTGEN;
+        case 10: launch_fused<K, M, G, 384, 1, 8, 2, true>(a, s); return PATH_FIRSTGEN;
+        case 11: launch_fused<K, M, G, 256, 2, 16, 2>(a, s); return PATH_FIRSTGEN;
+        case 12: launch_fused<K, M, G, 192, 2, 4, 2>(a, s); return PATH_FIRSTGEN;
+        case 13: launch_fused<K, M, G, 768, 1, 16, 2>(a, s); return PATH_FIRSTGEN;
+        case 14: launch_fused<K, M, G, 384, 1, 8, 1, true>(a, s); return PATH_FIRSTGEN;
+        case 15: launch_fused<K, M, G, 384, 1, 8, 3>(a, s); return PATH_FIRSTGEN;
+        case 16: launch_fused<K, M, G, 192, 1, 4, 3>(a, s); return PATH_FIRSTGEN;
+        case 17: launch_fused<K, M, G, 384, 1, 8, 1, false, true>(a, s); return PATH_FIRSTGEN;
+        case 18: launch_fused<K, M, G, 256, 2, 16, 1, false, true>(a, s); return PATH_FIRSTGEN;
+        case 20: launch_pipe<K, M, G, 384, 8>(a, s); return PATH_FIRSTGEN;
+        case 21: launch_pipe<K, M, G, 192, 4>(a, s); return PATH_FIRSTGEN;
+        case 22: launch_pipe<K, M, G, 256, 8>(a, s); return PATH_FIRSTGEN;
+        case 23: launch_pipe<K, M, G, 320, 8>(a, s); return PATH_FIRSTGEN;
+        case 24: launch_pipe<K, M, G, 384, 8, true>(a, s); return PATH_FIRSTGEN;
+        case 30: launch_pair<K, M, 384, 1, 16>(a, s); return PATH_FIRSTGEN;
+        case 31: launch_pair<K, M, 384, 2, 16>(a, s); return PATH_FIRSTGEN;
+        case 32: launch_pair<K, M, 192, 2, 8>(a, s); return PATH_FIRSTGEN;
+        case 33: launch_pair<K, M, 256, 1, 16>(a, s); return PATH_FIRSTGEN;
+        case 34: launch_pair<K, M, 192, 1, 8>(a, s); return PATH_FIRSTGEN;
+        case 41: launch_ablation<K, M, 1>(a, s); return PATH_FIRSTGEN;
+        case 42: launch_ablation<K, M, 2>(a, s); return PATH_FIRSTGEN;
+        case 43: launch_ablation<K, M, 3>(a, s); return PATH_FIRSTGEN;
+        case 44: launch_ablation<K, M, 4>(a, s); return PATH_FIRSTGEN;
+        case 45: launch_ablation<K, M, 1, 768, 16>(a, s); return PATH_FIRSTGEN;
+        case 46: launch_ablation<K, M, 1, 384, 8, 1, 2>(a, s); return PATH_FIRSTGEN;
+        case 47: launch_ablation<K, M, 3, 768, 16>(a, s); return PATH_FIRSTGEN;
+        case 48: launch_ablation<K, M, 4, 768, 16>(a, s); return PATH_FIRSTGEN;
         default: return launch_ehx(v, a, s);
     }
 }
+#endif  // ZS3_DIAG
 
 template <int K, int M>
-static hipError_t run_encode_fast(const EncArgs& a, hipStream_t s) {
+static hipError_t run_encode_fast(const EncArgs& a, hipStream_t s, int* path) {
+    int p = PATH_NONE;
     if (a.sums) {
         constexpr int R = K + M;
         constexpr int G = pick_G<R>();
         constexpr int NBUF = 2;
         constexpr int T = pick_T<G * R, NBUF>();
-        bool done = false;
+#if ZS3_DIAG
         if constexpr ((K == 8 && M == 4) || (K == 4 && M == 2) || (K == 16 && M == 4)) {
-            const int v = env_variant();
-            if (v > 0) done = launch_variant<K, M>(v, a, s);
+            if (a.variant > 0) p = launch_variant<K, M>(a.variant, a, s);
         }
-        if constexpr (K == 8 && M == 4) {
-            // Default RS(8+4): fused_v2 with 16 stripes per workgroup, i.e. one
-            // workgroup of 12 waves per CU in one barrier domain (variant 80).  With
-            // 4 independent workgroups per CU, oldest-first issue let the first finish
-            // in ~0.7 ms and the last in ~1.6 ms (per-wave stamps, scripts/stamps3.py),
-            // leaving CUs under-occupied for half the launch; one workgroup per CU
-            // keeps all of a CU's waves in lockstep (1.42 -> 1.31 ms).
-            // Variant 100 (warp-specialised k_ehx_ws: 6 hash waves in the pair form + 6
-            // encode waves with 16-byte columns) takes ~11 % off the compute-bound time
-            // (L2-resident alias runs 1.08 -> 0.96 ms) and 3 % off the HBM launch.
-            // Variant 105 = 100 with the encode waves at issue priority 1 over the hash
-            // waves (which idle 48-68 % of a step): the SIMDs holding two encode waves no
-            // longer end each step with one encode wave issuing alone; 0-4 % per box
-            // (scripts/box_sweep.sh), never slower than 100 beyond noise.
-            if (!done && a.dyb == M && a.n_blocks >= 16 * 256) done = launch_ehx(105, a, s);
-            if (!done && a.dyb == M && a.n_blocks >= 16 * 256) done = launch_ehx(100, a, s);
-            if (!done && a.dyb == M && a.n_blocks >= 16 * 256) done = launch_ehx(80, a, s);
-        }
-        if constexpr (K == 16 && M == 4) {
-            // RS(16+4), one 8-stripe workgroup per CU or more: k_ehx_ws variant 120 (5
-            // pair-form hash waves + 6 encode waves with 8-byte columns, buffer-addressed
-            // loads/stores): 0.81 -> 0.62 ms on 2048 x 1 MiB.
-            if (!done && a.dyb == M && a.n_blocks >= 8 * 256) done = launch_ehx(120, a, s);
-        }
-        if constexpr (K == 4 && M == 2) {
-            // Default RS(4+2) for batches of at most one 8-stripe workgroup per CU
-            // (BASELINE config 2, 1024 objects: 6144 hash chains, one wave per SIMD on
-            // 128 CUs, latency-bound): fused_v2 variant 91 = pipelined body (encode of
-            // tile i beside the hash of tile i-1), 4 tiles of loads in flight, one
-            // workgroup per CU.  1.03 -> 0.84 ms (scripts/box_sweep.sh).
-            // Up to one 4-stripe workgroup per CU: warp-specialised k_ehx_ws variant 111
-            // (quad-form hash waves alone on their SIMDs, encode on the other two, 4
-            // tiles of loads in flight): the hash chains' latency, not issue, sets the
-            // pace; 0.83 -> 0.41 ms on config 2.
-            if (!done && a.dyb == M && a.n_blocks <= 4 * 256) done = launch_ehx(111, a, s);
-            if (!done && a.dyb == M && a.n_blocks <= 8 * 256) done = launch_ehx(91, a, s);
-        }
-        if (!done) {
-            // Tuned defaults (scripts/sweep_variants.py on MI355X, profiles/r01):
-            // 8-byte columns so every thread encodes, one 384-byte tile per step.
-            // k <= 8: one LDS tile.  k > 8 (RS(16+4)): two LDS tiles, so the
-            // next tile's encode does not wait for the slower stripes' hashing.
+#endif
+        // Dyadic shapes (RS(4+2), RS(8+4), RS(16+4), ...): the second-generation
+        // kernels of fused_v2.hip pick their launch shape from (k, m, n_blocks).
+        if (p == PATH_NONE && a.variant == 0) p = launch_ehx(0, a, s);
+        if (p == PATH_NONE) {
+            // First-generation kernel (profiles/r01 tuning): 8-byte columns so every
+            // thread encodes, one 384-byte tile per step.  k <= 8: one LDS tile.
+            // k > 8: two LDS tiles, so the next tile's encode does not wait for the
+            // slower stripes' hashing.
             constexpr bool DY2 = K > 8 && (M == 2 || M == 4) && K % M == 0 &&
                                  2 * G * R * (384 + 32) + K * 32 <= 81920;
             if (DY2 && a.dyb == M) {
@@ -1137,13 +1161,16 @@ static hipError_t run_encode_fast(const EncArgs& a, hipStream_t s) {
             } else {
                 launch_fused<K, M, G, T, NBUF, 16>(a, s);
             }
+            p = PATH_FIRSTGEN;
         }
     } else {
         const int64_t cols = (a.S + 15) >> 4;
         const unsigned gx = (unsigned)((cols + 255) / 256);
         const unsigned gy = (unsigned)(a.n_blocks < 65535 ? a.n_blocks : 65535);
         hipLaunchKernelGGL((k_encode_only<K, M>), dim3(gx, gy), dim3(256), 0, s, a);
+        p = PATH_FIRSTGEN;
     }
+    if (path) *path = p;
     return hipGetLastError();
 }
 
@@ -1158,25 +1185,24 @@ bool has_fast_encode(int k, int m) {
     return false;
 }
 
-hipError_t launch_encode(const EncArgs& a, hipStream_t s, bool* used_fast) {
+hipError_t launch_encode(const EncArgs& a, hipStream_t s, int* path) {
+    if (path) *path = PATH_NONE;
     if (a.n_blocks <= 0 || a.S <= 0) return hipSuccess;
     // Vectorised kernels: 16-byte shard columns and no Split padding.
     const bool vec_ok = (a.S % 16) == 0 && a.n == (int64_t)a.k * a.S;
 #define X(K, M)                                  \
     if (vec_ok && a.k == K && a.m == M) {        \
-        if (used_fast) *used_fast = true;        \
-        return run_encode_fast<K, M>(a, s);      \
+        return run_encode_fast<K, M>(a, s, path); \
     }
     ZS3_FAST_KM(X)
 #undef X
-    if (used_fast) *used_fast = false;
+    if (path) *path = PATH_GENERIC;
     const int R = a.k + a.m;
     int nt = round64(4 * R);
     if (nt < 256) nt = 256;
     if (nt > 1024) nt = 1024;
     const size_t lds = (size_t)R * GEN_TS + 256 + 512 + (size_t)a.m * a.k;
-    hipError_t e = hipFuncSetAttribute((const void*)k_encode_hash_generic,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipError_t e = ensure_dyn_lds((const void*)k_encode_hash_generic, lds);
     if (e != hipSuccess) return e;
     const unsigned grid = (unsigned)(a.n_blocks < 65535 ? a.n_blocks : 65535);
     hipLaunchKernelGGL(k_encode_hash_generic, dim3(grid), dim3(nt), lds, s, a);
@@ -1188,8 +1214,11 @@ static hipError_t run_rec_fast(const RecArgs& a, hipStream_t s) {
     const int64_t cols = (a.S + 15) >> 4;
     const unsigned gx = (unsigned)((cols + 255) / 256);
     const unsigned gy = (unsigned)(a.n_blocks < 65535 ? a.n_blocks : 65535);
-    if (a.e <= 2 && (g_variant == 220 || g_variant == 221)) {
-        const int nc = g_variant == 220 ? 2 : 4;
+#if ZS3_DIAG
+    if (a.e <= 2 && (a.variant == 220 || a.variant == 221)) {
+        // 2 or 4 columns per thread, all loads issued before the products (measured
+        // slower: 1.04-1.06 vs 1.00 ms, scripts/rec_ab.py)
+        const int nc = a.variant == 220 ? 2 : 4;
         const unsigned gx2 = (unsigned)((cols + 256 * nc - 1) / (256 * nc));
         if (nc == 2)
             hipLaunchKernelGGL((k_reconstruct<K, 2, 2>), dim3(gx2, gy), dim3(256), 0, s, a);
@@ -1197,6 +1226,7 @@ static hipError_t run_rec_fast(const RecArgs& a, hipStream_t s) {
             hipLaunchKernelGGL((k_reconstruct<K, 2, 4>), dim3(gx2, gy), dim3(256), 0, s, a);
         return hipGetLastError();
     }
+#endif
     if (a.e <= 2)
         hipLaunchKernelGGL((k_reconstruct<K, 2>), dim3(gx, gy), dim3(256), 0, s, a);
     else
@@ -1204,10 +1234,11 @@ static hipError_t run_rec_fast(const RecArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_reconstruct(const RecArgs& a, hipStream_t s, bool* used_fast) {
+hipError_t launch_reconstruct(const RecArgs& a, hipStream_t s, int* path) {
+    if (path) *path = PATH_NONE;
     if (a.n_blocks <= 0 || a.S <= 0 || a.e <= 0) return hipSuccess;
     if (a.e <= 4 && (a.S % 16) == 0) {
-        if (used_fast) *used_fast = true;
+        if (path) *path = PATH_FIRSTGEN;
         switch (a.k) {
             case 2: return run_rec_fast<2>(a, s);
             case 3: return run_rec_fast<3>(a, s);
@@ -1221,10 +1252,9 @@ hipError_t launch_reconstruct(const RecArgs& a, hipStream_t s, bool* used_fast) 
             default: break;
         }
     }
-    if (used_fast) *used_fast = false;
+    if (path) *path = PATH_GENERIC;
     const size_t lds = (size_t)((a.e * a.k + 3) & ~3) + 4 * (size_t)(a.k + a.e);
-    hipError_t e = hipFuncSetAttribute((const void*)k_reconstruct_generic,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipError_t e = ensure_dyn_lds((const void*)k_reconstruct_generic, lds);
     if (e != hipSuccess) return e;
     const unsigned gx = (unsigned)((a.S + 255) / 256);
     const unsigned gy = (unsigned)(a.n_blocks < 65535 ? a.n_blocks : 65535);
@@ -1234,28 +1264,24 @@ hipError_t launch_reconstruct(const RecArgs& a, hipStream_t s, bool* used_fast) 
 
 template <int K, int EMAX, bool HOUT>
 static hipError_t run_vr(const VrArgs& a, hipStream_t s) {
-    // Variant 201 (diagnostics): 16 stripes per workgroup, one workgroup per CU (LDS
-    // >= 80 KiB + 1).  Measured SLOWER than the default on RS(8+4) 4096 x 1 MiB
-    // (verify 1.09 vs 0.84 ms, verify+rebuild 1.57 vs 1.40, heal 1.69 vs 1.50;
-    // scripts/get_ab.py): at 2 waves per SIMD this kernel, unlike the encode, is short of
-    // loads in flight, and the default's two workgroups per CU already balance.
+#if ZS3_DIAG
+    // Variant 201: 16 stripes per workgroup, one workgroup per CU (LDS >= 80 KiB + 1).
+    // Measured SLOWER than the default on RS(8+4) 4096 x 1 MiB (verify 1.09 vs 0.84 ms,
+    // verify+rebuild 1.57 vs 1.40, heal 1.69 vs 1.50; scripts/get_ab.py): at 2 waves per
+    // SIMD this kernel, unlike the encode, is short of loads in flight.
     using Big = VrShape<K, EMAX, HOUT, 16>;
     if constexpr (Big::NT <= 1024) {
-        if (a.n_blocks >= 16 * 256 && g_variant == 201) {
+        if (a.n_blocks >= 16 * 256 && a.variant == 201) {
             auto kern = k_verify_reconstruct<K, EMAX, HOUT, 16>;
             constexpr size_t dyn = Big::TILE > 82 * 1024 ? Big::TILE : 82 * 1024;
-            static bool attr = false;
-            if (!attr) {
-                hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                   (int)dyn);
-                if (e != hipSuccess) return e;
-                attr = true;
-            }
+            hipError_t e = ensure_dyn_lds((const void*)kern, dyn);
+            if (e != hipSuccess) return e;
             const int64_t grid = (a.n_blocks + Big::G - 1) / Big::G;
             hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(Big::NT), dyn, s, a);
             return hipGetLastError();
         }
     }
+#endif
     using Sh = VrShape<K, EMAX, HOUT>;
     static_assert(Sh::TILE <= 65536, "default GET tile fits the default LDS limit");
     const int64_t grid = (a.n_blocks + Sh::G - 1) / Sh::G;
@@ -1264,36 +1290,41 @@ static hipError_t run_vr(const VrArgs& a, hipStream_t s) {
 }
 
 template <int K>
-static hipError_t run_vr_k(const VrArgs& a, hipStream_t s) {
-    // Default for RS(8+4)-shaped verify-only / rebuild-2 GETs: the warp-specialised
-    // k_vr_ws (fused_v2.hip): verify 0.85 -> 0.70 ms, verify + rebuild 2 1.41 -> 1.13 ms
-    // on 4096 x 1 MiB (scripts/get_ab.py).  Variant 200-209 keep this kernel.
-    if (g_variant == 0 || (g_variant >= 210 && g_variant <= 215))
-        if (launch_vr_ws(g_variant, a, s)) return hipGetLastError();
+static hipError_t run_vr_k(const VrArgs& a, hipStream_t s, int* path) {
+    // Default for the RS(8+4)-, RS(4+2)- and RS(16+4)-shaped GETs: the warp-specialised
+    // k_vr_ws (fused_v2.hip): RS(8+4) verify 0.85 -> 0.70 ms, verify + rebuild 2
+    // 1.41 -> 1.13 ms on 4096 x 1 MiB (scripts/get_ab.py).  Variants 200-209 (diagnostics)
+    // force the first-generation kernel.
+    if (a.variant == 0 || (ZS3_DIAG && a.variant >= 210 && a.variant <= 219))
+        if (launch_vr_ws(a.variant, a, s)) {
+            if (path) *path = PATH_WS;
+            return hipGetLastError();
+        }
+    if (path) *path = PATH_FIRSTGEN;
     const bool hout = a.sums_out != nullptr;
     if (a.e == 0) return run_vr<K, 0, false>(a, s);
     if (a.e <= 2) return hout ? run_vr<K, 2, true>(a, s) : run_vr<K, 2, false>(a, s);
     return hout ? run_vr<K, 4, true>(a, s) : run_vr<K, 4, false>(a, s);
 }
 
-hipError_t launch_verify_reconstruct(const VrArgs& a, hipStream_t s, bool* used_fast) {
+hipError_t launch_verify_reconstruct(const VrArgs& a, hipStream_t s, int* path) {
+    if (path) *path = PATH_NONE;
     if (a.n_blocks <= 0 || a.S <= 0) return hipSuccess;
     if (a.e <= 4 && (a.S % 16) == 0) {
-        if (used_fast) *used_fast = true;
         switch (a.k) {
-            case 2: return run_vr_k<2>(a, s);
-            case 4: return run_vr_k<4>(a, s);
-            case 6: return run_vr_k<6>(a, s);
-            case 8: return run_vr_k<8>(a, s);
-            case 10: return run_vr_k<10>(a, s);
-            case 12: return run_vr_k<12>(a, s);
-            case 16: return run_vr_k<16>(a, s);
+            case 2: return run_vr_k<2>(a, s, path);
+            case 4: return run_vr_k<4>(a, s, path);
+            case 6: return run_vr_k<6>(a, s, path);
+            case 8: return run_vr_k<8>(a, s, path);
+            case 10: return run_vr_k<10>(a, s, path);
+            case 12: return run_vr_k<12>(a, s, path);
+            case 16: return run_vr_k<16>(a, s, path);
             default: break;
         }
     }
     // Any other shape: one verify launch per survivor row, then the reconstruct
     // kernel, then (heal) one hash launch per rebuilt row.
-    if (used_fast) *used_fast = false;
+    if (path) *path = PATH_GENERIC;
     const int R = a.k + a.m;
     int32_t rows[256];
     if (hipMemcpyAsync(rows, a.rows, (size_t)(a.k + a.e) * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
@@ -1309,6 +1340,7 @@ hipError_t launch_verify_reconstruct(const VrArgs& a, hipStream_t s, bool* used_
         h.bad = a.bad + rows[j];
         h.sum_stride = (int64_t)R * 32;
         h.bad_stride = R;
+        h.ids = a.ids;
         for (int q = 0; q < 4; ++q) h.key[q] = a.key[q];
         hipError_t e = launch_hash(h, s);
         if (e != hipSuccess) return e;
@@ -1324,6 +1356,7 @@ hipError_t launch_verify_reconstruct(const VrArgs& a, hipStream_t s, bool* used_
         r.rows = a.rows;
         r.k = a.k;
         r.e = a.e;
+        r.ids = a.ids;
         hipError_t e = launch_reconstruct(r, s, nullptr);
         if (e != hipSuccess) return e;
         if (a.sums_out) {
@@ -1335,6 +1368,7 @@ hipError_t launch_verify_reconstruct(const VrArgs& a, hipStream_t s, bool* used_
                 h.n = a.n_blocks;
                 h.sums = a.sums_out + (int64_t)rows[a.k + i] * 32;
                 h.sum_stride = (int64_t)R * 32;
+                h.ids = a.ids;
                 for (int q = 0; q < 4; ++q) h.key[q] = a.key[q];
                 e = launch_hash(h, s);
                 if (e != hipSuccess) return e;
@@ -1358,6 +1392,23 @@ hipError_t launch_fill(uint8_t* out, int64_t stride, int64_t len, int64_t n, uin
     const unsigned gx = (unsigned)((nw + 255) / 256 < 256 ? (nw + 255) / 256 : 256);
     const unsigned gy = (unsigned)(n < 65535 ? n : 65535);
     hipLaunchKernelGGL(k_fill, dim3(gx, gy), dim3(256), 0, s, out, stride, len, n, seed, obj0);
+    return hipGetLastError();
+}
+
+// One wavefront per row: OR of the row's flags (deep-scan: a file is corrupt when any
+// of its chunks is).
+__global__ void __launch_bounds__(256) k_any_rows(const int32_t* flags, int64_t rows, int64_t cols, int32_t* out) {
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= rows) return;
+    int any = 0;
+    for (int64_t c = threadIdx.x & 63; c < cols; c += 64) any |= flags[r * cols + c] != 0;
+    const unsigned long long b = __ballot(any);
+    if ((threadIdx.x & 63) == 0) out[r] = b ? 1 : 0;
+}
+
+hipError_t launch_any_rows(const int32_t* flags, int64_t rows, int64_t cols, int32_t* out, hipStream_t s) {
+    if (rows <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_any_rows, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, flags, rows, cols, out);
     return hipGetLastError();
 }
 

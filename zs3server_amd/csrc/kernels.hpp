@@ -1,10 +1,29 @@
 // kernels.hpp — launch interface between the C-ABI layer (zs3gpu.hip) and the
-// HIP kernels (kernels.hip).  Internal; not part of the public ABI.
+// HIP kernels (kernels.hip, fused_v2.hip, digest.hip).  Internal; not part of the
+// public ABI.
+//
+// There is no process-wide tuning state: every launch carries its own `variant`
+// (0 = the tuned default).  Non-zero variants exist only in the diagnostics build
+// (ZS3_DIAG, libzs3gpu_diag.so); the product library compiles the defaults and the
+// generic fallbacks only.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#ifndef ZS3_DIAG
+#define ZS3_DIAG 0
+#endif
+
 namespace zs3k {
+
+// Which kernel family served a launch (zs3_last_path; include/zs3gpu.h ZS3_PATH_*).
+enum Path : int {
+    PATH_NONE = -1,
+    PATH_GENERIC = 0,   // byte kernels with log/exp tables (any k, m, S)
+    PATH_FIRSTGEN = 1,  // first-generation specialised kernels (kernels.hip)
+    PATH_WS = 2,        // warp-specialised kernels (fused_v2.hip k_ehx_ws / k_vr_ws)
+    PATH_PIPE = 3,      // mixed-wave second-generation encode (fused_v2.hip k_ehx)
+};
 
 // Batched Split+Encode(+HH256) over n_blocks independent blocks.
 // Block b: data bytes at data + b*data_stride, length n (<= k*S; bytes beyond n are
@@ -23,13 +42,14 @@ struct EncArgs {
     int64_t n_blocks;
     uint64_t key[4];          // HighwayHash key words (little-endian)
     int k, m;
-    uint64_t* dbg;            // diagnostics build only: per-wave phase cycle sums
+    uint64_t* dbg;            // diagnostics build only: per-wave stamps (nullptr in the product)
     int dyb;                  // 0, or 2/4: parity block is dyadic in dyb x dyb blocks
-    const uint32_t* dtables;  // dyadic Karatsuba tables (3 or 9 coefficients per block)
+    const uint32_t* dtables;  // dyadic local-ring tables (m coefficients per block)
+    int variant;              // 0 = tuned default (the only value the product build accepts)
 };
 
 // Reconstruct: out rows = coef x valid rows, per block.  Block b shard i at
-// shards + b*block_stride + i*S.
+// shards + slot(b)*block_stride + i*S, slot(b) = ids ? ids[b] : b.
 struct RecArgs {
     uint8_t* shards;
     int64_t block_stride;
@@ -39,9 +59,18 @@ struct RecArgs {
     const uint8_t* coef;      // e x k coefficients (generic path)
     const int32_t* rows;      // k valid row indices then e output row indices
     int k, e;
+    const int32_t* ids;       // optional device block-slot list (per-block erasure patterns)
+    int variant;
 };
 
-// HighwayHash-256 of n equal-length messages (bitrot verify / reader path).
+// HighwayHash-256 of n messages (bitrot writer sums / reader verify / deep scan).
+// Message i: slot s = ids ? ids[i] : i.  Uniform mode: bytes at msgs + s*stride,
+// length len.  Ragged mode (lens != nullptr): length lens[i]; ptrs != nullptr gives
+// each message's address directly.  Chunked-file mode (chunk > 0): message i is chunk
+// c = i % nchunks of file f = i / nchunks in the on-disk HighwayHash256S layout
+// [32-byte sum][chunk]* (cmd/bitrot-streaming.go:43-65): bytes at
+// msgs + f*stride + c*(chunk+32) + 32, expected sum 32 bytes before them, length
+// chunk except the last chunk (last_len).
 struct HashArgs {
     const uint8_t* msgs;
     int64_t stride;
@@ -53,12 +82,19 @@ struct HashArgs {
     uint64_t key[4];
     int64_t sum_stride;       // 0 = 32
     int64_t bad_stride;       // 0 = 1
+    const int32_t* ids;       // optional slot list
+    const int64_t* lens;      // ragged lengths (device), or nullptr
+    const uint8_t* const* ptrs;  // ragged message addresses (device), or nullptr
+    int64_t chunk;            // chunked-file mode: shard size (0 = off)
+    int64_t nchunks;          // chunks per file
+    int64_t last_len;         // length of each file's last chunk
 };
 
 // GET / heal pass: verify the k survivor shards the decode reads
 // against their stored bitrot sums and rebuild the missing shards in one pass.
+// Block b lives in slot(b) = ids ? ids[b] : b of every array.
 struct VrArgs {
-    uint8_t* shards;          // [n][k+m][S] at block_stride
+    uint8_t* shards;          // [slots][k+m][S] at block_stride
     int64_t block_stride;
     int64_t S;
     int64_t n_blocks;
@@ -66,10 +102,12 @@ struct VrArgs {
     const uint8_t* coef;      // e x k coefficients (fallback path)
     const int32_t* rows;      // k survivor row indices then e rebuilt row indices
     int k, m, e;
-    const uint8_t* expect;    // [n][k+m][32] stored sums; survivors are compared
-    int32_t* bad;             // [n][k+m]: 1 = survivor failed bitrot (errFileCorrupt)
-    uint8_t* sums_out;        // optional [n][k+m][32]: HH256 of the rebuilt rows
+    const uint8_t* expect;    // [slots][k+m][32] stored sums; survivors are compared
+    int32_t* bad;             // [slots][k+m]: 1 = survivor failed bitrot (errFileCorrupt)
+    uint8_t* sums_out;        // optional [slots][k+m][32]: HH256 of the rebuilt rows
     uint64_t key[4];
+    const int32_t* ids;       // optional device block-slot list
+    int variant;
 };
 
 // Batched MD5 / SHA-256 (digest.hip): message i of lens[i] (or len) bytes at
@@ -83,27 +121,31 @@ struct DigestArgs {
     uint8_t* out;
 };
 
-// Returns hipSuccess or an error from the launch.
-hipError_t launch_encode(const EncArgs& a, hipStream_t s, bool* used_fast);
-hipError_t launch_reconstruct(const RecArgs& a, hipStream_t s, bool* used_fast);
-hipError_t launch_verify_reconstruct(const VrArgs& a, hipStream_t s, bool* used_fast);
+// Launches return hipSuccess or the launch error; *path (may be null) receives the
+// kernel family that ran.
+hipError_t launch_encode(const EncArgs& a, hipStream_t s, int* path);
+hipError_t launch_reconstruct(const RecArgs& a, hipStream_t s, int* path);
+hipError_t launch_verify_reconstruct(const VrArgs& a, hipStream_t s, int* path);
 hipError_t launch_hash(const HashArgs& a, hipStream_t s);
 hipError_t launch_md5(const DigestArgs& a, hipStream_t s);
 hipError_t launch_sha256(const DigestArgs& a, hipStream_t s);
 hipError_t launch_fill(uint8_t* out, int64_t stride, int64_t len, int64_t n, uint64_t seed,
                        uint64_t obj0, hipStream_t s);
+// out[r] = 1 if any of flags[r*cols .. r*cols+cols) is non-zero, else 0.
+hipError_t launch_any_rows(const int32_t* flags, int64_t rows, int64_t cols, int32_t* out, hipStream_t s);
 
-// Number of (k, m) pairs with a specialised fused kernel, and whether (k, m) has one.
+// Whether (k, m) has a specialised fused kernel.
 bool has_fast_encode(int k, int m);
 
-// Second-generation fused encode+hash kernel (fused_v2.hip), variant numbers 50+.
-// Returns false when the variant does not apply to a.k/a.m (caller falls back).
-bool launch_ehx(int v, const EncArgs& a, hipStream_t s);
+// Second-generation fused encode+hash kernels (fused_v2.hip).  `v` is a variant
+// number; the product build knows only the defaults it dispatches to.  Returns the
+// path that ran, or PATH_NONE when the variant does not apply (caller falls back).
+int launch_ehx(int v, const EncArgs& a, hipStream_t s);
 // Warp-specialised GET / heal pass (fused_v2.hip); false if the shape has no instance.
 bool launch_vr_ws(int v, const VrArgs& a, hipStream_t s);
 
-// Tuning knob for experiments: 0 = default variant.
-void set_variant(int v);
-int get_variant();
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device, size),
+// thread-safe.
+hipError_t ensure_dyn_lds(const void* kern, size_t bytes);
 
 }  // namespace zs3k

@@ -1,0 +1,582 @@
+// queue.hip — cross-request batching submission queue (SURVEY.md §8b "Threading",
+// §7 hard part iv).
+//
+// The reference encodes ONE 1 MiB block per request, strictly sequentially per object
+// (cmd/erasure-encode.go:83-111 -> Erasure.EncodeData, cmd/erasure-coding.go:77-91),
+// and decodes one block per parallelReader round (cmd/erasure-decode.go:230-276 ->
+// DecodeDataBlocks :96).  One block is ~0.2 us of HBM work against tens of us of
+// fixed launch + PCIe cost, so a drop-in that calls the device once per block loses to
+// the CPU.  This queue gathers the blocks of all concurrent requests (every Go
+// goroutine that calls EncodeData / DecodeDataBlocks sits in its own OS thread inside
+// cgo) into device batches:
+//
+//   submitter thread:  reserve a position in the lane's open slot (pinned staging),
+//                      copy its block in (in parallel with other submitters), return a
+//                      zs3_req handle
+//   dispatcher thread: close the open slot when it is full, when nothing is in flight
+//                      (batch-while-busy: an idle device gets work at once, a busy
+//                      one lets the next batch grow), when the oldest block has waited
+//                      max_wait_us, or on flush; then H2D -> kernels -> D2H on the
+//                      lane's stream, all asynchronous
+//   completer thread:  waits for each launched slot's event, marks it done
+//   zs3_req_wait:      the submitter copies its own results out of the slot (again in
+//                      parallel), the last one frees the slot for reuse
+//
+// Lanes: ENCODE (EncodeData + the k+m bitrot sums), GET (ReconstructData of the
+// missing data shards, with the survivors' bitrot sums verified in the same pass when
+// given — parallelReader + DecodeDataBlocks), HEAL (Reconstruct of data and parity plus
+// the rebuilt shards' sums — Erasure.Heal, cmd/erasure-decode.go:287-332).  Every block
+// in a batch keeps its own erasure pattern (zs3_verify_reconstruct_batch_masks).
+// Blocks of the full shard size fill a slot from the front and go in one launch; the
+// short last block of an object (its own shard size, erasure-encode.go:85-96) fills
+// from the back and is launched on its own.
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "../../include/zs3gpu.h"
+
+namespace {
+
+enum Lane { ENC = 0, GET = 1, HEAL = 2, NLANE = 3 };
+using Clock = std::chrono::steady_clock;
+
+struct Slot;
+
+}  // namespace
+
+struct zs3_req {
+    zs3_queue* q = nullptr;
+    Slot* slot = nullptr;
+    int lane = ENC;
+    int pos = 0;
+    int64_t S = 0;  // shard size of this block
+    // encode
+    uint8_t* h_buf = nullptr;
+    int64_t len = 0;
+    uint8_t* h_sums = nullptr;
+    // decode
+    uint8_t* h_shards = nullptr;
+    uint8_t present[256];
+    const uint8_t* h_expect = nullptr;
+    int32_t* h_bad = nullptr;
+    uint8_t* h_sums_out = nullptr;
+    int status = ZS3_OK;
+};
+
+namespace {
+
+struct Slot {
+    int lane = ENC;
+    uint8_t* h = nullptr;  // pinned, same layout as d
+    uint8_t* d = nullptr;
+    enum State { FREE, OPEN, LAUNCHED, DONE } state = FREE;
+    int front = 0;         // next full-size position
+    int back = 0;          // short blocks placed at cap-1, cap-2, ...
+    int copying = 0;       // submitters still copying in
+    int refs = 0;          // requests not yet collected by their waiter
+    std::vector<zs3_req*> reqs;
+    Clock::time_point opened;
+    hipEvent_t done_ev = nullptr;
+    int launch_status = ZS3_OK;
+};
+
+}  // namespace
+
+struct zs3_queue {
+    const zs3_codec* c = nullptr;
+    int k = 0, m = 0, R = 0;
+    int64_t B = 0, S = 0, E = 0;  // block size, full shard size, bytes per position
+    int device = 0;
+    int cap = 128;                // positions per slot
+    int max_wait_us = 200;
+    int nslots = 3;
+
+    std::mutex mu;
+    std::condition_variable cv_space;   // a slot became free / open
+    std::condition_variable cv_disp;    // dispatcher: new work, copies finished, flush, stop
+    std::condition_variable cv_done;    // a slot finished
+    std::condition_variable cv_comp;    // completer: a slot was launched
+    std::vector<Slot> slots[NLANE];
+    bool alloc_failed[NLANE] = {false, false, false};
+    Slot* open[NLANE] = {nullptr, nullptr, nullptr};
+    int inflight[NLANE] = {0, 0, 0};
+    std::deque<Slot*> launched;
+    bool flush = false;
+    bool stop = false;       // dispatcher: drain the open slots and exit
+    bool comp_stop = false;  // completer: exit once every launched slot is done
+    hipStream_t stream[NLANE] = {nullptr, nullptr, nullptr};
+    std::thread disp, comp;
+    std::atomic<int64_t> n_batches{0}, n_blocks{0};
+
+    // region offsets inside a slot (bytes)
+    size_t off_sums() const { return (size_t)cap * E; }                       // [cap][R][32] sums / expect
+    size_t off_bad() const { return off_sums() + (size_t)cap * R * 32; }      // [cap][R] int32
+    size_t off_out() const { return off_bad() + (size_t)cap * R * 4; }        // [cap][R][32] heal sums
+    size_t slot_bytes(int lane) const {
+        return lane == ENC ? off_bad() : lane == GET ? off_out() : off_out() + (size_t)cap * R * 32;
+    }
+};
+
+namespace {
+
+int map_hip(hipError_t e) { return e == hipSuccess ? ZS3_OK : (e == hipErrorOutOfMemory ? ZS3_ERR_NOMEM : ZS3_ERR_DEVICE); }
+
+// Allocate a lane's slots on first use (caller holds q->mu; runs on a submitter).
+int ensure_lane(zs3_queue* q, int lane) {
+    if (!q->slots[lane].empty()) return ZS3_OK;
+    if (q->alloc_failed[lane]) return ZS3_ERR_NOMEM;
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    if (hipSetDevice(q->device) != hipSuccess) return ZS3_ERR_DEVICE;
+    std::vector<Slot> v((size_t)q->nslots);
+    int rc = ZS3_OK;
+    const size_t bytes = q->slot_bytes(lane);
+    for (auto& s : v) {
+        s.lane = lane;
+        if (rc == ZS3_OK) rc = map_hip(hipHostMalloc((void**)&s.h, bytes, hipHostMallocDefault));
+        if (rc == ZS3_OK) rc = map_hip(hipMalloc((void**)&s.d, bytes));
+        if (rc == ZS3_OK) rc = map_hip(hipEventCreateWithFlags(&s.done_ev, hipEventDisableTiming));
+    }
+    if (rc != ZS3_OK) {
+        for (auto& s : v) {
+            if (s.h) (void)hipHostFree(s.h);
+            if (s.d) (void)hipFree(s.d);
+            if (s.done_ev) (void)hipEventDestroy(s.done_ev);
+        }
+        q->alloc_failed[lane] = true;
+    } else {
+        q->slots[lane] = std::move(v);
+    }
+    (void)hipSetDevice(prev);
+    return rc;
+}
+
+// Reserve a position for one block in the lane's open slot (caller holds lk).
+int reserve(zs3_queue* q, std::unique_lock<std::mutex>& lk, zs3_req* r, bool full) {
+    int rc = ensure_lane(q, r->lane);
+    if (rc) return rc;
+    for (;;) {
+        if (q->stop) return ZS3_ERR_INVALID_ARG;
+        Slot* s = q->open[r->lane];
+        if (s && s->front + s->back < q->cap) {
+            r->slot = s;
+            r->pos = full ? s->front++ : q->cap - 1 - s->back++;
+            s->copying++;
+            s->refs++;
+            s->reqs.push_back(r);
+            if (s->front + s->back == q->cap) q->cv_disp.notify_one();
+            return ZS3_OK;
+        }
+        if (!s) {
+            for (auto& x : q->slots[r->lane])
+                if (x.state == Slot::FREE) {
+                    x.state = Slot::OPEN;
+                    x.front = x.back = x.copying = x.refs = 0;
+                    x.reqs.clear();
+                    x.launch_status = ZS3_OK;
+                    x.opened = Clock::now();
+                    q->open[r->lane] = &x;
+                    break;
+                }
+            if (q->open[r->lane]) continue;
+        }
+        q->cv_space.wait(lk);  // every slot busy (or the open one full): backpressure
+    }
+}
+
+void copy_in_done(zs3_queue* q, Slot* s) {
+    std::lock_guard<std::mutex> g(q->mu);
+    if (--s->copying == 0) q->cv_disp.notify_one();
+}
+
+// ---- launch of a closed slot (dispatcher thread, no lock held) ----------------------
+void launch_slot(zs3_queue* q, Slot* s) {
+    hipStream_t st = q->stream[s->lane];
+    const int k = q->k, m = q->m, R = q->R;
+    const int64_t E = q->E, S = q->S;
+    const int nf = s->front;
+    int rc = ZS3_OK;
+    auto chk = [&](int e) {
+        if (e != ZS3_OK && rc == ZS3_OK) rc = e;
+    };
+    uint8_t* dsum = s->d + q->off_sums();
+    uint8_t* hsum = s->h + q->off_sums();
+    if (s->lane == ENC) {
+        // full-size blocks: data rows in, one fused launch, parity rows + sums out
+        if (nf > 0) {
+            chk(map_hip(hipMemcpy2DAsync(s->d, (size_t)E, s->h, (size_t)E, (size_t)(k * S), (size_t)nf,
+                                         hipMemcpyHostToDevice, st)));
+            chk(zs3_encode_batch(q->c, s->d, E, q->B, nf, s->d + k * S, E, dsum, st));
+            chk(map_hip(hipMemcpy2DAsync(s->h + k * S, (size_t)E, s->d + k * S, (size_t)E, (size_t)(m * S),
+                                         (size_t)nf, hipMemcpyDeviceToHost, st)));
+            chk(map_hip(hipMemcpyAsync(hsum, dsum, (size_t)nf * R * 32, hipMemcpyDeviceToHost, st)));
+        }
+        for (zs3_req* r : s->reqs) {
+            if (r->pos < nf) continue;
+            const size_t o = (size_t)r->pos * E;
+            uint8_t* sb = dsum + (size_t)r->pos * R * 32;
+            chk(map_hip(hipMemcpyAsync(s->d + o, s->h + o, (size_t)(k * r->S), hipMemcpyHostToDevice, st)));
+            chk(zs3_encode_batch(q->c, s->d + o, E, r->len, 1, s->d + o + k * r->S, E, sb, st));
+            chk(map_hip(hipMemcpyAsync(s->h + o + k * r->S, s->d + o + k * r->S, (size_t)(m * r->S),
+                                       hipMemcpyDeviceToHost, st)));
+            chk(map_hip(hipMemcpyAsync(hsum + (size_t)r->pos * R * 32, sb, (size_t)R * 32, hipMemcpyDeviceToHost, st)));
+        }
+    } else {
+        const int data_only = s->lane == GET ? 1 : 0;
+        int32_t* dbad = (int32_t*)(s->d + q->off_bad());
+        uint8_t* hbad = s->h + q->off_bad();
+        uint8_t* dout = s->lane == HEAL ? s->d + q->off_out() : nullptr;
+        uint8_t* hout = s->h + q->off_out();
+        std::vector<uint8_t> pres;
+        std::vector<int32_t> status;
+        if (nf > 0) {
+            chk(map_hip(hipMemcpyAsync(s->d, s->h, (size_t)nf * E, hipMemcpyHostToDevice, st)));
+            chk(map_hip(hipMemcpyAsync(dsum, hsum, (size_t)nf * R * 32, hipMemcpyHostToDevice, st)));
+            pres.assign((size_t)nf * R, 0);
+            status.assign((size_t)nf, ZS3_OK);
+            for (zs3_req* r : s->reqs)
+                if (r->pos < nf) std::memcpy(&pres[(size_t)r->pos * R], r->present, (size_t)R);
+            const int e = zs3_verify_reconstruct_batch_masks(q->c, s->d, E, S, nf, pres.data(), data_only, dsum, dbad,
+                                                             dout, status.data(), st);
+            if (e != ZS3_OK && e != ZS3_ERR_TOO_FEW_SHARDS && e != ZS3_ERR_SHARD_NO_DATA) chk(e);
+            for (zs3_req* r : s->reqs)
+                if (r->pos < nf) r->status = status[(size_t)r->pos];
+            chk(map_hip(hipMemcpyAsync(hbad, dbad, (size_t)nf * R * 4, hipMemcpyDeviceToHost, st)));
+            if (dout) chk(map_hip(hipMemcpyAsync(hout, dout, (size_t)nf * R * 32, hipMemcpyDeviceToHost, st)));
+        }
+        for (zs3_req* r : s->reqs) {
+            if (r->pos < nf) continue;
+            const size_t o = (size_t)r->pos * E;
+            const size_t so = (size_t)r->pos * R * 32, bo = (size_t)r->pos * R * 4;
+            chk(map_hip(hipMemcpyAsync(s->d + o, s->h + o, (size_t)(R * r->S), hipMemcpyHostToDevice, st)));
+            chk(map_hip(hipMemcpyAsync(dsum + so, hsum + so, (size_t)R * 32, hipMemcpyHostToDevice, st)));
+            int32_t one = ZS3_OK;
+            const int e = zs3_verify_reconstruct_batch_masks(q->c, s->d + o, E, r->S, 1, r->present, data_only,
+                                                             dsum + so, (int32_t*)((uint8_t*)dbad + bo),
+                                                             dout ? dout + so : nullptr, &one, st);
+            if (e != ZS3_OK && e != ZS3_ERR_TOO_FEW_SHARDS && e != ZS3_ERR_SHARD_NO_DATA) chk(e);
+            r->status = one;
+            chk(map_hip(hipMemcpyAsync(hbad + bo, (uint8_t*)dbad + bo, (size_t)R * 4, hipMemcpyDeviceToHost, st)));
+            if (dout) chk(map_hip(hipMemcpyAsync(hout + so, dout + so, (size_t)R * 32, hipMemcpyDeviceToHost, st)));
+        }
+        // rebuilt rows back to the pinned slot (only those, per block)
+        for (zs3_req* r : s->reqs) {
+            if (r->status != ZS3_OK) continue;
+            const size_t o = (size_t)r->pos * E;
+            for (int i = 0; i < R; ++i)
+                if (!r->present[i] && (i < k || !data_only))
+                    chk(map_hip(hipMemcpyAsync(s->h + o + (size_t)i * r->S, s->d + o + (size_t)i * r->S, (size_t)r->S,
+                                               hipMemcpyDeviceToHost, st)));
+        }
+    }
+    chk(map_hip(hipEventRecord(s->done_ev, st)));
+    s->launch_status = rc;
+    q->n_batches.fetch_add(1);
+    q->n_blocks.fetch_add((int64_t)s->reqs.size());
+}
+
+bool ready_to_close(zs3_queue* q, Slot* s, int lane, Clock::time_point now) {
+    if (s->reqs.empty()) return false;
+    if (s->front + s->back == q->cap || q->flush || q->stop) return true;
+    if (q->inflight[lane] == 0) return true;  // batch while busy
+    return now - s->opened >= std::chrono::microseconds(q->max_wait_us);
+}
+
+void dispatcher(zs3_queue* q) {
+    (void)hipSetDevice(q->device);
+    std::unique_lock<std::mutex> lk(q->mu);
+    for (;;) {
+        bool launched_any = false;
+        auto now = Clock::now();
+        Clock::time_point wake = now + std::chrono::milliseconds(50);
+        for (int lane = 0; lane < NLANE; ++lane) {
+            Slot* s = q->open[lane];
+            if (!s) continue;
+            if (!ready_to_close(q, s, lane, now)) {
+                if (!s->reqs.empty()) {
+                    auto t = s->opened + std::chrono::microseconds(q->max_wait_us);
+                    if (t < wake) wake = t;
+                }
+                continue;
+            }
+            if (s->copying > 0) continue;  // the last copier notifies
+            q->open[lane] = nullptr;
+            s->state = Slot::LAUNCHED;
+            q->inflight[lane]++;
+            q->cv_space.notify_all();  // submitters may open the next slot
+            lk.unlock();
+            launch_slot(q, s);
+            lk.lock();
+            q->launched.push_back(s);
+            q->cv_comp.notify_one();
+            launched_any = true;
+        }
+        bool pending = false;
+        for (int lane = 0; lane < NLANE; ++lane) pending |= q->open[lane] && !q->open[lane]->reqs.empty();
+        if (!pending) q->flush = false;
+        if (q->stop && !pending) break;
+        if (!launched_any) q->cv_disp.wait_until(lk, wake);
+    }
+}
+
+void completer(zs3_queue* q) {
+    std::unique_lock<std::mutex> lk(q->mu);
+    for (;;) {
+        q->cv_comp.wait(lk, [&] { return !q->launched.empty() || q->comp_stop; });
+        if (q->launched.empty()) break;
+        Slot* s = q->launched.front();
+        q->launched.pop_front();
+        lk.unlock();
+        const hipError_t e = hipEventSynchronize(s->done_ev);
+        lk.lock();
+        if (e != hipSuccess && s->launch_status == ZS3_OK) s->launch_status = ZS3_ERR_DEVICE;
+        s->state = Slot::DONE;
+        q->inflight[s->lane]--;
+        q->cv_done.notify_all();
+        q->cv_disp.notify_one();  // batch-while-busy: the next open slot may go now
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int zs3_queue_new(const zs3_codec* c, const zs3_queue_opts* opts, zs3_queue** out) {
+    if (!c || !out) return ZS3_ERR_INVALID_ARG;
+    *out = nullptr;
+    auto* q = new zs3_queue();
+    q->c = c;
+    if (zs3_codec_params(c, &q->k, &q->m, &q->B) != ZS3_OK) {
+        delete q;
+        return ZS3_ERR_INVALID_ARG;
+    }
+    q->R = q->k + q->m;
+    q->S = zs3_shard_size(c);
+    q->E = (int64_t)q->R * q->S;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    q->device = dev;
+    if (opts) {
+        if (opts->device >= 0) q->device = opts->device;
+        if (opts->max_batch > 0) q->cap = opts->max_batch;
+        if (opts->max_wait_us > 0) q->max_wait_us = opts->max_wait_us;
+        if (opts->slots > 0) q->nslots = opts->slots;
+    }
+    if (q->nslots < 2) q->nslots = 2;
+    int prev = dev;
+    if (hipSetDevice(q->device) != hipSuccess) {
+        delete q;
+        return ZS3_ERR_DEVICE;
+    }
+    for (auto& s : q->stream)
+        if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+            (void)hipSetDevice(prev);
+            delete q;
+            return ZS3_ERR_DEVICE;
+        }
+    (void)hipSetDevice(prev);
+    q->disp = std::thread(dispatcher, q);
+    q->comp = std::thread(completer, q);
+    *out = q;
+    return ZS3_OK;
+}
+
+void zs3_queue_free(zs3_queue* q) {
+    if (!q) return;
+    {
+        std::lock_guard<std::mutex> g(q->mu);
+        q->stop = true;
+        q->cv_disp.notify_all();
+        q->cv_space.notify_all();
+    }
+    q->disp.join();
+    {
+        std::lock_guard<std::mutex> g(q->mu);
+        q->comp_stop = true;
+        q->cv_comp.notify_all();
+    }
+    q->comp.join();
+    // outstanding requests must have been waited for by their owners; wait for any
+    // slot still referenced so their buffers outlive the copies
+    {
+        std::unique_lock<std::mutex> lk(q->mu);
+        q->cv_done.wait(lk, [&] {
+            for (auto& v : q->slots)
+                for (auto& s : v)
+                    if (s.state == Slot::LAUNCHED || (s.state == Slot::DONE && s.refs > 0)) return false;
+            return true;
+        });
+    }
+    for (auto& v : q->slots)
+        for (auto& s : v) {
+            if (s.h) (void)hipHostFree(s.h);
+            if (s.d) (void)hipFree(s.d);
+            if (s.done_ev) (void)hipEventDestroy(s.done_ev);
+        }
+    for (auto& s : q->stream)
+        if (s) (void)hipStreamDestroy(s);
+    delete q;
+}
+
+int zs3_queue_submit_encode(zs3_queue* q, uint8_t* h_buf, int64_t len, int64_t cap, uint8_t* h_sums,
+                            zs3_req** req) {
+    if (!q || !req || len < 0 || len > q->B || (len > 0 && !h_buf)) return ZS3_ERR_INVALID_ARG;
+    *req = nullptr;
+    if (len == 0) return ZS3_OK;  // EncodeData len 0: k+m empty shards, nothing to do
+    const int64_t Sb = (len + q->k - 1) / q->k;
+    if (cap < (int64_t)q->R * Sb) return ZS3_ERR_INVALID_ARG;
+    auto* r = new zs3_req();
+    r->q = q;
+    r->lane = ENC;
+    r->S = Sb;
+    r->h_buf = h_buf;
+    r->len = len;
+    r->h_sums = h_sums;
+    Slot* s;
+    {
+        std::unique_lock<std::mutex> lk(q->mu);
+        const int rc = reserve(q, lk, r, len == q->B);
+        if (rc) {
+            delete r;
+            return rc;
+        }
+        s = r->slot;
+    }
+    // Split (reedsolomon): data rows are the input bytes, zero-padded to k*S
+    uint8_t* dst = s->h + (size_t)r->pos * q->E;
+    std::memcpy(dst, h_buf, (size_t)len);
+    if (q->k * Sb > len) std::memset(dst + len, 0, (size_t)(q->k * Sb - len));
+    copy_in_done(q, s);
+    *req = r;
+    return ZS3_OK;
+}
+
+int zs3_queue_submit_decode(zs3_queue* q, uint8_t* h_shards, int64_t shard_len, const uint8_t* h_present,
+                            int data_only, const uint8_t* h_expect, int32_t* h_bad, uint8_t* h_sums_out,
+                            zs3_req** req) {
+    if (!q || !req || !h_present || shard_len < 0 || shard_len > q->S || (shard_len > 0 && !h_shards))
+        return ZS3_ERR_INVALID_ARG;
+    *req = nullptr;
+    if (shard_len == 0) return ZS3_ERR_SHARD_NO_DATA;
+    auto* r = new zs3_req();
+    r->q = q;
+    r->lane = data_only ? GET : HEAL;
+    r->S = shard_len;
+    r->h_shards = h_shards;
+    r->h_expect = h_expect;
+    r->h_bad = h_bad;
+    r->h_sums_out = h_sums_out;
+    for (int i = 0; i < q->R; ++i) r->present[i] = h_present[i] ? 1 : 0;
+    Slot* s;
+    {
+        std::unique_lock<std::mutex> lk(q->mu);
+        const int rc = reserve(q, lk, r, shard_len == q->S);
+        if (rc) {
+            delete r;
+            return rc;
+        }
+        s = r->slot;
+    }
+    uint8_t* dst = s->h + (size_t)r->pos * q->E;
+    for (int i = 0; i < q->R; ++i)
+        if (r->present[i]) std::memcpy(dst + (size_t)i * shard_len, h_shards + (size_t)i * shard_len, (size_t)shard_len);
+    uint8_t* exp = s->h + q->off_sums() + (size_t)r->pos * q->R * 32;
+    if (h_expect)
+        std::memcpy(exp, h_expect, (size_t)q->R * 32);
+    else
+        std::memset(exp, 0, (size_t)q->R * 32);  // no stored sums: flags are ignored
+    copy_in_done(q, s);
+    *req = r;
+    return ZS3_OK;
+}
+
+int64_t zs3_req_wait(zs3_req* r) {
+    if (!r) return ZS3_OK;  // the empty-block case returned no handle
+    zs3_queue* q = r->q;
+    Slot* s = r->slot;
+    {
+        std::unique_lock<std::mutex> lk(q->mu);
+        if (s->state == Slot::OPEN) {
+            // a lone waiter must not sit out max_wait_us behind an idle device
+            q->cv_disp.notify_one();
+        }
+        q->cv_done.wait(lk, [&] { return s->state == Slot::DONE; });
+    }
+    int64_t rc = s->launch_status != ZS3_OK ? s->launch_status : r->status;
+    const size_t o = (size_t)r->pos * q->E;
+    const int k = q->k, R = q->R;
+    if (rc == ZS3_OK) {
+        if (r->lane == ENC) {
+            std::memcpy(r->h_buf + (size_t)k * r->S, s->h + o + (size_t)k * r->S, (size_t)(q->m * r->S));
+            if (k * r->S > r->len)
+                std::memset(r->h_buf + r->len, 0, (size_t)(k * r->S - r->len));  // Split zero-fill in place
+            if (r->h_sums) std::memcpy(r->h_sums, s->h + q->off_sums() + (size_t)r->pos * R * 32, (size_t)R * 32);
+            rc = r->S;
+        } else {
+            const int data_only = r->lane == GET;
+            for (int i = 0; i < R; ++i)
+                if (!r->present[i] && (i < k || !data_only))
+                    std::memcpy(r->h_shards + (size_t)i * r->S, s->h + o + (size_t)i * r->S, (size_t)r->S);
+            const int32_t* bad = (const int32_t*)(s->h + q->off_bad()) + (size_t)r->pos * R;
+            bool corrupt = false;
+            for (int i = 0; i < R; ++i) corrupt |= r->h_expect && bad[i];
+            if (r->h_bad) {
+                for (int i = 0; i < R; ++i) r->h_bad[i] = r->h_expect ? bad[i] : 0;
+            }
+            if (r->h_sums_out && r->lane == HEAL)
+                std::memcpy(r->h_sums_out, s->h + q->off_out() + (size_t)r->pos * R * 32, (size_t)R * 32);
+            if (corrupt) rc = ZS3_ERR_FILE_CORRUPT;
+        }
+    }
+    {
+        std::lock_guard<std::mutex> g(q->mu);
+        if (--s->refs == 0) {
+            s->state = Slot::FREE;
+            s->reqs.clear();
+            q->cv_space.notify_all();
+            q->cv_done.notify_all();
+        }
+    }
+    delete r;
+    return rc;
+}
+
+int zs3_queue_flush(zs3_queue* q) {
+    if (!q) return ZS3_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> g(q->mu);
+    q->flush = true;
+    q->cv_disp.notify_one();
+    return ZS3_OK;
+}
+
+int zs3_queue_stats(const zs3_queue* q, int64_t* batches, int64_t* blocks) {
+    if (!q) return ZS3_ERR_INVALID_ARG;
+    if (batches) *batches = q->n_batches.load();
+    if (blocks) *blocks = q->n_blocks.load();
+    return ZS3_OK;
+}
+
+int64_t zs3_queue_encode_data(zs3_queue* q, uint8_t* h_buf, int64_t len, int64_t cap, uint8_t* h_sums) {
+    zs3_req* r = nullptr;
+    const int rc = zs3_queue_submit_encode(q, h_buf, len, cap, h_sums, &r);
+    if (rc) return rc;
+    return r ? zs3_req_wait(r) : 0;
+}
+
+int zs3_queue_decode_data_blocks(zs3_queue* q, uint8_t* h_shards, int64_t shard_len, const uint8_t* h_present,
+                                 int data_only, const uint8_t* h_expect, int32_t* h_bad) {
+    zs3_req* r = nullptr;
+    const int rc = zs3_queue_submit_decode(q, h_shards, shard_len, h_present, data_only, h_expect, h_bad, nullptr, &r);
+    if (rc) return rc;
+    return (int)zs3_req_wait(r);
+}
+
+}  // extern "C"

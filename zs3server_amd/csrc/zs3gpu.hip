@@ -18,6 +18,9 @@
 #include <vector>
 
 #include "../../include/zs3gpu.h"
+#if ZS3_DIAG
+#include "../../include/zs3gpu_diag.h"
+#endif
 #include "gf256.hpp"
 #include "kernels.hpp"
 
@@ -31,8 +34,16 @@ const uint8_t kMagicKey[32] = {0x4b, 0xe7, 0x34, 0xfa, 0x8e, 0x23, 0x8a, 0xcd, 0
                                0x44, 0x14, 0x97, 0xe0, 0x9d, 0x13, 0x22, 0xde, 0x36, 0xa0};
 
 thread_local int t_last_path = -1;
-uint64_t* g_dbg = nullptr;  // diagnostics: stamped-variant output buffer
-int g_no_dyadic = 0;        // diagnostics: force the plain (m*k multiply) encode
+#if ZS3_DIAG
+// Diagnostics build only (libzs3gpu_diag.so): per-OS-thread experiment selection, so
+// concurrent callers never see each other's settings.
+thread_local int t_variant = 0;          // fused-kernel variant (0 = tuned default)
+thread_local uint64_t* t_dbg = nullptr;  // stamped-variant output buffer
+thread_local int t_no_dyadic = 0;        // force the plain (m*k multiply) encode
+inline int call_variant() { return t_variant; }
+#else
+inline int call_variant() { return 0; }
+#endif
 
 void key_words(const uint8_t* key, uint64_t out[4]) {
     const uint8_t* k = key ? key : kMagicKey;
@@ -206,6 +217,79 @@ int plan_device(zs3_codec* c, RecPlan* p, const uint32_t** tabs, const uint8_t**
     *coef = base + tb;
     *rows = (const int32_t*)(base + tb + cb);
     return ZS3_OK;
+}
+
+// Per-OS-thread pinned staging for block-id lists (per-block erasure patterns): the
+// list is copied into pinned memory, then stream-ordered into a hipMallocAsync'd
+// device buffer that is freed (hipFreeAsync) behind the kernels that read it.
+struct IdsStage {
+    int32_t* h = nullptr;
+    size_t cap = 0;
+    hipEvent_t ev = nullptr;  // last copy out of h
+    ~IdsStage() {
+        if (ev) (void)hipEventDestroy(ev);
+        if (h) (void)hipHostFree(h);
+    }
+};
+thread_local std::map<int, std::unique_ptr<IdsStage>> t_ids;
+
+int upload_ids(const int32_t* ids, size_t n, hipStream_t s, int32_t** d_out) {
+    const int d = current_device();
+    if (d < 0) return ZS3_ERR_DEVICE;
+    auto& sp = t_ids[d];
+    if (!sp) {
+        sp.reset(new IdsStage());
+        if (hipEventCreateWithFlags(&sp->ev, hipEventDisableTiming) != hipSuccess) return ZS3_ERR_DEVICE;
+    } else if (hipEventSynchronize(sp->ev) != hipSuccess) {  // the previous copy out of h is done
+        return ZS3_ERR_DEVICE;
+    }
+    const size_t bytes = n * sizeof(int32_t);
+    if (sp->cap < bytes) {
+        if (sp->h) (void)hipHostFree(sp->h);
+        sp->h = nullptr;
+        sp->cap = 0;
+        if (hipHostMalloc((void**)&sp->h, bytes, hipHostMallocDefault) != hipSuccess) return ZS3_ERR_NOMEM;
+        sp->cap = bytes;
+    }
+    std::memcpy(sp->h, ids, bytes);
+    if (hipMallocAsync((void**)d_out, bytes, s) != hipSuccess) return ZS3_ERR_NOMEM;
+    if (hipMemcpyAsync(*d_out, sp->h, bytes, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipEventRecord(sp->ev, s) != hipSuccess)
+        return ZS3_ERR_DEVICE;
+    return ZS3_OK;
+}
+
+// Blocks of a batch grouped by erasure pattern (zs3_*_batch_masks).
+struct PatternGroup {
+    std::shared_ptr<RecPlan> plan;
+    std::vector<int32_t> blocks;
+};
+
+int group_patterns(zs3_codec* c, const uint8_t* present, int64_t n, int data_only, int32_t* status,
+                   std::vector<PatternGroup>& groups) {
+    const int R = c->k + c->m;
+    std::map<std::string, size_t> idx;
+    int first = ZS3_OK;
+    std::string key((size_t)R, '\0');
+    for (int64_t b = 0; b < n; ++b) {
+        const uint8_t* row = present + b * R;
+        for (int i = 0; i < R; ++i) key[(size_t)i] = row[i] ? 1 : 0;
+        auto it = idx.find(key);
+        if (it == idx.end()) {
+            PatternGroup g;
+            g.plan = get_plan(c, (const uint8_t*)key.data(), data_only);
+            it = idx.emplace(key, groups.size()).first;
+            groups.push_back(std::move(g));
+        }
+        PatternGroup& g = groups[it->second];
+        if (status) status[b] = g.plan->status;
+        if (g.plan->status) {
+            if (first == ZS3_OK) first = g.plan->status;
+            continue;
+        }
+        g.blocks.push_back((int32_t)b);
+    }
+    return first;
 }
 
 // Per-OS-thread staging for host-pointer calls.
@@ -421,6 +505,14 @@ int zs3_codec_matrix(const zs3_codec* c, uint8_t* out) {
     return ZS3_OK;
 }
 
+int zs3_codec_params(const zs3_codec* c, int* k, int* m, int64_t* block_size) {
+    if (!c) return ZS3_ERR_INVALID_ARG;
+    if (k) *k = c->k;
+    if (m) *m = c->m;
+    if (block_size) *block_size = c->block_size;
+    return ZS3_OK;
+}
+
 int64_t zs3_shard_size(const zs3_codec* c) { return c ? ceil_frac(c->block_size, c->k) : 0; }
 
 int64_t zs3_shard_file_size(const zs3_codec* c, int64_t total) {
@@ -467,13 +559,17 @@ int zs3_encode_batch(const zs3_codec* cc, const uint8_t* d_data, int64_t data_st
     a.n_blocks = n_blocks;
     a.k = c->k;
     a.m = c->m;
-    a.dyb = g_no_dyadic ? 0 : c->dyb;
+    a.dyb = c->dyb;
     a.dtables = a.tables + c->dyadic_off;
     key_words(nullptr, a.key);
-    a.dbg = g_dbg;
-    bool fast = false;
-    rc = map_hip(zs3k::launch_encode(a, (hipStream_t)stream, &fast));
-    t_last_path = fast ? 1 : 0;
+    a.variant = call_variant();
+#if ZS3_DIAG
+    if (t_no_dyadic) a.dyb = 0;
+    a.dbg = t_dbg;
+#endif
+    int path = zs3k::PATH_NONE;
+    rc = map_hip(zs3k::launch_encode(a, (hipStream_t)stream, &path));
+    t_last_path = path;
     return rc;
 }
 
@@ -494,9 +590,10 @@ int zs3_reconstruct_batch(const zs3_codec* cc, uint8_t* d_shards, int64_t block_
     a.n_blocks = n_blocks;
     a.k = c->k;
     a.e = plan->e;
-    bool fast = false;
-    rc = map_hip(zs3k::launch_reconstruct(a, (hipStream_t)stream, &fast));
-    t_last_path = fast ? 1 : 0;
+    a.variant = call_variant();
+    int path = zs3k::PATH_NONE;
+    rc = map_hip(zs3k::launch_reconstruct(a, (hipStream_t)stream, &path));
+    t_last_path = path;
     return rc;
 }
 
@@ -527,9 +624,10 @@ int zs3_verify_reconstruct_batch(const zs3_codec* cc, uint8_t* d_shards, int64_t
     a.bad = d_bad;
     a.sums_out = a.e > 0 ? d_sums_out : nullptr;
     key_words(nullptr, a.key);
-    bool fast = false;
-    rc = map_hip(zs3k::launch_verify_reconstruct(a, (hipStream_t)stream, &fast));
-    t_last_path = fast ? 1 : 0;
+    a.variant = call_variant();
+    int path = zs3k::PATH_NONE;
+    rc = map_hip(zs3k::launch_verify_reconstruct(a, (hipStream_t)stream, &path));
+    t_last_path = path;
     return rc;
 }
 
@@ -578,7 +676,7 @@ int zs3_etag_multipart(const uint8_t* h_etags, const int64_t* offsets, const int
     if (!cat.empty()) rc = map_hip(hipMemcpy(d, cat.data(), cat.size(), hipMemcpyHostToDevice));
     if (!rc) rc = zs3_md5_batch(d, 0, (int64_t)cat.size(), nullptr, 1, d + cat.size(), nullptr);
     if (!rc) rc = map_hip(hipMemcpy(h_out, d + cat.size(), 16, hipMemcpyDeviceToHost));
-    hipFree(d);
+    (void)hipFree(d);
     if (rc) return rc;
     char suffix[24];
     const int ns = snprintf(suffix, sizeof suffix, "-%lld", (long long)count);
@@ -611,6 +709,125 @@ int zs3_hh256_verify_batch(const uint8_t* key, const uint8_t* d_msgs, int64_t st
     a.bad = d_bad;
     key_words(key, a.key);
     return map_hip(zs3k::launch_hash(a, (hipStream_t)stream));
+}
+
+int zs3_reconstruct_batch_masks(const zs3_codec* cc, uint8_t* d_shards, int64_t block_stride, int64_t shard_len,
+                                int64_t n_blocks, const uint8_t* present, int data_only, int32_t* status,
+                                void* stream) {
+    zs3_codec* c = const_cast<zs3_codec*>(cc);
+    if (!c || !present || shard_len < 0 || n_blocks < 0) return ZS3_ERR_INVALID_ARG;
+    std::vector<PatternGroup> groups;
+    const int first = group_patterns(c, present, n_blocks, data_only, status, groups);
+    if (shard_len == 0) return first ? first : (n_blocks ? ZS3_ERR_SHARD_NO_DATA : ZS3_OK);
+    hipStream_t s = (hipStream_t)stream;
+    int last = zs3k::PATH_NONE;
+    for (auto& g : groups) {
+        if (g.blocks.empty() || g.plan->noop) continue;
+        zs3k::RecArgs a{};
+        int rc = plan_device(c, g.plan.get(), &a.tables, &a.coef, &a.rows);
+        if (rc) return rc;
+        int32_t* d_ids = nullptr;
+        rc = upload_ids(g.blocks.data(), g.blocks.size(), s, &d_ids);
+        if (rc) return rc;
+        a.shards = d_shards;
+        a.block_stride = block_stride;
+        a.S = shard_len;
+        a.n_blocks = (int64_t)g.blocks.size();
+        a.k = c->k;
+        a.e = g.plan->e;
+        a.ids = d_ids;
+        a.variant = call_variant();
+        rc = map_hip(zs3k::launch_reconstruct(a, s, &last));
+        (void)hipFreeAsync(d_ids, s);
+        if (rc) return rc;
+    }
+    t_last_path = last;
+    return first;
+}
+
+int zs3_verify_reconstruct_batch_masks(const zs3_codec* cc, uint8_t* d_shards, int64_t block_stride,
+                                       int64_t shard_len, int64_t n_blocks, const uint8_t* present, int data_only,
+                                       const uint8_t* d_expect, int32_t* d_bad, uint8_t* d_sums_out,
+                                       int32_t* status, void* stream) {
+    zs3_codec* c = const_cast<zs3_codec*>(cc);
+    if (!c || !present || shard_len < 0 || n_blocks < 0) return ZS3_ERR_INVALID_ARG;
+    std::vector<PatternGroup> groups;
+    const int first = group_patterns(c, present, n_blocks, data_only, status, groups);
+    if (shard_len == 0) return first ? first : (n_blocks ? ZS3_ERR_SHARD_NO_DATA : ZS3_OK);
+    if (n_blocks == 0) return first;
+    if (!d_shards || !d_expect || !d_bad) return ZS3_ERR_INVALID_ARG;
+    hipStream_t s = (hipStream_t)stream;
+    const int R = c->k + c->m;
+    int rc = map_hip(hipMemsetAsync(d_bad, 0, (size_t)n_blocks * R * 4, s));
+    if (rc) return rc;
+    int last = zs3k::PATH_NONE;
+    for (auto& g : groups) {
+        if (g.blocks.empty()) continue;
+        zs3k::VrArgs a{};
+        rc = plan_device(c, g.plan.get(), &a.tables, &a.coef, &a.rows);
+        if (rc) return rc;
+        int32_t* d_ids = nullptr;
+        rc = upload_ids(g.blocks.data(), g.blocks.size(), s, &d_ids);
+        if (rc) return rc;
+        a.shards = d_shards;
+        a.block_stride = block_stride;
+        a.S = shard_len;
+        a.n_blocks = (int64_t)g.blocks.size();
+        a.k = c->k;
+        a.m = c->m;
+        a.e = g.plan->noop ? 0 : g.plan->e;
+        a.expect = d_expect;
+        a.bad = d_bad;
+        a.sums_out = a.e > 0 ? d_sums_out : nullptr;
+        a.ids = d_ids;
+        key_words(nullptr, a.key);
+        a.variant = call_variant();
+        rc = map_hip(zs3k::launch_verify_reconstruct(a, s, &last));
+        (void)hipFreeAsync(d_ids, s);
+        if (rc) return rc;
+    }
+    t_last_path = last;
+    return first;
+}
+
+int zs3_hh256_batch_ragged(const uint8_t* key, const uint8_t* const* d_ptrs, const int64_t* d_lens, int64_t n,
+                           uint8_t* d_sums, void* stream) {
+    if (n < 0 || (n > 0 && (!d_ptrs || !d_lens || !d_sums))) return ZS3_ERR_INVALID_ARG;
+    zs3k::HashArgs a{};
+    a.ptrs = d_ptrs;
+    a.lens = d_lens;
+    a.n = n;
+    a.sums = d_sums;
+    key_words(key, a.key);
+    return map_hip(zs3k::launch_hash(a, (hipStream_t)stream));
+}
+
+int zs3_bitrot_verify_file_batch(const uint8_t* key, const uint8_t* d_files, int64_t file_stride, int64_t n_files,
+                                 int64_t want_size, int64_t part_size, int64_t shard_size, int32_t* d_bad,
+                                 int32_t* d_file_bad, int64_t* chunks_out, void* stream) {
+    if (n_files < 0 || part_size < 0 || shard_size <= 0) return ZS3_ERR_INVALID_ARG;
+    // bitrot.go:159-162: the stream must be exactly bitrotShardFileSize(partSize, shardSize)
+    if (want_size != zs3_bitrot_shard_file_size(part_size, shard_size)) return ZS3_ERR_FILE_CORRUPT;
+    const int64_t chunks = ceil_frac(part_size, shard_size);
+    if (chunks_out) *chunks_out = chunks;
+    hipStream_t s = (hipStream_t)stream;
+    if (n_files == 0) return ZS3_OK;
+    if (chunks == 0) {
+        return d_file_bad ? map_hip(hipMemsetAsync(d_file_bad, 0, (size_t)n_files * 4, s)) : ZS3_OK;
+    }
+    if (!d_files || !d_bad || file_stride < want_size) return ZS3_ERR_INVALID_ARG;
+    zs3k::HashArgs a{};
+    a.msgs = d_files;
+    a.stride = file_stride;
+    a.n = n_files * chunks;
+    a.bad = d_bad;
+    a.chunk = shard_size;
+    a.nchunks = chunks;
+    a.last_len = part_size - (chunks - 1) * shard_size;
+    key_words(key, a.key);
+    int rc = map_hip(zs3k::launch_hash(a, s));
+    if (rc || !d_file_bad) return rc;
+    return map_hip(zs3k::launch_any_rows(d_bad, n_files, chunks, d_file_bad, s));
 }
 
 int zs3_fill_batch(uint8_t* d_out, int64_t stride, int64_t len, int64_t n, uint64_t seed, uint64_t obj0,
@@ -912,16 +1129,18 @@ int zs3_selftest(void) {
 
 int zs3_last_path(void) { return t_last_path; }
 
+#if ZS3_DIAG
 int zs3_debug_set_variant(int variant) {
     // variant >= 1000: same variant with the plain (non-dyadic) GF encode
-    g_no_dyadic = variant >= 1000;
-    zs3k::set_variant(variant % 1000);
+    t_no_dyadic = variant >= 1000;
+    t_variant = variant % 1000;
     return ZS3_OK;
 }
 
 int zs3_debug_set_buffer(void* d_dbg) {
-    g_dbg = (uint64_t*)d_dbg;
+    t_dbg = (uint64_t*)d_dbg;
     return ZS3_OK;
 }
+#endif
 
 }  // extern "C"

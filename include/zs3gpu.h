@@ -248,6 +248,20 @@ int zs3_hh256(const uint8_t* h_key, const uint8_t* h_msg, int64_t len, uint8_t* 
 int64_t zs3_stream_encode(const zs3_codec* c, const uint8_t* h_src, int64_t total_len,
                           uint8_t* h_parity, uint8_t* h_sums, int64_t batch_blocks);
 
+/* The same stream over several devices (BASELINE config 5: a multipart PUT on the 8
+ * GPUs of a node): the full blocks are split into n_devices contiguous ranges
+ * (zs3_split_range), one host thread + stream set + pinned slots per device, no data
+ * exchanged between devices; the partial last block is encoded by the last device.
+ * Outputs land at the same offsets as zs3_stream_encode's.  Pageable buffers are
+ * staged through pinned memory by helper threads that overlap the GPU work. */
+int64_t zs3_stream_encode_multi(const zs3_codec* c, const int* devices, int n_devices, const uint8_t* h_src,
+                                int64_t total_len, uint8_t* h_parity, uint8_t* h_sums, int64_t batch_blocks);
+
+/* Range [lo, hi) of `total` units owned by `rank` of `world`: contiguous, near-equal,
+ * the first total % world ranks one longer (the object / block split of the
+ * multi-GPU paths). */
+void zs3_split_range(int64_t total, int world, int rank, int64_t* lo, int64_t* hi);
+
 /* ---- cross-request batching queue (SURVEY.md §8b Threading, §7 iv) ----------------
  * The reference calls EncodeData / DecodeDataBlocks once per 1 MiB block per request
  * (cmd/erasure-encode.go:83-111, cmd/erasure-decode.go:230-276); one block is far too
@@ -257,11 +271,12 @@ int64_t zs3_stream_encode(const zs3_codec* c, const uint8_t* h_src, int64_t tota
  *   - a block is copied into the queue's pinned staging by its submitting thread;
  *   - a batch is launched when it is full, when the device has nothing in flight
  *     (batch while busy), when its oldest block has waited max_wait_us, or on flush;
- *   - zs3_req_wait blocks until the batch is done and copies this block's results
- *     back into the caller's buffers (again on the caller's thread).
+ *   - when the batch is done the queue's completion thread copies every block's
+ *     results back into its caller's buffers; zs3_req_wait blocks until that has
+ *     happened for this block.
  * All entry points are thread-safe.  Every submitted request must be waited for
- * exactly once (before zs3_queue_free).  A submit may block while every staging slot
- * is busy, until earlier requests are waited for. */
+ * exactly once, before zs3_queue_free.  A submit may block while every staging slot
+ * is in use, until a batch completes (never on other requests being waited for). */
 typedef struct zs3_queue zs3_queue;
 typedef struct zs3_req zs3_req;
 typedef struct {

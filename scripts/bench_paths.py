@@ -1,119 +1,244 @@
-"""Secondary measurements: reconstruct (BASELINE config 3),
-hash-only and verify (GET path), and the end-to-end host->device->host stream
-(config 5, PCIe-inclusive).  Prints one JSON line per measurement."""
+"""Secondary measurements: every kernel family of the path at the
+BASELINE shapes, each as one JSON line with its roofline (algorithmic HBM bytes per
+launch / median launch time, against the 8 TB/s HBM3E spec), plus the batching queue
+and the end-to-end host stream.
+
+  PATHS=encode,rec,get,hash,deep,digest,queue,e2e  python scripts/bench_paths.py
+(default: all).  Kernel-only sections (encode..digest) are what scripts/profile_paths.sh
+runs under rocprofv3; queue and e2e include host copies and PCIe.
+"""
 import json
 import os
 import sys
+import threading
 import time
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import zs3server_amd as z  # noqa: E402
 
+PEAK = 8000.0  # GB/s, MI355X HBM3E spec
+MiB = 1 << 20
+KEY = z.MAGIC_HH256_KEY
+PATHS = set(os.environ.get("PATHS", "encode,rec,get,hash,deep,digest,queue,e2e").split(","))
+REPS = int(os.environ.get("REPS", "10"))
 
-def timeit(fn, steps=10):
+
+def timeit(fn, reps=REPS):
+    """Median of `reps` launches timed with HIP events on the launch stream."""
     fn()
     torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(steps):
+    st = torch.cuda.current_stream()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for a, b in ev:
+        a.record(st)
         fn()
-    e1.record()
+        b.record(st)
     torch.cuda.synchronize()
-    return e0.elapsed_time(e1) / steps
+    ts = sorted(a.elapsed_time(b) for a, b in ev)
+    return ts[len(ts) // 2]
 
 
-def out(**kw):
-    print(json.dumps(kw), flush=True)
+def out(path, what, ms, algo_bytes, objects=None, **kw):
+    ach = algo_bytes / (ms * 1e-3) / 1e9
+    d = {"path": path, "what": what, "ms": round(ms, 4), "kernel_path": z.last_path()}
+    if objects:
+        d["objects"] = objects
+        d["GiBps_object"] = round(objects * MiB / (ms * 1e-3) / 2**30, 1)
+    d["roofline"] = {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK, "unit": "GB/s",
+                     "frac": round(ach / PEAK, 4), "algo_bytes_per_launch": int(algo_bytes)}
+    d.update(kw)
+    print(json.dumps(d), flush=True)
 
 
-# ---- config 3: RS(8+4) 4096 x 1 MiB encode, then reconstruct with 2 erased
-k, m, blen, nobj = 8, 4, 1 << 20, 4096
-S = blen // k
-stride = (k + m) * S
-codec = z.Codec(k, m)
-buf = torch.empty(nobj * stride, dtype=torch.uint8, device="cuda")
-z.fill_batch(buf, stride, blen, nobj, seed=3)
-codec.encode_batch(buf, stride, blen, nobj, parity=buf, parity_offset=k * S, parity_stride=stride)
-torch.cuda.synchronize()
-for erased, data_only, label in (([0, 5], True, "ReconstructData, data shards 0+5 erased"),
-                                 ([2, 10], False, "Reconstruct, 1 data + 1 parity erased")):
-    pres = [i not in erased for i in range(k + m)]
-    ms = timeit(lambda: codec.reconstruct_batch(buf, stride, S, nobj, pres, data_only))
-    ab = nobj * (k * S + len(erased) * S)
-    out(path="reconstruct", shape="RS(8+4)", objects=nobj, what=label, ms=round(ms, 4),
-        GiBps_object=round(nobj * blen / ms / 1e-3 / 2**30, 1), hbm_GBps=round(ab / ms / 1e6, 1),
-        hbm_frac=round(ab / ms / 1e6 / 8000, 3))
+def encoded(k, m, nobj, seed):
+    S = -(-MiB // k)
+    stride = (k + m) * S
+    codec = z.Codec(k, m)
+    buf = torch.empty(nobj * stride, dtype=torch.uint8, device="cuda")
+    sums = torch.empty(nobj * (k + m) * 32, dtype=torch.uint8, device="cuda")
+    z.fill_batch(buf, stride, MiB, nobj, seed=seed)
+    codec.encode_batch(buf, stride, MiB, nobj, parity=buf, parity_offset=k * S, parity_stride=stride, sums=sums)
+    torch.cuda.synchronize()
+    return codec, buf, sums, S, stride
 
-# ---- GET / heal fused pass (zs3_verify_reconstruct_batch): verify the k survivors
-# against stored sums and rebuild the missing shards; heal also hashes the rebuilt rows
-sums = torch.empty(nobj * (k + m) * 32, dtype=torch.uint8, device="cuda")
-codec.encode_batch(buf, stride, blen, nobj, parity=buf, parity_offset=k * S, parity_stride=stride, sums=sums)
-vbad = torch.empty(nobj * (k + m), dtype=torch.int32, device="cuda")
-hsum = torch.empty_like(sums)
-for erased, data_only, heal, label in (([], True, False, "GET, all data shards present: verify 8"),
-                                       ([0, 5], True, False, "GET, data 0+5 lost: verify 8 + rebuild 2"),
-                                       ([2, 10], False, True, "heal 1 data + 1 parity: verify 8, rebuild+hash 2")):
-    pres = [i not in erased for i in range(k + m)]
-    ms = timeit(lambda: codec.verify_reconstruct_batch(buf, stride, S, nobj, pres, data_only, sums, vbad,
-                                                       sums_out=hsum if heal else None))
-    e = len(erased)
-    ab = nobj * (k * S + e * S + 32 * k + (32 * e if heal else 0))
-    out(path="verify_reconstruct", shape="RS(8+4)", objects=nobj, what=label, ms=round(ms, 4),
-        GiBps_object=round(nobj * blen / ms / 1e-3 / 2**30, 1), hbm_GBps=round(ab / ms / 1e6, 1),
-        hbm_frac=round(ab / ms / 1e6 / 8000, 3), bad=int(vbad.sum()))
 
-# ---- GET-side hash-only and verify over all 12 shards of every stripe
-ms = timeit(lambda: z.hh256_batch(buf, S, S, nobj * (k + m), sums))
-out(path="hh256_batch", msgs=nobj * (k + m), msg_len=S, ms=round(ms, 4),
-    hbm_GBps=round(nobj * (k + m) * S / ms / 1e6, 1))
-bad = torch.empty(nobj * (k + m), dtype=torch.int32, device="cuda")
-ms = timeit(lambda: z.hh256_verify_batch(buf, S, S, nobj * (k + m), sums, bad))
-out(path="hh256_verify_batch", msgs=nobj * (k + m), msg_len=S, ms=round(ms, 4),
-    hbm_GBps=round(nobj * (k + m) * S / ms / 1e6, 1), bad=int(bad.sum()))
+# ---- encode + bitrot sums (BASELINE configs 2, 3, RS(16+4)) and encode only
+if "encode" in PATHS:
+    for k, m, nobj, label in ((4, 2, 1024, "config 2: RS(4+2) 1024 x 1 MiB"),
+                              (8, 4, 4096, "config 3: RS(8+4) 4096 x 1 MiB"),
+                              (16, 4, 2048, "RS(16+4) 2048 x 1 MiB")):
+        codec, buf, sums, S, stride = encoded(k, m, nobj, 1)
+        ms = timeit(lambda: codec.encode_batch(buf, stride, MiB, nobj, parity=buf, parity_offset=k * S,
+                                               parity_stride=stride, sums=sums))
+        out("encode_hash", label, ms, nobj * (MiB + m * S + 32 * (k + m)), objects=nobj)
+        ms = timeit(lambda: codec.encode_batch(buf, stride, MiB, nobj, parity=buf, parity_offset=k * S,
+                                               parity_stride=stride))
+        out("encode_only", label, ms, nobj * (MiB + m * S), objects=nobj)
+        del buf, sums
+        torch.cuda.empty_cache()
+
+# ---- reconstruct (ReconstructData / Reconstruct), BASELINE config 3 and RS(16+4)
+if "rec" in PATHS:
+    for k, m, nobj, cases in ((8, 4, 4096, (([0, 5], True), ([2, 10], False))),
+                              (16, 4, 2048, (([0, 5], True), ([0, 5, 9, 14], True), ([3, 17], False)))):
+        codec, buf, sums, S, stride = encoded(k, m, nobj, 3)
+        for erased, data_only in cases:
+            pres = [i not in erased for i in range(k + m)]
+            e = len([i for i in erased if i < k or not data_only])
+            ms = timeit(lambda: codec.reconstruct_batch(buf, stride, S, nobj, pres, data_only))
+            out("reconstruct", f"RS({k}+{m}) {nobj} x 1 MiB, erased {erased}, "
+                f"{'ReconstructData' if data_only else 'Reconstruct'}", ms, nobj * (k * S + e * S), objects=nobj)
+        del buf, sums
+        torch.cuda.empty_cache()
+
+# ---- GET / heal fused pass: verify the k survivors, rebuild, (heal) hash the rebuilt rows
+if "get" in PATHS:
+    for k, m, nobj, cases in (
+            (8, 4, 4096, (([], True, False), ([0, 5], True, False), ([2, 10], False, True))),
+            (4, 2, 2048, (([], True, False), ([1], True, False), ([0, 3], True, False), ([0, 5], False, True))),
+            (16, 4, 2048, (([], True, False), ([0, 5], True, False), ([0, 5, 9, 14], True, False),
+                           ([3, 17], False, True), ([0, 1, 16, 19], False, True)))):
+        codec, buf, sums, S, stride = encoded(k, m, nobj, 5)
+        R = k + m
+        vbad = torch.empty(nobj * R, dtype=torch.int32, device="cuda")
+        hsum = torch.empty_like(sums)
+        for erased, data_only, heal in cases:
+            pres = [i not in erased for i in range(R)]
+            e = len([i for i in erased if i < k or not data_only])
+            ms = timeit(lambda: codec.verify_reconstruct_batch(buf, stride, S, nobj, pres, data_only, sums, vbad,
+                                                               sums_out=hsum if heal else None))
+            what = (f"RS({k}+{m}) {nobj} x 1 MiB: verify {k}" + (f" + rebuild {e}" if e else "") +
+                    (" + hash rebuilt (heal)" if heal and e else ""))
+            out("verify_reconstruct", what, ms, nobj * (k * S + e * S + 32 * k + (32 * e if heal else 0)),
+                objects=nobj, bad=int(vbad.sum()))
+        del buf, sums, vbad, hsum
+        torch.cuda.empty_cache()
+
+# ---- hash-only / verify over all 12 shard rows of 4096 RS(8+4) stripes
+if "hash" in PATHS:
+    k, m, nobj = 8, 4, 4096
+    codec, buf, sums, S, stride = encoded(k, m, nobj, 7)
+    n = nobj * (k + m)
+    ms = timeit(lambda: z.hh256_batch(buf, S, S, n, sums))
+    out("hh256_batch", f"{n} x {S} B messages", ms, n * (S + 32))
+    bad = torch.empty(n, dtype=torch.int32, device="cuda")
+    ms = timeit(lambda: z.hh256_verify_batch(buf, S, S, n, sums, bad))
+    out("hh256_verify_batch", f"{n} x {S} B messages", ms, n * (S + 32 + 4), bad=int(bad.sum()))
+    del buf, sums, bad
+    torch.cuda.empty_cache()
+
+# ---- deep scan: bitrotVerify over whole shard files ([sum|chunk]* in place)
+if "deep" in PATHS:
+    shard, chunks, nfiles = 131072, 64, 512        # 512 RS(8+4) shard files of a 64 MiB part
+    part = shard * chunks
+    want = z.bitrot_shard_file_size(part, shard)
+    files = torch.empty(nfiles * want, dtype=torch.uint8, device="cuda")
+    z.fill_batch(files, want, want, nfiles, seed=9)
+    bad = torch.empty(nfiles * chunks, dtype=torch.int32, device="cuda")
+    fbad = torch.empty(nfiles, dtype=torch.int32, device="cuda")
+    ms = timeit(lambda: z.bitrot_verify_file_batch(files, want, nfiles, want, part, shard, bad, fbad, key=KEY))
+    out("bitrot_verify_file_batch", f"{nfiles} shard files x {chunks} chunks of {shard} B", ms,
+        nfiles * (want + 4 * chunks + 4))
+    del files, bad, fbad
+    torch.cuda.empty_cache()
+
 # ---- PUT-stream object digests: S3 ETag (MD5) and content SHA-256
-# of 4096 x 1 MiB device-resident objects, one lane per object (serial chains)
-for name, fn, width in (("md5_batch", z.md5_batch, 16), ("sha256_batch", z.sha256_batch, 32)):
-    dout = torch.empty(nobj * width, dtype=torch.uint8, device="cuda")
-    ms = timeit(lambda: fn(buf, stride, blen, nobj, dout), steps=3)
-    out(path=name, objects=nobj, object_bytes=blen, ms=round(ms, 3),
-        GiBps=round(nobj * blen / ms / 1e-3 / 2**30, 1))
-import hashlib  # noqa: E402
-sample = np.frombuffer(os.urandom(64 << 20), dtype=np.uint8)
-for name, h in (("md5_cpu_1thread", hashlib.md5), ("sha256_cpu_1thread", hashlib.sha256)):
+if "digest" in PATHS:
+    nobj = 4096
+    buf = torch.empty(nobj * MiB, dtype=torch.uint8, device="cuda")
+    z.fill_batch(buf, MiB, MiB, nobj, seed=2)
+    for name, fn, width in (("md5_batch", z.md5_batch, 16), ("sha256_batch", z.sha256_batch, 32)):
+        dout = torch.empty(nobj * width, dtype=torch.uint8, device="cuda")
+        ms = timeit(lambda: fn(buf, MiB, MiB, nobj, dout), reps=3)
+        out(name, f"{nobj} x 1 MiB objects, one lane per object", ms, nobj * (MiB + width), objects=nobj)
+    del buf
+    torch.cuda.empty_cache()
+
+
+# ---- batching queue: T concurrent submitters (goroutines in cgo), per-block latency and
+# aggregate rate, next to the reference CPU structure at the same concurrency
+def queue_run(k, m, T, per_thread, q, cpu):
+    from oracle import cpuref, oracle_c
+    R = k + m
+    S = MiB // k
+    mat = oracle_c.build_matrix(k, m)
+    bufs = [np.zeros((per_thread, R * S), np.uint8) for _ in range(T)]
+    for t in range(T):
+        bufs[t][:, :MiB] = np.frombuffer(os.urandom(MiB), np.uint8)
+    sums = [np.zeros((per_thread, R * 32), np.uint8) for _ in range(T)]
+    lat = [[] for _ in range(T)]
+
+    def work(t):
+        for i in range(per_thread):
+            t0 = time.perf_counter()
+            if cpu:
+                par = bufs[t][i, k * S:]
+                cpuref.encode_hash(k, m, mat, bufs[t][i], MiB, 1, MiB, par, m * S, sums[t][i], KEY, 1)
+            else:
+                q.encode_data(bufs[t][i], MiB)
+            lat[t].append(time.perf_counter() - t0)
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(T)]
     t0 = time.perf_counter()
-    h(sample.tobytes()).digest()
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
     dt = time.perf_counter() - t0
-    out(path=name, bytes=len(sample), GiBps=round(len(sample) / dt / 2**30, 2))
-del buf, sums, bad
-torch.cuda.empty_cache()
+    allv = sorted(v for lt in lat for v in lt)
+    return T * per_thread * MiB / dt / 2**30, allv[len(allv) // 2] * 1e6, allv[int(len(allv) * 0.99)] * 1e6
+
+
+if "queue" in PATHS:
+    from oracle import cpuref
+    k, m = 8, 4
+    codec = z.Codec(k, m)
+    q = z.Queue(codec, max_batch=128, max_wait_us=200)
+    queue_run(k, m, 4, 4, q, False)  # warm
+    for T in (1, 4, 16, 64):
+        per = 32 if T <= 16 else 16
+        b0, n0 = q.stats()
+        g, p50, p99 = queue_run(k, m, T, per, q, False)
+        b1, n1 = q.stats()
+        c, cp50, cp99 = queue_run(k, m, T, max(2, per // 4), None, True)
+        print(json.dumps({"path": "queue_encode", "what": f"RS(8+4) 1 MiB blocks, {T} concurrent submitters",
+                          "GiBps": round(g, 2), "block_latency_us_p50": round(p50, 1),
+                          "block_latency_us_p99": round(p99, 1), "blocks_per_batch": round((n1 - n0) / max(1, b1 - b0), 1),
+                          "cpu_ref_same_concurrency": {"GiBps": round(c, 2), "block_latency_us_p50": round(cp50, 1),
+                                                       "threads": T, "cores_available": cpuref.threads_available()}}),
+              flush=True)
+    q.close()
 
 # ---- config 5: end-to-end stream incl. pinned / pageable host buffers and PCIe
-gib = float(os.environ.get("E2E_GIB", "10"))
-for (k, m) in ((16, 4), (8, 4)):
-    bs = 1 << 20
-    total = int(gib * (1 << 30))
-    nblk = total // bs
-    S = bs // k
-    codec = z.Codec(k, m, bs)
-    for pinned in (True, False):
-        if pinned:
-            src, par, sums = z.HostBuffer(total), z.HostBuffer(nblk * m * S), z.HostBuffer(nblk * (k + m) * 32)
-            src.array[:] = 7
-        else:
-            src = np.full(total, 7, dtype=np.uint8)
-            par = np.zeros(nblk * m * S, np.uint8)
-            sums = np.zeros(nblk * (k + m) * 32, np.uint8)
-        codec.stream_encode(src, 64 * bs, par, sums, batch_blocks=64)  # warm
-        t0 = time.perf_counter()
-        codec.stream_encode(src, total, par, sums, batch_blocks=512)
-        dt = time.perf_counter() - t0
-        out(path="stream_encode_e2e", shape=f"RS({k}+{m})", GiB=gib, host_buffers="pinned" if pinned else "pageable",
-            seconds=round(dt, 3), GiBps=round(total / dt / 2**30, 2),
-            pcie_GBps=round((total + nblk * (m * S + 32 * (k + m))) / dt / 1e9, 1))
-        if pinned:
-            for x in (src, par, sums):
-                x.free()
-        del src, par, sums
+if "e2e" in PATHS:
+    gib = float(os.environ.get("E2E_GIB", "10"))
+    for (k, m) in ((16, 4), (8, 4)):
+        bs = MiB
+        total = int(gib * (1 << 30))
+        nblk = total // bs
+        S = bs // k
+        codec = z.Codec(k, m, bs)
+        for pinned in (True, False):
+            if pinned:
+                src, par, sums = z.HostBuffer(total), z.HostBuffer(nblk * m * S), z.HostBuffer(nblk * (k + m) * 32)
+                src.array[:] = 7
+            else:
+                src = np.full(total, 7, dtype=np.uint8)
+                par = np.zeros(nblk * m * S, np.uint8)
+                sums = np.zeros(nblk * (k + m) * 32, np.uint8)
+            codec.stream_encode(src, 64 * bs, par, sums, batch_blocks=64)  # warm
+            t0 = time.perf_counter()
+            codec.stream_encode(src, total, par, sums, batch_blocks=512)
+            dt = time.perf_counter() - t0
+            print(json.dumps({"path": "stream_encode_e2e", "what": f"RS({k}+{m}) {gib:g} GiB stream, 1 MiB blocks",
+                              "host_buffers": "pinned" if pinned else "pageable", "seconds": round(dt, 3),
+                              "GiBps": round(total / dt / 2**30, 2),
+                              "pcie_GBps": round((total + nblk * (m * S + 32 * (k + m))) / dt / 1e9, 1)}), flush=True)
+            if pinned:
+                for x in (src, par, sums):
+                    x.free()
+            del src, par, sums

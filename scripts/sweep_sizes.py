@@ -25,6 +25,10 @@ m = int(os.environ.get("M", "4"))
 sizes = [int(x) for x in os.environ.get("SIZES", "256,512,1000,1024,2047,2048,3001,4096,8192,16384").split(",")]
 variants = [int(x) for x in os.environ.get("VARIANTS", "0").split(",")]
 rounds = int(os.environ.get("ROUNDS", "3"))
+# ALIAS=1: every block reads stripe 0 and writes its parity there (data_stride =
+# parity_stride = 0): the same instruction stream with the bytes L2-resident, i.e.
+# the launch's compute-bound time (timing only; output is meaningless)
+alias = os.environ.get("ALIAS", "0") == "1"
 reps = int(os.environ.get("REPS", "10"))
 B = 1 << 20
 S = B // k
@@ -52,17 +56,19 @@ for rnd in range(rounds):
                     codecs[key] = z.Codec(k, m, B)
                 c = codecs[key]
                 st = torch.cuda.current_stream()
+                bs = 0 if alias else R * S
                 for _ in range(2):
-                    c.encode_batch(buf, R * S, B, n, parity=buf, parity_offset=k * S, parity_stride=R * S, sums=sums)
+                    c.encode_batch(buf, bs, B, n, parity=buf, parity_offset=k * S, parity_stride=bs, sums=sums)
                 ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
                 for a, b in ev:
                     a.record(st)
-                    c.encode_batch(buf, R * S, B, n, parity=buf, parity_offset=k * S, parity_stride=R * S, sums=sums)
+                    c.encode_batch(buf, bs, B, n, parity=buf, parity_offset=k * S, parity_stride=bs, sums=sums)
                     b.record(st)
                 torch.cuda.synchronize()
                 path = z.last_path()
             ts = sorted(a.elapsed_time(b) for a, b in ev)
             ms = ts[len(ts) // 2]
-            print(json.dumps({"round": rnd, "k": k, "m": m, "n": n, "variant": v, "path": path, "ms": round(ms, 4),
+            print(json.dumps({"round": rnd, "k": k, "m": m, "n": n, "variant": v, "alias": alias, "path": path,
+                              "ms": round(ms, 4),
                               "min_ms": round(ts[0], 4), "GiBps": round(n * B / ms / 1e-3 / 2**30, 1),
                               "frac": round(n * abytes / (ms * 1e-3) / 8e12, 4)}), flush=True)

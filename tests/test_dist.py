@@ -1,9 +1,15 @@
-"""world_size-2 gloo test of the multi-GPU partitioning (CPU only).
+"""world_size-2 gloo tests of the multi-GPU partitioning (CPU only).
 
-Each rank encodes + hashes its own contiguous object range with the CPU oracle
-(standing in for its GPU), rank 0 gathers the digests and checks that the union
-equals the single-process result over all objects, and the timing reduction is a
-max over ranks.  No data-path collective exists in the product path.
+* The bench's object partition: each rank encodes + hashes its own contiguous object
+  range with the CPU oracle (standing in for its GPU), rank 0 gathers the digests and
+  checks that the union equals the single-process result over all objects, and the
+  timing reduction is a max over ranks.
+* The end-to-end stream split of zs3_stream_encode_multi (BASELINE config 5): each
+  rank takes the block range the LIBRARY's own zs3_split_range gives it (the last rank
+  also the partial last block), encodes it with oracle/cpu_ref into the stream's
+  output layout (parity of block b at b*m*S, sums at b*(k+m)*32), and the gathered,
+  reassembled outputs equal the single-process encode of the whole stream.
+No data-path collective exists in the product path.
 """
 import os
 import socket
@@ -43,6 +49,74 @@ def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
+
+
+def test_library_split_matches_python_split():
+    """zs3_split_range (the C driver's split) == dist.split_range (the bench's)."""
+    import zs3server_amd as z
+    for total in (65536, 10240, 1000, 7, 1, 0):
+        for world in (1, 2, 3, 4, 7, 8):
+            for r in range(world):
+                assert z.split_range(total, world, r) == split_range(total, world, r)
+
+
+SK, SM, SBS, SNFULL, STAIL = 8, 4, 1 << 14, 37, 5000
+
+
+def _stream_input():
+    from oracle import oracle_c as oc
+    total = SNFULL * SBS + STAIL
+    return np.concatenate([oc.fill(91, b, SBS) for b in range(SNFULL + 1)])[:total]
+
+
+def _encode_range(data, lo, hi, with_tail):
+    """Blocks [lo, hi) (+ the tail) of the stream into the full-size output layout."""
+    from oracle import cpuref, oracle_c as oc
+    R, S = SK + SM, SBS // SK
+    nblk = SNFULL + 1
+    par = np.zeros(nblk * SM * S, np.uint8)
+    sums = np.zeros(nblk * R * 32, np.uint8)
+    mat = oc.build_matrix(SK, SM)
+    if hi > lo:
+        cpuref.encode_hash(SK, SM, mat, data[lo * SBS:], SBS, hi - lo, SBS, par[lo * SM * S:], SM * S,
+                           sums[lo * R * 32:], KEY, 1)
+    if with_tail:
+        sh = oc.encode_data(SK, SM, data[SNFULL * SBS:])
+        St = sh.shape[1]
+        par[SNFULL * SM * S: SNFULL * SM * S + SM * St] = sh[SK:].reshape(-1)
+        sums[SNFULL * R * 32:] = oc.hh256_rows(KEY, sh).reshape(-1)
+    return par, sums
+
+
+def _stream_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import zs3server_amd as z
+    data = _stream_input()
+    lo, hi = z.split_range(SNFULL, world, rank)
+    par, sums = _encode_range(data, lo, hi, rank == world - 1)
+    mine = torch.from_numpy(np.concatenate([par, sums]).astype(np.int32))
+    gathered = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(gathered, mine)
+    if rank == 0:
+        q.put(torch.stack(gathered).sum(dim=0).numpy().astype(np.uint8))  # disjoint ranges: sum = union
+    dist.destroy_process_group()
+
+
+def test_two_ranks_gloo_stream_split_reassembles():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_stream_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    par, sums = _encode_range(_stream_input(), 0, SNFULL, True)
+    assert np.array_equal(got, np.concatenate([par, sums]))
 
 
 def test_split_range_covers_stream():

@@ -181,3 +181,46 @@ def test_config5_full_10gib_stream(oracle):
     assert np.array_equal(par.array[(nb - 1) * m * S:].reshape(m, S), want[k:])
     for x in (src, par, sm):
         x.free()
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0]])
+@pytest.mark.parametrize("pinned", [False, True])
+def test_stream_encode_multi_device_driver(oracle, devices, pinned):
+    """zs3_stream_encode_multi: the config-5 driver with its stream split over n
+    device threads (here n threads sharing device 0: the same split, per-thread
+    streams and pinned slots, reassembly at the stream offsets); RS(16+4) 1 MiB blocks
+    with a ragged tail, every block vs cpu_ref, the tail vs the scalar oracle."""
+    k, m = 16, 4
+    R = k + m
+    S = MiB // k
+    nfull, tail, batch = 29, 12345, 4
+    total = nfull * MiB + tail
+    nblk = nfull + 1
+    codec = z.Codec(k, m, MiB)
+    dsrc = torch.empty(nblk * MiB, dtype=torch.uint8, device=DEV)
+    z.fill_batch(dsrc, MiB, MiB, nblk, seed=77, obj0=0)
+    data = dsrc.cpu().numpy()[:total]
+    bufs = []
+    if pinned:
+        src = z.HostBuffer(total)
+        src.array[:] = data
+        par = z.HostBuffer(nblk * m * S)
+        sm = z.HostBuffer(nblk * R * 32)
+        bufs = [src, par, sm]
+        par_a, sums_a = par.array, sm.array
+    else:
+        src, par_a, sums_a = data.copy(), np.zeros(nblk * m * S, np.uint8), np.zeros(nblk * R * 32, np.uint8)
+        par, sm = par_a, sums_a
+    assert codec.stream_encode_multi(devices, src, total, par, sm, batch_blocks=batch) == nblk
+    mat = oracle.build_matrix(k, m)
+    pref = np.empty(nfull * m * S, np.uint8)
+    sref = np.empty(nfull * R * 32, np.uint8)
+    cpuref.encode_hash(k, m, mat, data, MiB, nfull, MiB, pref, m * S, sref, KEY, cpuref.threads_available())
+    assert np.array_equal(par_a[:nfull * m * S], pref)
+    assert np.array_equal(sums_a[:nfull * R * 32], sref)
+    want = oracle.encode_data(k, m, data[nfull * MiB:], mat)
+    St = want.shape[1]
+    assert np.array_equal(par_a[nfull * m * S: nfull * m * S + m * St].reshape(m, St), want[k:])
+    assert np.array_equal(sums_a[nfull * R * 32:].reshape(R, 32), oracle.hh256_rows(KEY, want))
+    for x in bufs:
+        x.free()

@@ -54,6 +54,7 @@ EXPORTS = [
     "zs3_hh256_batch_ragged", "zs3_bitrot_verify_file_batch", "zs3_codec_params",
     "zs3_queue_new", "zs3_queue_free", "zs3_queue_submit_encode", "zs3_queue_submit_decode", "zs3_req_wait",
     "zs3_queue_flush", "zs3_queue_stats", "zs3_queue_encode_data", "zs3_queue_decode_data_blocks",
+    "zs3_stream_encode_multi", "zs3_split_range",
 ]
 # include/zs3gpu_diag.h: exported by the diagnostics build only
 DIAG_EXPORTS = ["zs3_debug_set_variant", "zs3_debug_set_buffer"]
@@ -166,6 +167,10 @@ def _load(path):
     L.zs3_queue_encode_data.argtypes = [vp, vp, i64, i64, vp]
     L.zs3_queue_encode_data.restype = i64
     L.zs3_queue_decode_data_blocks.argtypes = [vp, vp, i64, vp, C.c_int, vp, vp]
+    L.zs3_stream_encode_multi.argtypes = [vp, vp, C.c_int, vp, i64, vp, vp, i64]
+    L.zs3_stream_encode_multi.restype = i64
+    L.zs3_split_range.argtypes = [i64, C.c_int, C.c_int, C.POINTER(i64), C.POINTER(i64)]
+    L.zs3_split_range.restype = None
     return L
 
 
@@ -310,6 +315,16 @@ class Codec:
         n = self._L.zs3_stream_encode(self._h, addr(src), total_len, addr(parity), addr(sums), batch_blocks)
         return _check(n, "stream_encode")
 
+    def stream_encode_multi(self, devices, src, total_len: int, parity, sums, batch_blocks: int = 256) -> int:
+        """zs3_stream_encode_multi: the stream split over `devices` (one host thread,
+        stream set and pinned slots per device)."""
+        def addr(x):
+            return x.ptr if isinstance(x, HostBuffer) else x.ctypes.data
+        devs = (C.c_int * len(devices))(*devices)
+        n = self._L.zs3_stream_encode_multi(self._h, devs, len(devices), addr(src), total_len, addr(parity),
+                                            addr(sums), batch_blocks)
+        return _check(n, "stream_encode_multi")
+
     def decode_data_blocks(self, shards, present, data_only: bool) -> None:
         """Reconstruct in place on a (k+m, S) C-contiguous numpy uint8 array."""
         pres = (C.c_uint8 * (self.k + self.m))(*[1 if p else 0 for p in present])
@@ -402,6 +417,13 @@ class HostBuffer:
         if self.ptr:
             lib().zs3_host_free(self.ptr)
             self.ptr = None
+
+
+def split_range(total: int, world: int, rank: int) -> tuple[int, int]:
+    """zs3_split_range: the library's own multi-GPU split (pure host arithmetic)."""
+    lo, hi = C.c_int64(0), C.c_int64(0)
+    lib().zs3_split_range(total, world, rank, C.byref(lo), C.byref(hi))
+    return lo.value, hi.value
 
 
 def bitrot_shard_file_size(size: int, shard_size: int) -> int:

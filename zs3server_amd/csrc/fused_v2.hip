@@ -84,11 +84,39 @@ __device__ __forceinline__ void ld_async(typename VecOf<NWd>::type& dst, const u
 
 // s_waitcnt vmcnt(N), then an empty asm that "redefines" each column, so no use of a
 // column can be scheduled above the wait.
+// Non-temporal form (streamed data read once: nt cache policy).
+template <int NWd>
+__device__ __forceinline__ void ld_async_nt(typename VecOf<NWd>::type& dst, const uint8_t* p) {
+    if constexpr (NWd == 4)
+        asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(dst) : "v"(p) : "memory");
+    else if constexpr (NWd == 2)
+        asm volatile("global_load_dwordx2 %0, %1, off nt" : "=v"(dst) : "v"(p) : "memory");
+    else
+        asm volatile("global_load_dword %0, %1, off nt" : "=v"(dst) : "v"(p) : "memory");
+}
+
 template <int N, int K, typename V>
 __device__ __forceinline__ void vm_wait(V (&xs)[K]) {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 #pragma unroll
     for (int j = 0; j < K; ++j) asm volatile("" : "+v"(xs[j]));
+}
+
+// LDS hand-off counters (k_ehx_ws RING).  Signal: this wave's LDS accesses have
+// completed (lgkmcnt(0)), then one lane adds 1.  Wait: poll until the count reaches
+// `target`, sleeping between polls; the spin is bounded so that a protocol error can
+// only produce wrong output, never a wave that does not finish.
+__device__ __forceinline__ void ring_signal(uint32_t* ctr) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (__lane_id() == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void ring_wait(const uint32_t* ctr, uint32_t target) {
+    for (int spin = 0; spin < (1 << 22); ++spin) {
+        const uint32_t v = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (__builtin_amdgcn_readfirstlane(v) >= target) break;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    asm volatile("" ::: "memory");
 }
 
 template <int NWd>
@@ -420,8 +448,16 @@ constexpr int ws_cwe() {
 // plus the younger encode wave of each SIMD-sharing pair (waves w, w+4) at 2; 3 = hash
 // waves at 1.
 // CWX: encode column width override (0 = ws_cwe's default).
+// RING: the two roles hand tiles over through per-slot LDS counters instead of one
+// workgroup barrier per step (pair-form hash role only).  An encode wave waits only
+// until every hash wave has read the slot it is about to overwrite (tile s-2), a hash
+// wave only until every encode wave has written tile s; a hash wave releases the slot
+// as soon as its 12 reads have landed, before hashing them.  So the older encode wave
+// of a SIMD goes straight on to the next tile instead of idling at a barrier while its
+// younger partner finishes alone.
+// NTM (memory policy experiments): 1 = data loads non-temporal, 2 = also parity stores.
 template <int K, int M, int G, int T, int PF, bool BUF = false, bool HQ = false, bool WT = false, int PM = 0,
-          int CWX = 0>
+          int CWX = 0, bool RING = false, int NTM = 0>
 __global__ void __launch_bounds__((ws_nh<K, M, G, T, HQ>() + G * (T / ws_cwe<K, CWX>()))) __attribute__((amdgpu_waves_per_eu(3)))
 k_ehx_ws(EncArgs a) {
     constexpr int R = K + M;
@@ -438,11 +474,16 @@ k_ehx_ws(EncArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_dyn[];
     uint8_t(*tile)[G * R * TS] = reinterpret_cast<uint8_t(*)[G * R * TS]>(smem_dyn);
     __shared__ __attribute__((aligned(16))) uint32_t tabs[NTAB];
+    // RING: [0..1] encode-wave completions per slot, [2..3] hash-wave releases per slot
+    __shared__ uint32_t ring[4];
+    static_assert(!RING || !HQ, "ring hand-off: pair-form hash role");
+    constexpr uint32_t NEW = (uint32_t)(NT - NH) / 64, NHW = (uint32_t)NH / 64;
 
     const int tid = threadIdx.x;
     const int64_t blk0 = (int64_t)blockIdx.x * G;
     const int64_t S = a.S;
     for (int i = tid; i < NTAB; i += NT) tabs[i] = a.dtables[i];
+    if (RING && tid < 4) ring[tid] = 0;
     const int64_t nfull = S / T;
     const int tail = (int)(S - nfull * T);  // multiple of 16 (launch requires S % 16 == 0)
     // Step schedule shared by both roles: PF edge steps, the steady loop in units of PF
@@ -530,6 +571,36 @@ k_ehx_ws(EncArgs a) {
         const int row_off = chain * TS;
         HHPair st = hh2_init(hh, a.key[0], a.key[1], a.key[2], a.key[3]);
         bar();  // tables (matches the encode role)
+        if constexpr (RING) {
+            for (int64_t s = 0; s <= nfull; ++s) {
+                if (s == nfull && !tail) break;
+                ring_wait(&ring[s & 1], NEW * (uint32_t)((s >> 1) + 1));  // tile s written
+                if (s == nfull) {
+                    const uint8_t* row = tile[nfull & 1] + row_off;
+                    hh2_packets(st, row, tail >> 5, hh);
+                    if (tail & 31) hh2_remainder(st, row + (tail & ~31), (uint32_t)(tail & 31), hh);
+                    break;
+                }
+                const uint4* p = reinterpret_cast<const uint4*>(tile[s & 1] + row_off) + hh;
+                uint4 w[NPK];
+#pragma unroll
+                for (int i = 0; i < NPK; ++i) w[i] = p[2 * i];
+                ring_signal(&ring[2 + (s & 1)]);  // reads landed: the slot may be refilled
+#pragma unroll
+                for (int i = 0; i < NPK; ++i)
+                    hh2_update(st, ((uint64_t)w[i].y << 32) | w[i].x, ((uint64_t)w[i].w << 32) | w[i].z);
+            }
+            uint64_t d0, d1;
+            hh2_finalize256(st, d0, d1);
+            if (blk0 + chain / R < a.n_blocks) {
+                const int64_t bb = blk0 + chain / R;
+                uint64_t* out = reinterpret_cast<uint64_t*>(a.sums + (bb * R + chain % R) * 32 + 16 * hh);
+                out[0] = d0;
+                out[1] = d1;
+            }
+            stamp();
+            return;
+        }
         bar();  // step 0: tile 0 being encoded
         for (int64_t s = 1; s <= nfull; ++s) {
             const uint4* p = reinterpret_cast<const uint4*>(tile[(s - 1) & 1] + row_off) + hh;
@@ -610,6 +681,9 @@ k_ehx_ws(EncArgs a) {
     auto load = [&](VT (&xs)[K], int64_t t0) {
         if constexpr (BUF) {
             load_buf(xs, vo_d, t0);
+        } else if constexpr (NTM >= 1) {
+#pragma unroll
+            for (int j = 0; j < K; ++j) ld_async_nt<NWd>(xs[j], src + (int64_t)j * S + t0);
         } else {
 #pragma unroll
             for (int j = 0; j < K; ++j) ld_async<NWd>(xs[j], src + (int64_t)j * S + t0);
@@ -651,28 +725,38 @@ k_ehx_ws(EncArgs a) {
                     const VT v = {par[r].w[0], par[r].w[1]};
                     __builtin_amdgcn_raw_buffer_store_b64(v, rs_p, (int)vo_p, so, 0);
                 }
+            } else if constexpr (NTM >= 2) {
+                st_col_nt<NWd>(pdst + (int64_t)r * S + t0, par[r]);
             } else {
                 st_col<NWd>(pdst + (int64_t)r * S + t0, par[r]);
             }
         }
     };
+    // RING: slot of tile ti free = every hash wave has read tile ti-2 out of it
+    auto slot_free = [&](int64_t ti) {
+        if (RING && ti >= 2) ring_wait(&ring[2 + (ti & 1)], NHW * (uint32_t)(ti >> 1));
+    };
     // steady step (see k_ehx): wait for loads(ti) only
     auto step = [&](VT (&xs)[K], int64_t ti) {
         Col<NWd> par[M];
+        slot_free(ti);
         vm_wait<M + (PF - 1) * (K + M)>(xs);
         encode(xs, tile[ti & 1], par);
+        if constexpr (RING) ring_signal(&ring[ti & 1]);
         load(xs, (ti + PF) * T);
         store_par(par, ti * T);
-        bar();
+        if constexpr (!RING) bar();
     };
     auto edge = [&](VT (&xs)[K], int64_t ti) {
         const bool full = ti < nfull, part = ti == nfull && tail;
+        if (full || part) slot_free(ti);
         vm_wait<0>(xs);
         Col<NWd> par[M];
         if (full || part) encode(xs, tile[ti & 1], par);
+        if (RING && (full || part)) ring_signal(&ring[ti & 1]);
         prefetch_any(xs, ti + PF);
         if (full || (part && o < tail)) store_par(par, ti * T);
-        bar();
+        if constexpr (!RING) bar();
     };
     bar();  // tables visible
 #pragma unroll
@@ -688,14 +772,14 @@ k_ehx_ws(EncArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
     for (int p = 0; p < 2 * PF; ++p) edge(x[p % PF], i + p);
-    bar();  // the hash-only step
+    if constexpr (!RING) bar();  // the hash-only step
 #pragma unroll
     for (int p = 0; p < PF; ++p) vm_wait<0>(x[p]);
     stamp();
 }
 
 template <int K, int M, int G, int T, int PF, bool BUF = false, bool HQ = false, int LDSMIN = 0, bool WT = false,
-          int PM = 0, int CWX = 0>
+          int PM = 0, int CWX = 0, bool RING = false, int NTM = 0>
 static bool launch_ws_t(const EncArgs& a, hipStream_t s) {
     constexpr int R = K + M;
     constexpr int NT = ws_nh<K, M, G, T, HQ>() + G * (T / ws_cwe<K, CWX>());
@@ -708,7 +792,7 @@ static bool launch_ws_t(const EncArgs& a, hipStream_t s) {
         if (BUF && ((G - 1) * a.data_stride + K * a.S > 0x7FFFFFFF ||
                     (G - 1) * a.parity_stride + M * a.S > 0x7FFFFFFF || a.data_stride < 0 || a.parity_stride < 0))
             return false;
-        auto kern = k_ehx_ws<K, M, G, T, PF, BUF, HQ, WT, PM, CWX>;
+        auto kern = k_ehx_ws<K, M, G, T, PF, BUF, HQ, WT, PM, CWX, RING, NTM>;
         if (ensure_dyn_lds((const void*)kern, dyn) != hipSuccess) return false;
         const int64_t grid = (a.n_blocks + G - 1) / G;
         hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), dyn, s, a);
@@ -758,9 +842,13 @@ static bool launch_ehx_t(const EncArgs& a, hipStream_t s) {
 //           n < 2048:  PATH_NONE -> the first-generation kernel (4 stripes per
 //                      workgroup, quad-form hash lanes: more threads per stripe when
 //                      there are too few stripes to fill 256 CUs with 16 each)
-//  RS(16+4) n >= 2048: k_ehx_ws G = 8 (variant 120)
-//  RS(4+2)  n <= 1024: k_ehx_ws G = 4, quad-form hash waves (variant 111; BASELINE config 2)
-//           n <= 2048: k_ehx mixed waves, pipelined body (variant 91)
+//  RS(16+4) n >= 2048: k_ehx_ws G = 8 (variant 120: 5 pair-form hash waves + 6 encode
+//                      waves with 8-byte buffer-addressed columns)
+//           n <  2048: G = 4 with quad-form hash waves (variant 121)
+//  RS(4+2)  n <= 2048: k_ehx_ws G = 4, quad-form hash waves (variant 111; BASELINE config 2:
+//                      the hash chains' latency, not issue, sets the pace)
+//           n >  2048: k_ehx_ws G = 16, pair-form hash waves (variant 113)
+// (profiles/r02/sweep_sizes_*.txt)
 template <int K, int M>
 static int launch_ehx_default(const EncArgs& a, hipStream_t s) {
     const int64_t n = a.n_blocks;
@@ -770,10 +858,10 @@ static int launch_ehx_default(const EncArgs& a, hipStream_t s) {
         if (n >= 2048) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1>(a, s) ? PATH_WS : PATH_NONE;
     } else if constexpr (K == 16 && M == 4) {
         if (n >= 8 * 256) return launch_ws_t<K, M, 8, 384, 1, true>(a, s) ? PATH_WS : PATH_NONE;
+        return launch_ws_t<K, M, 4, 512, 1, true, true>(a, s) ? PATH_WS : PATH_NONE;
     } else if constexpr (K == 4 && M == 2) {
-        if (n <= 4 * 256) return launch_ws_t<K, M, 4, 512, 4, false, true, 83968>(a, s) ? PATH_WS : PATH_NONE;
-        if (n <= 8 * 256)
-            return launch_ehx_t<K, M, 8, 4, 2, false, 0, true, 1, false, 83968>(a, s) ? PATH_PIPE : PATH_NONE;
+        if (n <= 8 * 256) return launch_ws_t<K, M, 4, 512, 4, false, true, 83968>(a, s) ? PATH_WS : PATH_NONE;
+        return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1>(a, s) ? PATH_WS : PATH_NONE;
     }
     return PATH_NONE;
 }
@@ -814,6 +902,11 @@ static bool launch_ehx_km(int v, const EncArgs& a, hipStream_t s) {
         case 106: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 2>(a, s); else return false;
         case 107: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 3>(a, s); else return false;
         case 104: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, true>(a, s); else return false;
+        case 150: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 1>(a, s); else return false;
+        case 151: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 2>(a, s); else return false;
+        case 152: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 2, false, false, 0, false, 1>(a, s); else return false;
+        case 140: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, true>(a, s); else return false;
+        case 141: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 0, 0, true>(a, s); else return false;
         case 130: if constexpr (deep) return launch_ws_t<K, M, 8, 384, 1, false, false, 0, false, 1>(a, s); else return false;
         case 131: if constexpr (deep) return launch_ws_t<K, M, 4, 512, 2, false, true>(a, s); else return false;
         case 132: if constexpr (deep) return launch_ws_t<K, M, 2, 512, 2, false, true>(a, s); else return false;

@@ -18,9 +18,12 @@
 //                      one lets the next batch grow), when the oldest block has waited
 //                      max_wait_us, or on flush; then H2D -> kernels -> D2H on the
 //                      lane's stream, all asynchronous
-//   completer thread:  waits for each launched slot's event, marks it done
-//   zs3_req_wait:      the submitter copies its own results out of the slot (again in
-//                      parallel), the last one frees the slot for reuse
+//   completer thread:  waits for each launched slot's event, copies every block's
+//                      results back into its caller's buffers (split over helper
+//                      threads for big batches), frees the slot, wakes the waiters
+//   zs3_req_wait:      the submitter waits for its block's completion flag
+// Slot reuse never depends on a waiter, so a thread may hold any number of
+// un-waited requests.
 //
 // Lanes: ENCODE (EncodeData + the k+m bitrot sums), GET (ReconstructData of the
 // missing data shards, with the survivors' bitrot sums verified in the same pass when
@@ -32,6 +35,7 @@
 // from the back and is launched on its own.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -68,7 +72,9 @@ struct zs3_req {
     const uint8_t* h_expect = nullptr;
     int32_t* h_bad = nullptr;
     uint8_t* h_sums_out = nullptr;
-    int status = ZS3_OK;
+    int status = ZS3_OK;   // the block's status at launch (its pattern's reedsolomon error)
+    bool done = false;     // results copied out (completer)
+    int64_t result = 0;    // zs3_req_wait's return value
 };
 
 namespace {
@@ -77,11 +83,10 @@ struct Slot {
     int lane = ENC;
     uint8_t* h = nullptr;  // pinned, same layout as d
     uint8_t* d = nullptr;
-    enum State { FREE, OPEN, LAUNCHED, DONE } state = FREE;
+    enum State { FREE, OPEN, LAUNCHED } state = FREE;
     int front = 0;         // next full-size position
     int back = 0;          // short blocks placed at cap-1, cap-2, ...
     int copying = 0;       // submitters still copying in
-    int refs = 0;          // requests not yet collected by their waiter
     std::vector<zs3_req*> reqs;
     Clock::time_point opened;
     hipEvent_t done_ev = nullptr;
@@ -170,7 +175,6 @@ int reserve(zs3_queue* q, std::unique_lock<std::mutex>& lk, zs3_req* r, bool ful
             r->slot = s;
             r->pos = full ? s->front++ : q->cap - 1 - s->back++;
             s->copying++;
-            s->refs++;
             s->reqs.push_back(r);
             if (s->front + s->back == q->cap) q->cv_disp.notify_one();
             return ZS3_OK;
@@ -179,7 +183,7 @@ int reserve(zs3_queue* q, std::unique_lock<std::mutex>& lk, zs3_req* r, bool ful
             for (auto& x : q->slots[r->lane])
                 if (x.state == Slot::FREE) {
                     x.state = Slot::OPEN;
-                    x.front = x.back = x.copying = x.refs = 0;
+                    x.front = x.back = x.copying = 0;
                     x.reqs.clear();
                     x.launch_status = ZS3_OK;
                     x.opened = Clock::now();
@@ -327,6 +331,36 @@ void dispatcher(zs3_queue* q) {
     }
 }
 
+// Copy one finished block's results from the pinned slot into its caller's buffers.
+void finish_req(zs3_queue* q, Slot* s, zs3_req* r) {
+    int64_t rc = s->launch_status != ZS3_OK ? s->launch_status : r->status;
+    const size_t o = (size_t)r->pos * q->E;
+    const int k = q->k, R = q->R;
+    if (rc == ZS3_OK) {
+        if (r->lane == ENC) {
+            std::memcpy(r->h_buf + (size_t)k * r->S, s->h + o + (size_t)k * r->S, (size_t)(q->m * r->S));
+            if (k * r->S > r->len)
+                std::memset(r->h_buf + r->len, 0, (size_t)(k * r->S - r->len));  // Split zero-fill in place
+            if (r->h_sums) std::memcpy(r->h_sums, s->h + q->off_sums() + (size_t)r->pos * R * 32, (size_t)R * 32);
+            rc = r->S;
+        } else {
+            const int data_only = r->lane == GET;
+            for (int i = 0; i < R; ++i)
+                if (!r->present[i] && (i < k || !data_only))
+                    std::memcpy(r->h_shards + (size_t)i * r->S, s->h + o + (size_t)i * r->S, (size_t)r->S);
+            const int32_t* bad = (const int32_t*)(s->h + q->off_bad()) + (size_t)r->pos * R;
+            bool corrupt = false;
+            for (int i = 0; i < R; ++i) corrupt |= r->h_expect && bad[i];
+            if (r->h_bad)
+                for (int i = 0; i < R; ++i) r->h_bad[i] = r->h_expect ? bad[i] : 0;
+            if (r->h_sums_out && r->lane == HEAL)
+                std::memcpy(r->h_sums_out, s->h + q->off_out() + (size_t)r->pos * R * 32, (size_t)R * 32);
+            if (corrupt) rc = ZS3_ERR_FILE_CORRUPT;
+        }
+    }
+    r->result = rc;
+}
+
 void completer(zs3_queue* q) {
     std::unique_lock<std::mutex> lk(q->mu);
     for (;;) {
@@ -335,12 +369,29 @@ void completer(zs3_queue* q) {
         Slot* s = q->launched.front();
         q->launched.pop_front();
         lk.unlock();
-        const hipError_t e = hipEventSynchronize(s->done_ev);
+        if (hipEventSynchronize(s->done_ev) != hipSuccess && s->launch_status == ZS3_OK)
+            s->launch_status = ZS3_ERR_DEVICE;
+        // scatter the results (big batches over helper threads: one PCIe-rate stream of
+        // host copies per ~16 blocks)
+        const size_t n = s->reqs.size();
+        const size_t nt = std::min<size_t>(8, (n + 15) / 16);
+        if (nt <= 1) {
+            for (zs3_req* r : s->reqs) finish_req(q, s, r);
+        } else {
+            std::vector<std::thread> th;
+            for (size_t t = 0; t < nt; ++t)
+                th.emplace_back([=] {
+                    for (size_t i = t; i < n; i += nt) finish_req(q, s, s->reqs[i]);
+                });
+            for (auto& x : th) x.join();
+        }
         lk.lock();
-        if (e != hipSuccess && s->launch_status == ZS3_OK) s->launch_status = ZS3_ERR_DEVICE;
-        s->state = Slot::DONE;
+        for (zs3_req* r : s->reqs) r->done = true;
+        s->reqs.clear();
+        s->state = Slot::FREE;
         q->inflight[s->lane]--;
         q->cv_done.notify_all();
+        q->cv_space.notify_all();
         q->cv_disp.notify_one();  // batch-while-busy: the next open slot may go now
     }
 }
@@ -404,17 +455,6 @@ void zs3_queue_free(zs3_queue* q) {
         q->cv_comp.notify_all();
     }
     q->comp.join();
-    // outstanding requests must have been waited for by their owners; wait for any
-    // slot still referenced so their buffers outlive the copies
-    {
-        std::unique_lock<std::mutex> lk(q->mu);
-        q->cv_done.wait(lk, [&] {
-            for (auto& v : q->slots)
-                for (auto& s : v)
-                    if (s.state == Slot::LAUNCHED || (s.state == Slot::DONE && s.refs > 0)) return false;
-            return true;
-        });
-    }
     for (auto& v : q->slots)
         for (auto& s : v) {
             if (s.h) (void)hipHostFree(s.h);
@@ -501,50 +541,12 @@ int zs3_queue_submit_decode(zs3_queue* q, uint8_t* h_shards, int64_t shard_len, 
 int64_t zs3_req_wait(zs3_req* r) {
     if (!r) return ZS3_OK;  // the empty-block case returned no handle
     zs3_queue* q = r->q;
-    Slot* s = r->slot;
     {
         std::unique_lock<std::mutex> lk(q->mu);
-        if (s->state == Slot::OPEN) {
-            // a lone waiter must not sit out max_wait_us behind an idle device
-            q->cv_disp.notify_one();
-        }
-        q->cv_done.wait(lk, [&] { return s->state == Slot::DONE; });
+        if (!r->done) q->cv_disp.notify_one();  // a lone waiter: the device may be idle
+        q->cv_done.wait(lk, [&] { return r->done; });
     }
-    int64_t rc = s->launch_status != ZS3_OK ? s->launch_status : r->status;
-    const size_t o = (size_t)r->pos * q->E;
-    const int k = q->k, R = q->R;
-    if (rc == ZS3_OK) {
-        if (r->lane == ENC) {
-            std::memcpy(r->h_buf + (size_t)k * r->S, s->h + o + (size_t)k * r->S, (size_t)(q->m * r->S));
-            if (k * r->S > r->len)
-                std::memset(r->h_buf + r->len, 0, (size_t)(k * r->S - r->len));  // Split zero-fill in place
-            if (r->h_sums) std::memcpy(r->h_sums, s->h + q->off_sums() + (size_t)r->pos * R * 32, (size_t)R * 32);
-            rc = r->S;
-        } else {
-            const int data_only = r->lane == GET;
-            for (int i = 0; i < R; ++i)
-                if (!r->present[i] && (i < k || !data_only))
-                    std::memcpy(r->h_shards + (size_t)i * r->S, s->h + o + (size_t)i * r->S, (size_t)r->S);
-            const int32_t* bad = (const int32_t*)(s->h + q->off_bad()) + (size_t)r->pos * R;
-            bool corrupt = false;
-            for (int i = 0; i < R; ++i) corrupt |= r->h_expect && bad[i];
-            if (r->h_bad) {
-                for (int i = 0; i < R; ++i) r->h_bad[i] = r->h_expect ? bad[i] : 0;
-            }
-            if (r->h_sums_out && r->lane == HEAL)
-                std::memcpy(r->h_sums_out, s->h + q->off_out() + (size_t)r->pos * R * 32, (size_t)R * 32);
-            if (corrupt) rc = ZS3_ERR_FILE_CORRUPT;
-        }
-    }
-    {
-        std::lock_guard<std::mutex> g(q->mu);
-        if (--s->refs == 0) {
-            s->state = Slot::FREE;
-            s->reqs.clear();
-            q->cv_space.notify_all();
-            q->cv_done.notify_all();
-        }
-    }
+    const int64_t rc = r->result;
     delete r;
     return rc;
 }

@@ -9,7 +9,9 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
+#include <future>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -949,33 +951,35 @@ bool is_pinned(const void* p) {
 
 extern "C" {
 
-int64_t zs3_stream_encode(const zs3_codec* cc, const uint8_t* src, int64_t total_len, uint8_t* h_parity,
-                          uint8_t* h_sums, int64_t batch_blocks) {
-    zs3_codec* c = const_cast<zs3_codec*>(cc);
-    if (!c || total_len < 0 || batch_blocks <= 0 || (total_len > 0 && (!src || !h_parity || !h_sums)))
-        return ZS3_ERR_INVALID_ARG;
-    if (total_len == 0) return 0;
+}  // extern "C"
+
+namespace {
+
+// One device's share of an end-to-end stream (blocks [b0, b1) of full size B): a
+// 3-slot pipeline.  For pageable caller buffers the host copies run on helper tasks —
+// pageable -> pinned for batch i+1 while batch i is in flight, pinned -> pageable for
+// batch i once its D2H event fires — so the submitting thread only enqueues
+// H2D -> fused kernel -> D2H (three streams, cross-stream events) and never copies.
+int stream_range(zs3_codec* c, int device, const uint8_t* src, int64_t b0, int64_t b1, uint8_t* h_parity,
+                 uint8_t* h_sums, int64_t NB, bool src_pinned, bool out_pinned, int cpu_threads) {
+    if (b1 <= b0) return ZS3_OK;
+    if (hipSetDevice(device) != hipSuccess) return ZS3_ERR_DEVICE;
     const int k = c->k, m = c->m, R = k + m;
     const int64_t B = c->block_size;
     const int64_t S = ceil_frac(B, k);
-    const int64_t nfull = total_len / B;
-    const int64_t tail = total_len % B;
-    const int64_t nblocks = nfull + (tail ? 1 : 0);
     const int64_t stride = (int64_t)R * S;
-    const int64_t NB = batch_blocks;
-    const bool src_pinned = is_pinned(src);
-    const bool out_pinned = is_pinned(h_parity) && is_pinned(h_sums);
-    const int cpu_threads = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-
+    constexpr int NS = 3;
     struct Slot {
-        uint8_t* d = nullptr;      // NB stripes [k*S data | m*S parity] + sums
-        uint8_t* hin = nullptr;    // pinned input staging
-        uint8_t* hout = nullptr;   // pinned parity+sums staging
-        hipEvent_t done_out = nullptr;
-        int64_t b0 = -1, nb = 0;
+        uint8_t* d = nullptr;     // NB stripes [k*S data | m*S parity] + sums
+        uint8_t* hin = nullptr;   // pinned input staging (pageable src)
+        uint8_t* hout = nullptr;  // pinned parity+sums staging (pageable outputs)
+        hipEvent_t in_done = nullptr, out_done = nullptr;
+        bool used = false;
+        std::future<int> fill, drain;
     };
-    Slot sl[2];
-    hipStream_t s_in, s_comp, s_out;
+    Slot sl[NS];
+    hipStream_t s_in = nullptr, s_comp = nullptr, s_out = nullptr;
+    hipEvent_t ev_in = nullptr, ev_comp = nullptr;
     int rc = ZS3_OK;
     auto chk = [&](hipError_t e) {
         if (e != hipSuccess && rc == ZS3_OK) rc = map_hip(e);
@@ -984,79 +988,185 @@ int64_t zs3_stream_encode(const zs3_codec* cc, const uint8_t* src, int64_t total
     chk(hipStreamCreateWithFlags(&s_in, hipStreamNonBlocking));
     chk(hipStreamCreateWithFlags(&s_comp, hipStreamNonBlocking));
     chk(hipStreamCreateWithFlags(&s_out, hipStreamNonBlocking));
+    chk(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
+    chk(hipEventCreateWithFlags(&ev_comp, hipEventDisableTiming));
     const size_t dbytes = (size_t)NB * stride + (size_t)NB * R * 32;
     const size_t obytes = (size_t)NB * m * S + (size_t)NB * R * 32;
     for (auto& x : sl) {
         chk(hipMalloc(&x.d, dbytes));
         if (!src_pinned) chk(hipHostMalloc(&x.hin, (size_t)NB * B, hipHostMallocDefault));
         if (!out_pinned) chk(hipHostMalloc(&x.hout, obytes, hipHostMallocDefault));
-        chk(hipEventCreateWithFlags(&x.done_out, hipEventDisableTiming));
+        chk(hipEventCreateWithFlags(&x.in_done, hipEventDisableTiming));
+        chk(hipEventCreateWithFlags(&x.out_done, hipEventDisableTiming));
     }
-    // copy the finished outputs of a slot back to the caller's buffers (pageable case)
-    auto drain = [&](Slot& x) {
-        if (x.b0 < 0) return;
-        chk(hipEventSynchronize(x.done_out));
-        if (!out_pinned) {
-            par_memcpy(h_parity + x.b0 * m * S, x.hout, (size_t)x.nb * m * S, cpu_threads);
-            std::memcpy(h_sums + x.b0 * R * 32, x.hout + (size_t)NB * m * S, (size_t)x.nb * R * 32);
-        }
-        x.b0 = -1;
+    const int64_t nbatch = (b1 - b0 + NB - 1) / NB;
+    const int th = std::max(1, cpu_threads / 2);  // half for the fill side, half for the drain side
+    auto range = [&](int64_t i, int64_t& bb, int64_t& nb) {
+        bb = b0 + i * NB;
+        nb = std::min(NB, b1 - bb);
     };
-    hipEvent_t ev_in, ev_comp;
-    chk(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
-    chk(hipEventCreateWithFlags(&ev_comp, hipEventDisableTiming));
-    for (int64_t b0 = 0, it = 0; b0 < nfull && rc == ZS3_OK; b0 += NB, ++it) {
-        Slot& x = sl[it & 1];
-        drain(x);  // slot reuse: its previous batch must be out
-        const int64_t nb = std::min(NB, nfull - b0);
-        const uint8_t* in = src + b0 * B;
+    auto start_fill = [&](int64_t i) {
+        Slot& x = sl[i % NS];
+        int64_t bb, nb;
+        range(i, bb, nb);
+        const bool wait_prev = x.used;
+        hipEvent_t prev = x.in_done;
+        uint8_t* hin = x.hin;
+        x.fill = std::async(std::launch::async, [=]() -> int {
+            // the slot's previous H2D must have read hin before it is refilled
+            if (wait_prev && hipEventSynchronize(prev) != hipSuccess) return ZS3_ERR_DEVICE;
+            par_memcpy(hin, src + bb * B, (size_t)nb * B, th);
+            return ZS3_OK;
+        });
+    };
+    if (!src_pinned && rc == ZS3_OK) start_fill(0);
+    for (int64_t i = 0; i < nbatch && rc == ZS3_OK; ++i) {
+        Slot& x = sl[i % NS];
+        int64_t bb, nb;
+        range(i, bb, nb);
+        if (x.drain.valid()) {  // the slot's previous outputs are back in the caller's buffers
+            const int e = x.drain.get();
+            if (e && rc == ZS3_OK) rc = e;
+        }
+        const uint8_t* in = src + bb * B;
         if (!src_pinned) {
-            par_memcpy(x.hin, in, (size_t)nb * B, cpu_threads);
+            const int e = x.fill.get();
+            if (e && rc == ZS3_OK) rc = e;
             in = x.hin;
         }
-        // H2D into the in-place stripe layout (row pitch (k+m)*S)
+        if (rc) break;
+        if (!src_pinned && i + 1 < nbatch) {
+            Slot& y = sl[(i + 1) % NS];
+            if (y.drain.valid()) {
+                const int e = y.drain.get();
+                if (e && rc == ZS3_OK) rc = e;
+            }
+            start_fill(i + 1);
+        }
+        // the previous use of x.d (its D2H) must be done before the H2D overwrites it
+        if (x.used) chk(hipStreamWaitEvent(s_in, x.out_done, 0));
         chk(hipMemcpy2DAsync(x.d, (size_t)stride, in, (size_t)B, (size_t)B, (size_t)nb, hipMemcpyHostToDevice, s_in));
+        chk(hipEventRecord(x.in_done, s_in));
         chk(hipEventRecord(ev_in, s_in));
         chk(hipStreamWaitEvent(s_comp, ev_in, 0));
         uint8_t* dsums = x.d + (size_t)NB * stride;
-        rc = zs3_encode_batch(c, x.d, stride, B, nb, x.d + (size_t)k * S, stride, dsums, s_comp);
+        const int e = zs3_encode_batch(c, x.d, stride, B, nb, x.d + (size_t)k * S, stride, dsums, s_comp);
+        if (e && rc == ZS3_OK) rc = e;
         chk(hipEventRecord(ev_comp, s_comp));
         chk(hipStreamWaitEvent(s_out, ev_comp, 0));
-        uint8_t* po = out_pinned ? h_parity + b0 * m * S : x.hout;
-        uint8_t* so = out_pinned ? h_sums + b0 * R * 32 : x.hout + (size_t)NB * m * S;
+        uint8_t* po = out_pinned ? h_parity + bb * m * S : x.hout;
+        uint8_t* so = out_pinned ? h_sums + bb * R * 32 : x.hout + (size_t)NB * m * S;
         chk(hipMemcpy2DAsync(po, (size_t)m * S, x.d + (size_t)k * S, (size_t)stride, (size_t)m * S, (size_t)nb,
                              hipMemcpyDeviceToHost, s_out));
         chk(hipMemcpyAsync(so, dsums, (size_t)nb * R * 32, hipMemcpyDeviceToHost, s_out));
-        chk(hipEventRecord(x.done_out, s_out));
-        x.b0 = b0;
-        x.nb = nb;
-    }
-    for (auto& x : sl) drain(x);
-    if (rc == ZS3_OK && tail) {
-        // last partial block: EncodeData on its own shard size (erasure-encode.go:85-96)
-        std::vector<uint8_t> buf((size_t)R * ceil_frac(tail, k), 0);
-        std::memcpy(buf.data(), src + nfull * B, (size_t)tail);
-        uint8_t sums[32 * 256];
-        const int64_t St = zs3_encode_data(c, buf.data(), tail, (int64_t)buf.size(), sums);
-        if (St < 0) {
-            rc = (int)St;
-        } else {
-            std::memcpy(h_parity + nfull * m * S, buf.data() + (size_t)k * St, (size_t)m * St);
-            std::memcpy(h_sums + nfull * R * 32, sums, (size_t)R * 32);
+        chk(hipEventRecord(x.out_done, s_out));
+        x.used = true;
+        if (!out_pinned) {
+            hipEvent_t done = x.out_done;
+            uint8_t* hout = x.hout;
+            x.drain = std::async(std::launch::async, [=]() -> int {
+                if (hipEventSynchronize(done) != hipSuccess) return ZS3_ERR_DEVICE;
+                par_memcpy(h_parity + bb * m * S, hout, (size_t)nb * m * S, th);
+                std::memcpy(h_sums + bb * R * 32, hout + (size_t)NB * m * S, (size_t)nb * R * 32);
+                return ZS3_OK;
+            });
         }
     }
+    for (auto& x : sl) {
+        if (x.fill.valid()) (void)x.fill.get();
+        if (x.drain.valid()) {
+            const int e = x.drain.get();
+            if (e && rc == ZS3_OK) rc = e;
+        }
+    }
+    chk(hipStreamSynchronize(s_out));
     for (auto& x : sl) {
         if (x.d) (void)hipFree(x.d);
         if (x.hin) (void)hipHostFree(x.hin);
         if (x.hout) (void)hipHostFree(x.hout);
-        if (x.done_out) (void)hipEventDestroy(x.done_out);
+        if (x.in_done) (void)hipEventDestroy(x.in_done);
+        if (x.out_done) (void)hipEventDestroy(x.out_done);
     }
-    (void)hipEventDestroy(ev_in);
-    (void)hipEventDestroy(ev_comp);
-    (void)hipStreamDestroy(s_in);
-    (void)hipStreamDestroy(s_comp);
-    (void)hipStreamDestroy(s_out);
-    return rc == ZS3_OK ? nblocks : rc;
+    if (ev_in) (void)hipEventDestroy(ev_in);
+    if (ev_comp) (void)hipEventDestroy(ev_comp);
+    if (s_in) (void)hipStreamDestroy(s_in);
+    if (s_comp) (void)hipStreamDestroy(s_comp);
+    if (s_out) (void)hipStreamDestroy(s_out);
+    return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+void zs3_split_range(int64_t total, int world, int rank, int64_t* lo, int64_t* hi) {
+    // contiguous near-equal ranges, the first total % world ranks one longer
+    // (zs3server_amd/dist.py split_range)
+    if (world <= 0 || rank < 0 || rank >= world || total < 0) {
+        if (lo) *lo = 0;
+        if (hi) *hi = 0;
+        return;
+    }
+    const int64_t base = total / world, extra = total % world;
+    const int64_t l = (int64_t)rank * base + std::min<int64_t>(rank, extra);
+    if (lo) *lo = l;
+    if (hi) *hi = l + base + (rank < extra ? 1 : 0);
+}
+
+int64_t zs3_stream_encode_multi(const zs3_codec* cc, const int* devices, int n_devices, const uint8_t* src,
+                                int64_t total_len, uint8_t* h_parity, uint8_t* h_sums, int64_t batch_blocks) {
+    zs3_codec* c = const_cast<zs3_codec*>(cc);
+    if (!c || total_len < 0 || batch_blocks <= 0 || n_devices <= 0 || !devices ||
+        (total_len > 0 && (!src || !h_parity || !h_sums)))
+        return ZS3_ERR_INVALID_ARG;
+    if (total_len == 0) return 0;
+    const int k = c->k, m = c->m, R = k + m;
+    const int64_t B = c->block_size;
+    const int64_t S = ceil_frac(B, k);
+    const int64_t nfull = total_len / B;
+    const int64_t tail = total_len % B;
+    const int64_t nblocks = nfull + (tail ? 1 : 0);
+    const bool src_pinned = is_pinned(src);
+    const bool out_pinned = is_pinned(h_parity) && is_pinned(h_sums);
+    const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
+    const int cpu_threads = std::max(2, std::min(16, hw / n_devices));
+    int caller_dev = 0;
+    (void)hipGetDevice(&caller_dev);
+    std::vector<int> rcs((size_t)n_devices, ZS3_OK);
+    std::vector<std::thread> th;
+    for (int r = 0; r < n_devices; ++r) {
+        int64_t lo, hi;
+        zs3_split_range(nfull, n_devices, r, &lo, &hi);
+        th.emplace_back([&, r, lo, hi] {
+            rcs[(size_t)r] = stream_range(c, devices[r], src, lo, hi, h_parity, h_sums, batch_blocks, src_pinned,
+                                          out_pinned, cpu_threads);
+            if (r == n_devices - 1 && tail && rcs[(size_t)r] == ZS3_OK) {
+                // last partial block: EncodeData on its own shard size (erasure-encode.go:85-96)
+                std::vector<uint8_t> buf((size_t)R * ceil_frac(tail, k), 0);
+                std::memcpy(buf.data(), src + nfull * B, (size_t)tail);
+                uint8_t sums[32 * 256];
+                const int64_t St = zs3_encode_data(c, buf.data(), tail, (int64_t)buf.size(), sums);
+                if (St < 0) {
+                    rcs[(size_t)r] = (int)St;
+                } else {
+                    std::memcpy(h_parity + nfull * m * S, buf.data() + (size_t)k * St, (size_t)m * St);
+                    std::memcpy(h_sums + nfull * R * 32, sums, (size_t)R * 32);
+                }
+            }
+        });
+    }
+    for (auto& t : th) t.join();
+    (void)hipSetDevice(caller_dev);
+    for (int e : rcs)
+        if (e) return e;
+    return nblocks;
+}
+
+int64_t zs3_stream_encode(const zs3_codec* c, const uint8_t* src, int64_t total_len, uint8_t* h_parity,
+                          uint8_t* h_sums, int64_t batch_blocks) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return ZS3_ERR_DEVICE;
+    return zs3_stream_encode_multi(c, &dev, 1, src, total_len, h_parity, h_sums, batch_blocks);
 }
 
 int zs3_selftest(void) {

@@ -66,16 +66,25 @@ def test_verify_reconstruct(oracle, k, m, blen, erased, data_only, heal, variant
 # tile edges (no full tile, one tile, ragged tails) and dead stripes of the 16-stripe
 # workgroup
 WS_CASES = [(8, 4, 1 << 16, []), (8, 4, 1 << 16, [0, 5]), (8, 4, 1 << 16, [3, 9]), (8, 4, 8 * 48, [2, 11]),
-            (8, 4, 8 * 256, [1, 4]), (8, 4, 8 * (256 * 3 + 16), [0, 7]), (8, 4, 8 * (256 * 2 + 48), [])]
+            (8, 4, 8 * 256, [1, 4]), (8, 4, 8 * (256 * 3 + 16), [0, 7]), (8, 4, 8 * (256 * 2 + 48), []),
+            (8, 4, 1 << 16, [6]), (8, 4, 8 * (256 * 3 + 16), [2]), (8, 4, 1 << 16, [0, 5, 6]),
+            (8, 4, 8 * (256 * 2 + 48), [1, 2, 3]), (8, 4, 1 << 16, [1, 2, 5, 7]), (8, 4, 8 * 48, [0, 3, 4, 7]),
+            (8, 4, 1 << 16, [4, 9])]
 
 
 @pytest.mark.parametrize("k,m,blen,erased", WS_CASES)
 @pytest.mark.parametrize("data_only", [True, False])
 @pytest.mark.parametrize("heal", [False, True])
-@pytest.mark.parametrize("variant", [210, 211, 212, 213])
+@pytest.mark.parametrize("variant", [0, 210, 211, 212, 213, 216, 218])
 def test_verify_reconstruct_ws(oracle, k, m, blen, erased, data_only, heal, variant):
+    """Variant 0: the product dispatch, asserted to run k_vr_ws for every RS(8+4) GET
+    with 0-4 rebuilt rows and every heal with 2 (zs3_last_path)."""
+    e = len([i for i in erased if i < k or not data_only])
+    want = None
+    if variant == 0:
+        want = 2  # heals with e != 2: k_vr_ws rebuild + the hash kernel over the rebuilt rows
     with variant_ctx(variant):
-        run_verify_case(oracle, k, m, blen, erased, data_only, heal, nb=17)
+        run_verify_case(oracle, k, m, blen, erased, data_only, heal, nb=17, want_path=want)
 
 
 WS4_CASES = [(4, 2, 1 << 16, []), (4, 2, 1 << 16, [1]), (4, 2, 1 << 16, [0, 5]), (4, 2, 4 * 48, [2, 3]),
@@ -101,12 +110,12 @@ WS16_HEAL_CASES = [(16, 4, 1 << 16, [0, 5]), (16, 4, 1 << 16, [3, 17]), (16, 4, 
 @pytest.mark.parametrize("k,m,blen,erased", WS16_HEAL_CASES)
 @pytest.mark.parametrize("variant", [0, 215])
 def test_heal_ws_rs164(oracle, k, m, blen, erased, variant):
-    """RS(16+4) heal (rebuild 2 or 4 shards and hash them): the default (first-
-    generation kernel) and k_vr_ws with quad-form hash waves (diagnostics variant 215,
-    asserted to have run): tile edges, ragged tails and dead stripes of the 8-stripe
-    workgroup."""
+    """RS(16+4) heal (rebuild 2 or 4 shards and hash them): the default (k_vr_ws GET
+    rebuild, then the hash kernel over the rebuilt rows) and the fused k_vr_ws with
+    quad-form hash waves (diagnostics variant 215), both asserted to have run: tile
+    edges, ragged tails and dead stripes of the 8-stripe workgroup."""
     with variant_ctx(variant):
-        run_verify_case(oracle, k, m, blen, erased, False, True, nb=11, want_path=2 if variant == 215 else None)
+        run_verify_case(oracle, k, m, blen, erased, False, True, nb=11, want_path=2)
 
 
 # RS(16+4) GET on the default k_vr_ws (8-byte rebuild columns, e = 2 and e = 4): tile
@@ -114,14 +123,18 @@ def test_heal_ws_rs164(oracle, k, m, blen, erased, variant):
 WS16_GET_CASES = [(16, 4, blen, erased, data_only)
                   for blen in (1 << 16, 16 * 48, 16 * (256 * 3 + 16), 16 * (256 * 2 + 48))
                   for erased, data_only in (([0, 5], True), ([4, 15], True), ([3, 17], False),
-                                            ([0, 1, 16, 19], False), ([2, 7, 9, 12], True))]
+                                            ([0, 1, 16, 19], False), ([2, 7, 9, 12], True), ([6], True),
+                                            ([1, 7, 15], True), ([5, 18], True), ([0, 13, 16], False))]
 
 
 @pytest.mark.parametrize("k,m,blen,erased,data_only", WS16_GET_CASES)
-def test_verify_reconstruct_ws_rs164(oracle, k, m, blen, erased, data_only):
-    """The RS(16+4) rebuild-2 / rebuild-4 defaults run the warp-specialised kernel
-    (asserted through zs3_last_path) and are bit-exact vs the oracle."""
-    run_verify_case(oracle, k, m, blen, erased, data_only, False, nb=11, want_path=2)
+@pytest.mark.parametrize("variant", [0, 216])
+def test_verify_reconstruct_ws_rs164(oracle, k, m, blen, erased, data_only, variant):
+    """The RS(16+4) rebuild-1..4 defaults run the warp-specialised kernel (asserted
+    through zs3_last_path) and are bit-exact vs the oracle; 216 = the rebuild role
+    with scalar (SGPR) coefficient tables."""
+    with variant_ctx(variant):
+        run_verify_case(oracle, k, m, blen, erased, data_only, False, nb=11, want_path=2)
 
 
 def run_verify_case(oracle, k, m, blen, erased, data_only, heal, nb=3, want_path=None):

@@ -455,9 +455,10 @@ constexpr int ws_cwe() {
 // as soon as its 12 reads have landed, before hashing them.  So the older encode wave
 // of a SIMD goes straight on to the next tile instead of idling at a barrier while its
 // younger partner finishes alone.
-// NTM (memory policy experiments): 1 = data loads non-temporal, 2 = also parity stores.
+// NTM (memory policy, bit mask): 1 = data loads non-temporal, 2 = parity stores non-temporal.
+// STB: encode role reads the coefficient tables with scalar loads (SGPRs) instead of LDS.
 template <int K, int M, int G, int T, int PF, bool BUF = false, bool HQ = false, bool WT = false, int PM = 0,
-          int CWX = 0, bool RING = false, int NTM = 0>
+          int CWX = 0, bool RING = false, int NTM = 0, bool STB = false>
 __global__ void __launch_bounds__((ws_nh<K, M, G, T, HQ>() + G * (T / ws_cwe<K, CWX>()))) __attribute__((amdgpu_waves_per_eu(3)))
 k_ehx_ws(EncArgs a) {
     constexpr int R = K + M;
@@ -666,8 +667,18 @@ k_ehx_ws(EncArgs a) {
 #pragma unroll
         for (int j = 0; j < K; ++j) {
             const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)(j * S + t0u));
-            if constexpr (NWd == 4)
+            if constexpr (NWd == 4 && (NTM & 1))
+                asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen nt"
+                             : "=v"(xs[j])
+                             : "v"(vo), "s"(rs_d), "s"(so)
+                             : "memory");
+            else if constexpr (NWd == 4)
                 asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen"
+                             : "=v"(xs[j])
+                             : "v"(vo), "s"(rs_d), "s"(so)
+                             : "memory");
+            else if constexpr (NTM & 1)
+                asm volatile("buffer_load_dwordx2 %0, %1, %2, %3 offen nt"
                              : "=v"(xs[j])
                              : "v"(vo), "s"(rs_d), "s"(so)
                              : "memory");
@@ -681,7 +692,7 @@ k_ehx_ws(EncArgs a) {
     auto load = [&](VT (&xs)[K], int64_t t0) {
         if constexpr (BUF) {
             load_buf(xs, vo_d, t0);
-        } else if constexpr (NTM >= 1) {
+        } else if constexpr ((NTM & 1) != 0) {
 #pragma unroll
             for (int j = 0; j < K; ++j) ld_async_nt<NWd>(xs[j], src + (int64_t)j * S + t0);
         } else {
@@ -706,7 +717,7 @@ k_ehx_ws(EncArgs a) {
             __builtin_amdgcn_sched_barrier(0);
             __builtin_amdgcn_s_setprio(K / M >= 3 ? 0 : 1);
         } else {
-            encode_dyadic<NWd, K, M>(xs, par, tabs);
+            encode_dyadic<NWd, K, M, true, false, STB>(xs, par, tabs, const_tables(a.dtables));
         }
 #pragma unroll
         for (int j = 0; j < K; ++j) st_col<NWd>(tl + col_off + j * TS, xs[j]);
@@ -718,14 +729,15 @@ k_ehx_ws(EncArgs a) {
         for (int r = 0; r < M; ++r) {
             if constexpr (BUF) {
                 const int so = (int)__builtin_amdgcn_readfirstlane((uint32_t)(r * S + t0));
+                constexpr int aux = (NTM & 2) ? 2 : 0;  // cache policy: 2 = nt (gfx940 family)
                 if constexpr (NWd == 4) {
                     const VT v = {par[r].w[0], par[r].w[1], par[r].w[2], par[r].w[3]};
-                    __builtin_amdgcn_raw_buffer_store_b128(v, rs_p, (int)vo_p, so, 0);
+                    __builtin_amdgcn_raw_buffer_store_b128(v, rs_p, (int)vo_p, so, aux);
                 } else {
                     const VT v = {par[r].w[0], par[r].w[1]};
-                    __builtin_amdgcn_raw_buffer_store_b64(v, rs_p, (int)vo_p, so, 0);
+                    __builtin_amdgcn_raw_buffer_store_b64(v, rs_p, (int)vo_p, so, aux);
                 }
-            } else if constexpr (NTM >= 2) {
+            } else if constexpr ((NTM & 2) != 0) {
                 st_col_nt<NWd>(pdst + (int64_t)r * S + t0, par[r]);
             } else {
                 st_col<NWd>(pdst + (int64_t)r * S + t0, par[r]);
@@ -779,7 +791,7 @@ k_ehx_ws(EncArgs a) {
 }
 
 template <int K, int M, int G, int T, int PF, bool BUF = false, bool HQ = false, int LDSMIN = 0, bool WT = false,
-          int PM = 0, int CWX = 0, bool RING = false, int NTM = 0>
+          int PM = 0, int CWX = 0, bool RING = false, int NTM = 0, bool STB = false>
 static bool launch_ws_t(const EncArgs& a, hipStream_t s) {
     constexpr int R = K + M;
     constexpr int NT = ws_nh<K, M, G, T, HQ>() + G * (T / ws_cwe<K, CWX>());
@@ -792,7 +804,7 @@ static bool launch_ws_t(const EncArgs& a, hipStream_t s) {
         if (BUF && ((G - 1) * a.data_stride + K * a.S > 0x7FFFFFFF ||
                     (G - 1) * a.parity_stride + M * a.S > 0x7FFFFFFF || a.data_stride < 0 || a.parity_stride < 0))
             return false;
-        auto kern = k_ehx_ws<K, M, G, T, PF, BUF, HQ, WT, PM, CWX, RING, NTM>;
+        auto kern = k_ehx_ws<K, M, G, T, PF, BUF, HQ, WT, PM, CWX, RING, NTM, STB>;
         if (ensure_dyn_lds((const void*)kern, dyn) != hipSuccess) return false;
         const int64_t grid = (a.n_blocks + G - 1) / G;
         hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), dyn, s, a);
@@ -831,37 +843,39 @@ static bool launch_ehx_t(const EncArgs& a, hipStream_t s) {
 // registers of in-flight loads).
 //
 // Product defaults (variant 0), by shape and batch size n (scripts/sweep_sizes.py,
-// profiles/r02/sweep_sizes_rs84.txt: the fastest launch at each n, so throughput grows
-// monotonically with the batch):
-//  RS(8+4)  n >= 4096: k_ehx_ws G = 16 (variant 105: 6 pair-form hash waves + 6 encode
-//                      waves with 16-byte columns, encode waves at s_setprio 1; one
-//                      workgroup of 12 waves per CU)
+// profiles/r02/sweep_sizes_*.txt: the fastest launch at each n, so throughput grows
+// monotonically with the batch).  Data loads and parity stores of the 16-stripe
+// kernels carry the non-temporal cache policy (NTM = 3: each byte is touched once;
+// +2-3 % over the default policy at 4096-65536 stripes, profiles/r02/sweep_sizes_nt*.txt).
+//  RS(8+4)  n >= 2048: k_ehx_ws G = 16 (variant 151: 6 pair-form hash waves + 6 encode
+//                      waves with 16-byte columns, encode waves at s_setprio 1, nt policy;
+//                      one workgroup of 12 waves per CU)
 //           2048 <= n <= 2304: G = 8 (variant 130: 256-288 workgroups, one per CU)
-//           2304 < n < 4096: G = 16 again (a G = 8 grid of 289-511 workgroups doubles
-//                      up on some CUs and runs slower than 145-255 G = 16 workgroups)
 //           n < 2048:  PATH_NONE -> the first-generation kernel (4 stripes per
 //                      workgroup, quad-form hash lanes: more threads per stripe when
 //                      there are too few stripes to fill 256 CUs with 16 each)
-//  RS(16+4) n >= 2048: k_ehx_ws G = 8 (variant 120: 5 pair-form hash waves + 6 encode
-//                      waves with 8-byte buffer-addressed columns)
+//  RS(16+4) n >= 2048: k_ehx_ws G = 8 (variant 122: 5 pair-form hash waves + 6 encode
+//                      waves with 8-byte buffer-addressed columns, nt policy)
 //           n <  2048: G = 4 with quad-form hash waves (variant 121)
-//  RS(4+2)  n <= 2048: k_ehx_ws G = 4, quad-form hash waves (variant 111; BASELINE config 2:
-//                      the hash chains' latency, not issue, sets the pace)
-//           n >  2048: k_ehx_ws G = 16, pair-form hash waves (variant 113)
-// (profiles/r02/sweep_sizes_*.txt)
+//  RS(4+2)  n <= 2048: k_ehx_ws G = 4, quad-form hash waves, nt stores (variant 116;
+//                      BASELINE config 2: the hash chains' latency sets the pace)
+//           n >  2048: k_ehx_ws G = 16, pair-form hash waves, nt policy (variant 115)
 template <int K, int M>
 static int launch_ehx_default(const EncArgs& a, hipStream_t s) {
     const int64_t n = a.n_blocks;
     if constexpr (K == 8 && M == 4) {
         if (n >= 2048 && n <= 2304)
             return launch_ws_t<K, M, 8, 384, 1, false, false, 0, false, 1>(a, s) ? PATH_WS : PATH_NONE;
-        if (n >= 2048) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1>(a, s) ? PATH_WS : PATH_NONE;
+        if (n >= 2048)
+            return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3>(a, s) ? PATH_WS : PATH_NONE;
     } else if constexpr (K == 16 && M == 4) {
-        if (n >= 8 * 256) return launch_ws_t<K, M, 8, 384, 1, true>(a, s) ? PATH_WS : PATH_NONE;
+        if (n >= 8 * 256)
+            return launch_ws_t<K, M, 8, 384, 1, true, false, 0, false, 0, 0, false, 3>(a, s) ? PATH_WS : PATH_NONE;
         return launch_ws_t<K, M, 4, 512, 1, true, true>(a, s) ? PATH_WS : PATH_NONE;
     } else if constexpr (K == 4 && M == 2) {
-        if (n <= 8 * 256) return launch_ws_t<K, M, 4, 512, 4, false, true, 83968>(a, s) ? PATH_WS : PATH_NONE;
-        return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1>(a, s) ? PATH_WS : PATH_NONE;
+        if (n <= 8 * 256)
+            return launch_ws_t<K, M, 4, 512, 4, false, true, 83968, false, 0, 0, false, 2>(a, s) ? PATH_WS : PATH_NONE;
+        return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3>(a, s) ? PATH_WS : PATH_NONE;
     }
     return PATH_NONE;
 }
@@ -903,7 +917,10 @@ static bool launch_ehx_km(int v, const EncArgs& a, hipStream_t s) {
         case 107: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 3>(a, s); else return false;
         case 104: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, true>(a, s); else return false;
         case 150: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 1>(a, s); else return false;
-        case 151: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 2>(a, s); else return false;
+        case 151: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3>(a, s); else return false;
+        case 155: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, true>(a, s); else return false;
+        case 153: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 2>(a, s); else return false;
+        case 154: if constexpr (deep) return launch_ws_t<K, M, 8, 384, 1, false, false, 0, false, 1, 0, false, 2>(a, s); else return false;
         case 152: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 2, false, false, 0, false, 1>(a, s); else return false;
         case 140: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, true>(a, s); else return false;
         case 141: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 0, 0, true>(a, s); else return false;
@@ -911,11 +928,17 @@ static bool launch_ehx_km(int v, const EncArgs& a, hipStream_t s) {
         case 131: if constexpr (deep) return launch_ws_t<K, M, 4, 512, 2, false, true>(a, s); else return false;
         case 132: if constexpr (deep) return launch_ws_t<K, M, 2, 512, 2, false, true>(a, s); else return false;
         case 120: if constexpr (K == 16 && M == 4) return launch_ws_t<K, M, 8, 384, 1, true>(a, s); else return false;
+        case 122: if constexpr (K == 16 && M == 4) return launch_ws_t<K, M, 8, 384, 1, true, false, 0, false, 0, 0, false, 3>(a, s); else return false;
+        case 123: if constexpr (K == 16 && M == 4) return launch_ws_t<K, M, 8, 384, 1, true, false, 0, false, 0, 0, false, 2>(a, s); else return false;
+        case 124: if constexpr (K == 16 && M == 4) return launch_ws_t<K, M, 4, 512, 1, true, true, 0, false, 0, 0, false, 3>(a, s); else return false;
         case 121: if constexpr (K == 16 && M == 4) return launch_ws_t<K, M, 4, 512, 1, true, true>(a, s); else return false;
         case 110: if constexpr (few) return launch_ws_t<K, M, 4, 512, 2, false, true, 83968>(a, s); else return false;
         case 111: if constexpr (few) return launch_ws_t<K, M, 4, 512, 4, false, true, 83968>(a, s); else return false;
         case 112: if constexpr (few) return launch_ws_t<K, M, 4, 256, 4, false, true, 83968>(a, s); else return false;
         case 113: if constexpr (few) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1>(a, s); else return false;
+        case 114: if constexpr (few) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 2>(a, s); else return false;
+        case 115: if constexpr (few) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3>(a, s); else return false;
+        case 116: if constexpr (few) return launch_ws_t<K, M, 4, 512, 4, false, true, 83968, false, 0, 0, false, 2>(a, s); else return false;
         case 61: if constexpr (deep) return launch_ehx_t<K, M, 8, 1, 2, false, 1>(a, s); else return false;
         case 64: if constexpr (deep) return launch_ehx_t<K, M, 8, 2, 2, false, 1>(a, s); else return false;
         default: return false;
@@ -940,7 +963,10 @@ constexpr int vr_nh() {
 
 // HQ: quad-form hash waves (one HH lane per thread; pad quads hash a real row and
 // discard the digest) for chain-latency-bound shapes (few chains per CU, e.g. RS(4+2)).
-template <int K, int EX, bool HOUT, int G, int T, int PF, int CW = 16, bool HQ = false>
+// ST: the rebuild role reads its coefficient tables with scalar loads (SGPRs) instead of
+// from LDS (gf_dev.hpp load_coef_s): rebuilding e rows from k survivors needs e*k
+// tables per column, which from LDS is ~10x the column's own bytes for RS(16+4), e = 4.
+template <int K, int EX, bool HOUT, int G, int T, int PF, int CW = 16, bool HQ = false, bool ST = false>
 __global__ void __launch_bounds__((vr_nh<G, K + (HOUT ? EX : 0), HQ>() + G * (T / CW))) __attribute__((amdgpu_waves_per_eu(2)))
 k_vr_ws(VrArgs a) {
     constexpr int RH = K + (HOUT ? EX : 0);
@@ -1096,6 +1122,9 @@ k_vr_ws(VrArgs a) {
         for (int j = 0; j < K; ++j) xs[j] = to_col<NWd>(xr[j]);
         if constexpr (EX > 0) {
             const uint32_t* tb = tabs + opaque_zero();
+            // opaque offset: the tables are reloaded per tile (scalar cache hits), not
+            // hoisted out of the tile loop into e*k*5 SGPRs
+            const ctab_ptr tg = const_tables(a.tables) + opaque_zero();
 #pragma unroll
             for (int r = 0; r < EX; ++r) {
                 GfAcc acc[NWd];
@@ -1103,9 +1132,15 @@ k_vr_ws(VrArgs a) {
                 for (int w = 0; w < NWd; ++w) acc_init(acc[w]);
 #pragma unroll
                 for (int j = 0; j < K; ++j) {
-                    const CoefTab t = load_coef(tb, r * K + j);
+                    if constexpr (ST) {
+                        const CoefTab t = load_coef_s(tg, r * K + j);
 #pragma unroll
-                    for (int w = 0; w < NWd; ++w) acc_add(acc[w], gf_lookup(split_nibbles(xs[j].w[w]), t));
+                        for (int w = 0; w < NWd; ++w) acc_add(acc[w], gf_lookup_s(split_nibbles(xs[j].w[w]), t));
+                    } else {
+                        const CoefTab t = load_coef(tb, r * K + j);
+#pragma unroll
+                        for (int w = 0; w < NWd; ++w) acc_add(acc[w], gf_lookup(split_nibbles(xs[j].w[w]), t));
+                    }
                 }
 #pragma unroll
                 for (int w = 0; w < NWd; ++w) y[r].w[w] = acc_done(acc[w]);
@@ -1160,7 +1195,7 @@ k_vr_ws(VrArgs a) {
     for (int p = 0; p < PF; ++p) vm_wait<0>(x[p]);
 }
 
-template <int K, int EX, bool HOUT, int G, int T, int PF, int CW = 16, bool HQ = false>
+template <int K, int EX, bool HOUT, int G, int T, int PF, int CW = 16, bool HQ = false, bool ST = false>
 static bool launch_vr_ws_t(const VrArgs& a, hipStream_t s) {
     constexpr int RH = K + (HOUT ? EX : 0);
     constexpr int NT = vr_nh<G, RH, HQ>() + G * (T / CW);
@@ -1171,7 +1206,7 @@ static bool launch_vr_ws_t(const VrArgs& a, hipStream_t s) {
         return false;
     } else {
         if (a.e != EX || (a.S % 16) != 0 || a.k != K || (HOUT != (a.sums_out != nullptr) && EX > 0)) return false;
-        auto kern = k_vr_ws<K, EX, HOUT, G, T, PF, CW, HQ>;
+        auto kern = k_vr_ws<K, EX, HOUT, G, T, PF, CW, HQ, ST>;
         if (ensure_dyn_lds((const void*)kern, dyn) != hipSuccess) return false;
         const int64_t grid = (a.n_blocks + G - 1) / G;
         hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), dyn, s, a);
@@ -1206,7 +1241,7 @@ bool launch_vr_ws(int v, const VrArgs& a, hipStream_t s) {
         return false;
     }
 #endif
-    if (a.k == 16 && (v == 0 || v == 210 || v == 215)) {
+    if (a.k == 16 && (v == 0 || v == 210 || v == 215 || v == 216)) {
         // RS(16+4)-shaped GET: 8 stripes, 256-byte tiles; rebuilds with 8-byte columns
         // (16-byte columns spill: 16 survivors x 2 tiles beside 32-64 generic products).
         if (a.sums_out != nullptr) {
@@ -1224,6 +1259,19 @@ bool launch_vr_ws(int v, const VrArgs& a, hipStream_t s) {
             return false;
         }
         if (v == 215) return false;
+        if (v == 0) {
+            if (a.e == 1) return launch_vr_ws_t<16, 1, false, 8, 256, 1, 8>(a, s);
+            if (a.e == 3) return launch_vr_ws_t<16, 3, false, 8, 256, 1, 8>(a, s);
+        }
+#if ZS3_DIAG
+        if (v == 216) {  // scalar coefficient tables in the rebuild role
+            if (a.e == 1) return launch_vr_ws_t<16, 1, false, 8, 256, 1, 8, false, true>(a, s);
+            if (a.e == 3) return launch_vr_ws_t<16, 3, false, 8, 256, 1, 8, false, true>(a, s);
+            if (a.e == 2) return launch_vr_ws_t<16, 2, false, 8, 256, 1, 8, false, true>(a, s);
+            if (a.e == 4) return launch_vr_ws_t<16, 4, false, 8, 256, 1, 8, false, true>(a, s);
+            return false;
+        }
+#endif
         if (a.e == 0) return launch_vr_ws_t<16, 0, false, 8, 256, 2>(a, s);
         if (a.e == 2) return launch_vr_ws_t<16, 2, false, 8, 256, 1, 8>(a, s);
         if (a.e == 4) return launch_vr_ws_t<16, 4, false, 8, 256, 1, 8>(a, s);
@@ -1233,8 +1281,13 @@ bool launch_vr_ws(int v, const VrArgs& a, hipStream_t s) {
     if (a.sums_out != nullptr) {
         // heal (10 hashed rows): 8-byte rebuild columns and 128-byte tiles keep the
         // 9-wave workgroup inside 168 VGPRs (1.50 -> 1.25 ms, 1 data + 1 parity)
+        // (scalar coefficient tables, variant 216: 1.28 -> 1.18 ms on 4096 x 1 MiB,
+        // profiles/r02/get_ab.txt)
         if (a.e != 2) return false;
-        if (v == 0 || v == 212) return launch_vr_ws_t<8, 2, true, 16, 128, 2, 8>(a, s);
+        if (v == 0 || v == 216) return launch_vr_ws_t<8, 2, true, 16, 128, 2, 8, false, true>(a, s);
+#if ZS3_DIAG
+        if (v == 212) return launch_vr_ws_t<8, 2, true, 16, 128, 2, 8>(a, s);
+#endif
 #if ZS3_DIAG
         if (v == 213) return launch_vr_ws_t<8, 2, true, 16, 256, 1, 8>(a, s);
 #endif
@@ -1244,12 +1297,21 @@ bool launch_vr_ws(int v, const VrArgs& a, hipStream_t s) {
         case 0:
         case 210:
             if (a.e == 0) return launch_vr_ws_t<8, 0, false, 16, 256, 2>(a, s);
+            if (a.e == 1) return launch_vr_ws_t<8, 1, false, 16, 256, 2>(a, s);
             if (a.e == 2) return launch_vr_ws_t<8, 2, false, 16, 256, 2>(a, s);
+            if (a.e == 3) return launch_vr_ws_t<8, 3, false, 16, 256, 1>(a, s);
+            if (a.e == 4) return launch_vr_ws_t<8, 4, false, 16, 256, 1>(a, s);
             return false;
 #if ZS3_DIAG
         case 211:
             if (a.e == 0) return launch_vr_ws_t<8, 0, false, 16, 256, 1>(a, s);
             if (a.e == 2) return launch_vr_ws_t<8, 2, false, 16, 256, 1>(a, s);
+            return false;
+        case 216:
+            if (a.e == 1) return launch_vr_ws_t<8, 1, false, 16, 256, 2, 16, false, true>(a, s);
+            if (a.e == 2) return launch_vr_ws_t<8, 2, false, 16, 256, 2, 16, false, true>(a, s);
+            if (a.e == 3) return launch_vr_ws_t<8, 3, false, 16, 256, 1, 16, false, true>(a, s);
+            if (a.e == 4) return launch_vr_ws_t<8, 4, false, 16, 256, 1, 16, false, true>(a, s);
             return false;
 #endif
         default:

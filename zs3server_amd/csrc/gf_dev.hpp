@@ -48,6 +48,26 @@ __device__ __forceinline__ CoefTab load_coef(const uint32_t* lds_tab, int idx) {
     return t;
 }
 
+// Coefficient tables read with SCALAR loads: the plan / codec tables are uniform across
+// the wave, so a constant-address-space pointer with compile-time offsets compiles to
+// s_load and the tables live in SGPRs instead of being re-read from LDS (ds_read_b128 +
+// ds_read_b32 per coefficient per column) by every lane.  gfx950 VOP3 instructions read
+// at most one SGPR (constant bus), so each v_perm takes the low table dword as its SGPR
+// operand and the high dword from a VGPR (one v_mov, shared by the column's dwords).
+typedef const __attribute__((address_space(4))) uint32_t* ctab_ptr;
+
+__device__ __forceinline__ ctab_ptr const_tables(const uint32_t* p) { return (ctab_ptr)p; }
+
+__device__ __forceinline__ CoefTab load_coef_s(ctab_ptr t, int idx) {
+    CoefTab c;
+    c.ab.x = t[8 * idx + 0];
+    c.ab.y = t[8 * idx + 1];
+    c.ab.z = t[8 * idx + 2];
+    c.ab.w = t[8 * idx + 3];
+    c.c = t[8 * idx + 4];
+    return c;
+}
+
 // The three partial products of c*x (XOR of the three = c*x).
 struct Prod3 {
     uint32_t a, b, c;
@@ -58,6 +78,16 @@ __device__ __forceinline__ Prod3 gf_lookup(const Nib& n, const CoefTab& t) {
     p.a = __builtin_amdgcn_perm(t.ab.y, t.ab.x, n.a);
     p.b = __builtin_amdgcn_perm(t.ab.w, t.ab.z, n.b);
     p.c = __builtin_amdgcn_perm(t.c, t.c, n.c);
+    return p;
+}
+
+// gf_lookup for SGPR tables: the 2-bit chunk selects bytes 0-3 only (src1), so src0 can
+// be any VGPR (the selector itself): one SGPR operand per v_perm.
+__device__ __forceinline__ Prod3 gf_lookup_s(const Nib& n, const CoefTab& t) {
+    Prod3 p;
+    p.a = __builtin_amdgcn_perm(t.ab.y, t.ab.x, n.a);
+    p.b = __builtin_amdgcn_perm(t.ab.w, t.ab.z, n.b);
+    p.c = __builtin_amdgcn_perm(n.c, t.c, n.c);
     return p;
 }
 
@@ -143,8 +173,10 @@ __device__ __forceinline__ int opaque_zero() {
 // VGPRs); without it the scheduler may interleave the encode with other work.
 // PRS: lower the wave's issue priority by one after each block (progress-equalising
 // priority, fused_v2.hip PM = 4; the caller sets the starting priority).
-template <int NWd, int K, int M, bool SB = true, bool PRS = false>
-__device__ __forceinline__ void encode_dyadic(const Col<NWd> (&x)[K], Col<NWd> (&out)[M], const uint32_t* dtabs) {
+// ST: tables by scalar loads (ctabs, SGPR operands) instead of LDS (dtabs).
+template <int NWd, int K, int M, bool SB = true, bool PRS = false, bool ST = false>
+__device__ __forceinline__ void encode_dyadic(const Col<NWd> (&x)[K], Col<NWd> (&out)[M], const uint32_t* dtabs,
+                                              ctab_ptr ctabs = nullptr) {
     static_assert(M == 2 || M == 4, "dyadic block");
     uint32_t Y[M][NWd];
 #pragma unroll
@@ -155,10 +187,16 @@ __device__ __forceinline__ void encode_dyadic(const Col<NWd> (&x)[K], Col<NWd> (
             if (q == 2) __builtin_amdgcn_s_setprio(1);
             if (q > 0) __builtin_amdgcn_sched_barrier(0);
         }
-        const uint32_t* tq = dtabs + opaque_zero() + q * M * 8;
         CoefTab t[M];
+        if constexpr (ST) {
 #pragma unroll
-        for (int i = 0; i < M; ++i) t[i] = load_coef(tq, i);
+            for (int i = 0; i < M; ++i) t[i] = load_coef_s(ctabs, q * M + i);
+        } else {
+            const uint32_t* tq = dtabs + opaque_zero() + q * M * 8;
+#pragma unroll
+            for (int i = 0; i < M; ++i) t[i] = load_coef(tq, i);
+        }
+        auto gf_lookup = [](const Nib& n, const CoefTab& c) { return ST ? gf_lookup_s(n, c) : zs3dev::gf_lookup(n, c); };
 #pragma unroll
         for (int w = 0; w < NWd; ++w) {
             if constexpr (M == 4) {

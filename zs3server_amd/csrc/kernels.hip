@@ -1289,6 +1289,27 @@ static hipError_t run_vr(const VrArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
+// HighwayHash-256 of the rebuilt rows of every block of a GET / heal batch (a heal's
+// new bitrot sums) with the standalone hash kernel, one launch per rebuilt row.
+static hipError_t hash_rebuilt_rows(const VrArgs& a, hipStream_t s) {
+    const int R = a.k + a.m;
+    for (int i = 0; i < a.e; ++i) {
+        const int row = a.h_rows[a.k + i];
+        HashArgs h{};
+        h.msgs = a.shards + (int64_t)row * a.S;
+        h.stride = a.block_stride;
+        h.len = a.S;
+        h.n = a.n_blocks;
+        h.sums = a.sums_out + (int64_t)row * 32;
+        h.sum_stride = (int64_t)R * 32;
+        h.ids = a.ids;
+        for (int q = 0; q < 4; ++q) h.key[q] = a.key[q];
+        hipError_t e = launch_hash(h, s);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
 template <int K>
 static hipError_t run_vr_k(const VrArgs& a, hipStream_t s, int* path) {
     // Default for the RS(8+4)-, RS(4+2)- and RS(16+4)-shaped GETs: the warp-specialised
@@ -1300,6 +1321,21 @@ static hipError_t run_vr_k(const VrArgs& a, hipStream_t s, int* path) {
             if (path) *path = PATH_WS;
             return hipGetLastError();
         }
+    // Heals without a fused k_vr_ws instance (RS(16+4): 16 + e hashed rows per stripe do
+    // not fit pair-form waves and the VGPR budget; RS(8+4) with e != 2): the first-
+    // generation fused kernel is VALU-starved (RS(16+4) heal 2: 0.94 ms on 2048 x
+    // 1 MiB).  Run the GET rebuild on k_vr_ws and hash only the e rebuilt rows with the
+    // standalone hash kernel: e*S extra bytes read per stripe, profiles/r02/get_ab.txt.
+    if (a.sums_out && a.e > 0 && a.h_rows && (a.variant == 0 || a.variant == 218)) {
+        VrArgs g = a;
+        g.sums_out = nullptr;
+        if (launch_vr_ws(0, g, s)) {
+            hipError_t e = hipGetLastError();
+            if (e == hipSuccess) e = hash_rebuilt_rows(a, s);
+            if (path) *path = PATH_WS;
+            return e;
+        }
+    }
     if (path) *path = PATH_FIRSTGEN;
     const bool hout = a.sums_out != nullptr;
     if (a.e == 0) return run_vr<K, 0, false>(a, s);
@@ -1327,9 +1363,12 @@ hipError_t launch_verify_reconstruct(const VrArgs& a, hipStream_t s, int* path) 
     if (path) *path = PATH_GENERIC;
     const int R = a.k + a.m;
     int32_t rows[256];
-    if (hipMemcpyAsync(rows, a.rows, (size_t)(a.k + a.e) * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess)
+    if (a.h_rows) {
+        for (int i = 0; i < a.k + a.e; ++i) rows[i] = a.h_rows[i];
+    } else if (hipMemcpyAsync(rows, a.rows, (size_t)(a.k + a.e) * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+               hipStreamSynchronize(s) != hipSuccess) {
         return hipGetLastError();
+    }
     for (int j = 0; j < a.k; ++j) {
         HashArgs h{};
         h.msgs = a.shards + (int64_t)rows[j] * a.S;

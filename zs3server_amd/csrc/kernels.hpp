@@ -108,6 +108,7 @@ struct VrArgs {
     uint64_t key[4];
     const int32_t* ids;       // optional device block-slot list
     int variant;
+    const int32_t* h_rows;    // host copy of `rows` (k survivors, then e rebuilt rows)
 };
 
 // Batched MD5 / SHA-256 (digest.hip): message i of lens[i] (or len) bytes at

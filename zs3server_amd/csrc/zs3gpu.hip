@@ -625,6 +625,7 @@ int zs3_verify_reconstruct_batch(const zs3_codec* cc, uint8_t* d_shards, int64_t
     a.expect = d_expect;
     a.bad = d_bad;
     a.sums_out = a.e > 0 ? d_sums_out : nullptr;
+    a.h_rows = plan->rows.data();
     key_words(nullptr, a.key);
     a.variant = call_variant();
     int path = zs3k::PATH_NONE;
@@ -781,6 +782,7 @@ int zs3_verify_reconstruct_batch_masks(const zs3_codec* cc, uint8_t* d_shards, i
         a.expect = d_expect;
         a.bad = d_bad;
         a.sums_out = a.e > 0 ? d_sums_out : nullptr;
+        a.h_rows = g.plan->rows.data();
         a.ids = d_ids;
         key_words(nullptr, a.key);
         a.variant = call_variant();

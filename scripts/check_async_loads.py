@@ -7,7 +7,8 @@ runs a forward dataflow over each kernel's basic blocks: the state maps every pe
 asm-load destination to its age (vector-memory ops issued after it: every global_,
 buffer_, scratch_ and flat_ op counts on vmcnt), merged by minimum age at control-flow
 joins; `s_waitcnt vmcnt(N)` retires entries of age >= N.  Any instruction other than
-another asm load touching a pending destination is reported.
+another asm load touching a pending destination is reported.  Join blocks that branch
+on a flag every predecessor sets to a constant are split per predecessor (specialize).
 
   hipcc --offload-arch=gfx950 -O3 -std=c++17 --cuda-device-only -S -o v2.s fused_v2.hip
   python scripts/check_async_loads.py v2.s [kernel-substring]
@@ -75,6 +76,72 @@ def parse_blocks(body):
     return blocks
 
 
+SREG = re.compile(r"\bs\[(\d+):(\d+)\]|\bs(\d+)\b")
+
+
+def sregs(text):
+    out = set()
+    for m in SREG.finditer(text):
+        if m.group(3) is not None:
+            out.add(int(m.group(3)))
+        else:
+            out.update(range(int(m.group(1)), int(m.group(2)) + 1))
+    return out
+
+
+def dest(code):
+    parts = code.split(None, 1)
+    return parts[1].split(",")[0].strip() if len(parts) > 1 else ""
+
+
+def const_of(insns, pair):
+    """Value the block leaves in the SGPR pair (s_mov_b64 <pair>, imm as its last write)."""
+    val = None
+    for _, code, _ in insns:
+        if pair & sregs(dest(code)):
+            m = re.match(r"s_mov_b64\s+s\[(\d+):(\d+)\],\s*(-?\d+)$", code)
+            val = int(m.group(3)) if m and set(range(int(m.group(1)), int(m.group(2)) + 1)) == pair else None
+    return val
+
+
+def specialize(blocks):
+    """Clone a join block that ends `s_and_b64 vcc, exec, s[a:b]` + `s_cbranch_vcc(n)z`
+    once per predecessor when every predecessor leaves a known constant (0 or -1) in
+    s[a:b]: each clone keeps only the successor that constant selects.  The compiler
+    emits this for 'was the loop entered' flags; without it the dataflow merges the
+    loop-exit state into a path that only the skipped-loop predecessor can take."""
+    i = 0
+    while i < len(blocks):
+        label, insns, succs = blocks[i]
+        last = insns[-1][1] if insns else ""
+        op = last.split()[0] if last else ""
+        if op in ("s_cbranch_vccz", "s_cbranch_vccnz") and len(insns) >= 2:
+            pair = None
+            for j in range(len(insns) - 2, -1, -1):
+                code = insns[j][1]
+                m = re.match(r"s_and_b64\s+vcc,\s*exec,\s*s\[(\d+):(\d+)\]$", code)
+                if m:
+                    pair = set(range(int(m.group(1)), int(m.group(2)) + 1))
+                    before = insns[:j]
+                    break
+                if "vcc" in dest(code) or code.startswith(("s_cbranch", "s_branch")):
+                    break
+            preds = [p for p, b in enumerate(blocks) if i in b[2]]
+            if pair and len(preds) > 1 and "@" not in label and not any(pair & sregs(dest(c)) for _, c, _ in before):
+                vals = [const_of(blocks[p][1], pair) for p in preds]
+                if all(v in (0, -1) for v in vals):
+                    tgt = last.split()[1]
+                    taken = [t for t in succs if blocks[t][0] == tgt]
+                    fall = [t for t in succs if blocks[t][0] != tgt]
+                    for p, v in zip(preds, vals):
+                        zero = v == 0  # vcc = exec & v; exec is non-zero on a uniform branch
+                        go = taken if (zero == (op == "s_cbranch_vccz")) else fall
+                        blocks.append([f"{label}@{p}", insns, list(go)])
+                        blocks[p][2] = [len(blocks) - 1 if t == i else t for t in blocks[p][2]]
+        i += 1
+    return blocks
+
+
 def transfer(state, insns, report, name):
     st = dict(state)
     bad = 0
@@ -107,7 +174,7 @@ def transfer(state, insns, report, name):
 
 
 def check(body, name):
-    blocks = parse_blocks(body)
+    blocks = specialize(parse_blocks(body))
     ins = [None] * len(blocks)
     ins[0] = {}
     work = [0]

@@ -1,7 +1,7 @@
 """A/B of the GET / heal launches for the RS(4+2), RS(8+4) and RS(16+4) shapes
 (variant 0 = product default dispatch; others forced through the diagnostics build,
 e.g. 200 = first-generation kernel, 216/217 = scalar coefficient tables), interleaved
-rounds.  SHAPES=4,8,16 selects the shapes."""
+rounds.  SHAPES=4,8,16 selects the shapes, CASES=heal filters the case names."""
 import contextlib
 import json
 import os
@@ -27,6 +27,7 @@ def timeit(fn, steps=10):
 
 variants = [int(v) for v in os.environ.get("VARIANTS", "0,200").split(",")]
 shapes = [int(x) for x in os.environ.get("SHAPES", "4,8,16").split(",")]
+only = os.environ.get("CASES")  # e.g. CASES=heal: substring filter on the case names
 ALL = ((4, 2, 2048, (("verify 4", [], False), ("verify + rebuild 2", [0, 3], False),
                      ("verify + rebuild 1", [1], False), ("heal 2", [1, 5], True))),
        (8, 4, 4096, (("verify 8", [], False), ("verify + rebuild 1", [3], False),
@@ -34,7 +35,8 @@ ALL = ((4, 2, 2048, (("verify 4", [], False), ("verify + rebuild 2", [0, 3], Fal
                      ("verify + rebuild 4", [1, 2, 5, 7], False), ("heal 1", [4], True), ("heal 2", [2, 10], True))),
        (16, 4, 2048, (("verify 16", [], False), ("verify + rebuild 1", [6], False), ("verify + rebuild 2", [0, 9], False),
                       ("verify + rebuild 3", [1, 7, 15], False), ("verify + rebuild 4", [1, 7, 14, 15], False),
-                      ("heal 2", [0, 17], True), ("heal 4", [1, 7, 15, 19], True))))
+                      ("heal 1", [5], True), ("heal 2", [0, 17], True), ("heal 3", [2, 11, 18], True),
+                      ("heal 4", [1, 7, 15, 19], True))))
 
 
 def ctx(v):
@@ -57,6 +59,8 @@ for k, m, nobj, cases in [c for c in ALL if c[0] in shapes]:
     out = torch.zeros_like(sums)
     for rnd in range(2):
         for name, erased, heal in cases:
+            if only and only not in name:
+                continue
             present = [i not in erased for i in range(R)]
             for v in variants:
                 c = codec if v == 0 else dcodec

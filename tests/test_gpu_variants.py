@@ -74,3 +74,49 @@ def test_rs84_variant_dead_stripes(oracle, variant, nb):
                                       (16, 4, 16 * 640 * 2), (16, 4, 1 << 20)])
 def test_other_shapes_variants(oracle, variant, k, m, blen):
     run_case(oracle, k, m, blen, 3, variant, seed=k + m)
+
+
+def test_variants_are_per_thread(oracle):
+    """The diagnostics build's variant selection is thread-local (no process-wide tuning
+    state): two threads encode concurrently with different variants — and a third on
+    the product library — and every result matches the oracle."""
+    import threading
+
+    k, m, blen, nb = 8, 4, 8 * (384 * 5 + 16), 17
+    S = -(-blen // k)
+    R = k + m
+    host = np.zeros(nb * R * S, dtype=np.uint8)
+    for b in range(nb):
+        host[b * R * S: b * R * S + blen] = oracle.fill(71, b, blen)
+    mat = oracle.build_matrix(k, m)
+    want = [oracle.encode_data(k, m, host[b * R * S: b * R * S + blen], mat) for b in range(nb)]
+    want_sums = [oracle.hh256_rows(KEY, w) for w in want]
+    errs = []
+
+    def worker(variant, reps):
+        try:
+            with variant_ctx(variant):
+                codec = z.Codec(k, m, 1 << 20)
+                stream = torch.cuda.Stream()
+                for _ in range(reps):
+                    with torch.cuda.stream(stream):
+                        d = torch.from_numpy(host).to(DEV)
+                        sums = torch.zeros(nb * R * 32, dtype=torch.uint8, device=DEV)
+                        codec.encode_batch(d, R * S, blen, nb, parity=d, parity_offset=k * S, parity_stride=R * S,
+                                           sums=sums)
+                    stream.synchronize()
+                    out = d.cpu().numpy().reshape(nb, R, S)
+                    hs = sums.cpu().numpy().reshape(nb, R, 32)
+                    for b in range(nb):
+                        assert np.array_equal(out[b], want[b]), (variant, b)
+                        assert np.array_equal(hs[b], want_sums[b]), (variant, b)
+        except BaseException as e:  # noqa: BLE001 - re-raised below
+            errs.append(e)
+
+    th = [threading.Thread(target=worker, args=(v, 20)) for v in (5, 140, 0)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    if errs:
+        raise errs[0]

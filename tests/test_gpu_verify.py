@@ -78,11 +78,12 @@ WS_CASES = [(8, 4, 1 << 16, []), (8, 4, 1 << 16, [0, 5]), (8, 4, 1 << 16, [3, 9]
 @pytest.mark.parametrize("variant", [0, 210, 211, 212, 213, 216, 218])
 def test_verify_reconstruct_ws(oracle, k, m, blen, erased, data_only, heal, variant):
     """Variant 0: the product dispatch, asserted to run k_vr_ws for every RS(8+4) GET
-    with 0-4 rebuilt rows and every heal with 2 (zs3_last_path)."""
-    e = len([i for i in erased if i < k or not data_only])
+    with 0-4 rebuilt rows and every heal of 0-2 rows (zs3_last_path); heals of 3-4 rows
+    run the first-generation kernel.  218 = split heal (GET rebuild + hash kernel)."""
+    e = len(erased) if heal else len([i for i in erased if i < k or not data_only])
     want = None
     if variant == 0:
-        want = 2  # heals with e != 2: k_vr_ws rebuild + the hash kernel over the rebuilt rows
+        want = 2 if (not heal or e <= 2) else 1
     with variant_ctx(variant):
         run_verify_case(oracle, k, m, blen, erased, data_only, heal, nb=17, want_path=want)
 
@@ -104,18 +105,24 @@ def test_verify_reconstruct_ws_rs42(oracle, k, m, blen, erased, data_only, heal,
 
 WS16_HEAL_CASES = [(16, 4, 1 << 16, [0, 5]), (16, 4, 1 << 16, [3, 17]), (16, 4, 16 * 48, [2, 19]),
                    (16, 4, 16 * (256 * 3 + 16), [0, 1, 16, 19]), (16, 4, 16 * 256, [4, 5, 6, 7]),
-                   (16, 4, 16 * (256 * 2 + 48), [15, 18])]
+                   (16, 4, 16 * (256 * 2 + 48), [15, 18]), (16, 4, 1 << 16, [7]), (16, 4, 16 * 48, [18]),
+                   (16, 4, 16 * (256 * 3 + 16), [16]), (16, 4, 16 * (256 * 2 + 48), [2, 9, 19]),
+                   (16, 4, 16 * 256, [0, 8, 17])]
 
 
 @pytest.mark.parametrize("k,m,blen,erased", WS16_HEAL_CASES)
-@pytest.mark.parametrize("variant", [0, 215])
+@pytest.mark.parametrize("variant", [0, 215, 216, 218])
 def test_heal_ws_rs164(oracle, k, m, blen, erased, variant):
-    """RS(16+4) heal (rebuild 2 or 4 shards and hash them): the default (k_vr_ws GET
-    rebuild, then the hash kernel over the rebuilt rows) and the fused k_vr_ws with
-    quad-form hash waves (diagnostics variant 215), both asserted to have run: tile
-    edges, ragged tails and dead stripes of the 8-stripe workgroup."""
+    """RS(16+4) heal (rebuild 1-4 shards and hash them) on k_vr_ws: the default for one
+    lost shard (padded pair-form hash waves), diagnostics 215 (quad-form hash waves,
+    e = 2 / 4), 216 (pair form, e = 1..4) and 218 (split: GET rebuild + hash kernel);
+    the default runs the first-generation kernel for 2-4 lost shards.  The launched
+    family is asserted: tile edges, ragged tails and dead stripes of the 8-stripe
+    workgroup."""
+    e = len(erased)
+    want = {0: 2 if e == 1 else 1, 215: 2 if e in (2, 4) else None, 216: 2, 218: 2}[variant]
     with variant_ctx(variant):
-        run_verify_case(oracle, k, m, blen, erased, False, True, nb=11, want_path=2)
+        run_verify_case(oracle, k, m, blen, erased, False, True, nb=11, want_path=want)
 
 
 # RS(16+4) GET on the default k_vr_ws (8-byte rebuild columns, e = 2 and e = 4): tile

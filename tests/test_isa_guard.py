@@ -53,3 +53,40 @@ def test_untracked_loads_never_touched_in_flight(tmp_path, diag):
     assert kernels, "no k_ehx instance found in the assembly"
     bad = {n: cal.check(b, n) for n, b in kernels}
     assert all(v == 0 for v in bad.values()), bad
+
+
+def _body(src):
+    return [(i, line) for i, line in enumerate(src.strip("\n").split("\n"), 1)]
+
+
+LOOP_FLAG = """
+	s_cbranch_scc0 .LBB0_5
+	;;#ASMSTART
+	global_load_dwordx2 v[10:11], v[2:3], off
+	;;#ASMEND
+	s_mov_b64 s[0:1], 0
+	s_branch .LBB0_6
+.LBB0_5:
+	s_waitcnt vmcnt(0)
+	s_mov_b64 s[0:1], -1
+.LBB0_6:
+	s_and_b64 vcc, exec, s[0:1]
+	s_cbranch_vccz .LBB0_8
+	v_mov_b64_e32 v[10:11], v[20:21]
+.LBB0_8:
+	s_waitcnt vmcnt(0)
+	v_mov_b64_e32 v[30:31], v[10:11]
+"""
+
+
+def test_guard_specializes_loop_entered_flag():
+    """The join block's fall-through (the mov into v[10:11]) is reachable only from the
+    predecessor that set s[0:1] = -1, where nothing is in flight: no violation.  With
+    the flag constants swapped the load path reaches the mov: reported."""
+    import check_async_loads as cal
+    assert cal.check(_body(LOOP_FLAG), "ok") == 0
+    swapped = LOOP_FLAG.replace("s_mov_b64 s[0:1], 0", "s_mov_b64 s[0:1], @").replace(
+        "s_mov_b64 s[0:1], -1", "s_mov_b64 s[0:1], 0").replace("s_mov_b64 s[0:1], @", "s_mov_b64 s[0:1], -1")
+    assert cal.check(_body(swapped), "bad") == 1
+    unknown = LOOP_FLAG.replace("s_mov_b64 s[0:1], 0", "s_mov_b64 s[0:1], s[4:5]")
+    assert cal.check(_body(unknown), "unknown") == 1

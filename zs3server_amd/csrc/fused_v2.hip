@@ -958,7 +958,8 @@ static bool launch_ehx_km(int v, const EncArgs& a, hipStream_t s) {
 // G*T/16 rebuild (16-byte columns, untracked loads PF tiles ahead, exact vmcnt waits).
 template <int G, int RH, bool HQ>
 constexpr int vr_nh() {
-    return HQ ? ((4 * G * RH + 63) / 64) * 64 : 2 * G * RH;
+    // whole wavefronts; the pad chains hash a real row and discard the digest
+    return HQ ? ((4 * G * RH + 63) / 64) * 64 : ((2 * G * RH + 63) / 64) * 64;
 }
 
 // HQ: quad-form hash waves (one HH lane per thread; pad quads hash a real row and
@@ -1041,8 +1042,11 @@ k_vr_ws(VrArgs a) {
         return;
     }
     if (!HQ && __builtin_amdgcn_readfirstlane(tid) < NH) {
-        // ---- hash role (pair form): hashed row cj of stripe g
-        const int chain = tid >> 1, hh = tid & 1;
+        // ---- hash role (pair form): hashed row cj of stripe g (pad pairs past G*RH
+        // hash row chain - G*RH again and discard the digest)
+        const int chain0 = tid >> 1, hh = tid & 1;
+        const bool pad = chain0 >= G * RH;
+        const int chain = pad ? chain0 - G * RH : chain0;
         const int g = chain / RH, cj = chain % RH;
         const int row_off = chain * TS;
         HHPair st = hh2_init(hh, a.key[0], a.key[1], a.key[2], a.key[3]);
@@ -1066,7 +1070,7 @@ k_vr_ws(VrArgs a) {
         for (int64_t s = nfull + 1; s < total; ++s) lds_barrier2();
         uint64_t d0, d1;
         hh2_finalize256(st, d0, d1);
-        const bool live = blk0 + g < a.n_blocks;
+        const bool live = !pad && blk0 + g < a.n_blocks;
         const int64_t b = live && a.ids ? (int64_t)a.ids[blk0 + g] : blk0 + g;
         const int srow = srows[cj];
         if (cj < K) {
@@ -1244,6 +1248,22 @@ bool launch_vr_ws(int v, const VrArgs& a, hipStream_t s) {
     if (a.k == 16 && (v == 0 || v == 210 || v == 215 || v == 216)) {
         // RS(16+4)-shaped GET: 8 stripes, 256-byte tiles; rebuilds with 8-byte columns
         // (16-byte columns spill: 16 survivors x 2 tiles beside 32-64 generic products).
+        if (a.sums_out != nullptr && ((v == 0 && a.e == 1) || v == 216)) {
+            // Heal (17..20 hashed rows): 8 stripes per workgroup, pair-form hash waves
+            // padded to whole waves (e.g. heal 2: 288 -> 320 threads) beside 2-4 rebuild
+            // waves with 8-byte columns; e >= 2 reads the rebuild tables with scalar loads
+            // (the VGPR copy spills).  Product default for heal 1 only: 0.535 vs 0.785 ms
+            // (first generation) on 2048 x 1 MiB; heal 2/3/4 measured 0.967/1.31/1.58 vs
+            // 0.946/1.13/1.31 ms (2 rebuild waves are the bound), diagnostics 216
+            // (profiles/r02/get_ab.txt)
+            if (a.e == 1) return launch_vr_ws_t<16, 1, true, 8, 256, 1, 8, false, false>(a, s);
+#if ZS3_DIAG
+            if (a.e == 2) return launch_vr_ws_t<16, 2, true, 8, 128, 1, 8, false, false>(a, s);
+            if (a.e == 3) return launch_vr_ws_t<16, 3, true, 8, 128, 1, 8, false, true>(a, s);
+            if (a.e == 4) return launch_vr_ws_t<16, 4, true, 8, 128, 1, 8, false, true>(a, s);
+#endif
+            return false;
+        }
         if (a.sums_out != nullptr) {
 #if ZS3_DIAG
             // Heal (18 / 20 hashed rows): 2*8*18 pair-form threads are not whole waves,
@@ -1283,6 +1303,7 @@ bool launch_vr_ws(int v, const VrArgs& a, hipStream_t s) {
         // 9-wave workgroup inside 168 VGPRs (1.50 -> 1.25 ms, 1 data + 1 parity)
         // (scalar coefficient tables, variant 216: 1.28 -> 1.18 ms on 4096 x 1 MiB,
         // profiles/r02/get_ab.txt)
+        if ((v == 0 || v == 216) && a.e == 1) return launch_vr_ws_t<8, 1, true, 16, 128, 2, 8, false, true>(a, s);
         if (a.e != 2) return false;
         if (v == 0 || v == 216) return launch_vr_ws_t<8, 2, true, 16, 128, 2, 8, false, true>(a, s);
 #if ZS3_DIAG

@@ -1321,12 +1321,11 @@ static hipError_t run_vr_k(const VrArgs& a, hipStream_t s, int* path) {
             if (path) *path = PATH_WS;
             return hipGetLastError();
         }
-    // Heals without a fused k_vr_ws instance (RS(16+4): 16 + e hashed rows per stripe do
-    // not fit pair-form waves and the VGPR budget; RS(8+4) with e != 2): the first-
-    // generation fused kernel is VALU-starved (RS(16+4) heal 2: 0.94 ms on 2048 x
-    // 1 MiB).  Run the GET rebuild on k_vr_ws and hash only the e rebuilt rows with the
-    // standalone hash kernel: e*S extra bytes read per stripe, profiles/r02/get_ab.txt.
-    if (a.sums_out && a.e > 0 && a.h_rows && (a.variant == 0 || a.variant == 218)) {
+    // Diagnostics variant 218: heal split into the k_vr_ws GET rebuild and the standalone
+    // hash kernel over the e rebuilt rows.  Measured SLOWER than the fused kernels
+    // (RS(16+4) heal 2: 1.12 vs 0.95 ms, heal 4: 1.87 vs 1.32; profiles/r02/get_ab.txt):
+    // e*n_blocks serial chains are too few to hide the hash kernel's load latency.
+    if (ZS3_DIAG && a.sums_out && a.e > 0 && a.h_rows && a.variant == 218) {
         VrArgs g = a;
         g.sums_out = nullptr;
         if (launch_vr_ws(0, g, s)) {

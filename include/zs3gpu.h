@@ -267,13 +267,14 @@ void zs3_split_range(int64_t total, int world, int rank, int64_t* lo, int64_t* h
  * (cmd/erasure-encode.go:83-111, cmd/erasure-decode.go:230-276); one block is far too
  * little work for one device round trip.  A queue gathers the blocks that concurrent
  * callers (OS threads: every goroutine inside cgo holds one) submit into device
- * batches on its own streams and pinned staging:
+ * batches on pinned staging slots, each slot with its own stream:
  *   - a block is copied into the queue's pinned staging by its submitting thread;
- *   - a batch is launched when it is full, when the device has nothing in flight
- *     (batch while busy), when its oldest block has waited max_wait_us, or on flush;
- *   - when the batch is done the queue's completion thread copies every block's
- *     results back into its caller's buffers; zs3_req_wait blocks until that has
- *     happened for this block.
+ *   - a batch is launched when it is full, when fewer than slots-1 batches of its lane
+ *     are in flight (batch while busy), when its oldest block has waited max_wait_us,
+ *     or on flush;
+ *   - when the batch is done, zs3_req_wait copies its own block's results back into
+ *     the caller's buffers on the calling thread; blocks nobody is waiting for are
+ *     copied back by the queue's completion thread.
  * All entry points are thread-safe.  Every submitted request must be waited for
  * exactly once, before zs3_queue_free.  A submit may block while every staging slot
  * is in use, until a batch completes (never on other requests being waited for). */
@@ -283,7 +284,7 @@ typedef struct {
     int device;       /* HIP device ordinal; -1 = the calling thread's current device */
     int max_batch;    /* blocks per device batch (0 = 128) */
     int max_wait_us;  /* longest a block waits for its batch to fill (0 = 200) */
-    int slots;        /* pinned staging slots per lane (0 = 3; at least 2) */
+    int slots;        /* pinned staging slots (+ streams) per lane (0 = 4; at least 2) */
 } zs3_queue_opts;
 
 int zs3_queue_new(const zs3_codec* c, const zs3_queue_opts* opts /* NULL = defaults */, zs3_queue** out);

@@ -98,17 +98,19 @@ if "rec" in PATHS:
 # ---- GET / heal fused pass: verify the k survivors, rebuild, (heal) hash the rebuilt rows
 if "get" in PATHS:
     for k, m, nobj, cases in (
-            (8, 4, 4096, (([], True, False), ([0, 5], True, False), ([2, 10], False, True))),
+            (8, 4, 4096, (([], True, False), ([3], True, False), ([0, 5], True, False), ([0, 5, 6], True, False),
+                          ([1, 2, 5, 7], True, False), ([4], False, True), ([2, 10], False, True))),
             (4, 2, 2048, (([], True, False), ([1], True, False), ([0, 3], True, False), ([0, 5], False, True))),
-            (16, 4, 2048, (([], True, False), ([0, 5], True, False), ([0, 5, 9, 14], True, False),
-                           ([3, 17], False, True), ([0, 1, 16, 19], False, True)))):
+            (16, 4, 2048, (([], True, False), ([6], True, False), ([0, 5], True, False), ([1, 7, 15], True, False),
+                           ([0, 5, 9, 14], True, False), ([5], False, True), ([3, 17], False, True),
+                           ([0, 1, 16, 19], False, True)))):
         codec, buf, sums, S, stride = encoded(k, m, nobj, 5)
         R = k + m
         vbad = torch.empty(nobj * R, dtype=torch.int32, device="cuda")
         hsum = torch.empty_like(sums)
         for erased, data_only, heal in cases:
             pres = [i not in erased for i in range(R)]
-            e = len([i for i in erased if i < k or not data_only])
+            e = len(erased) if heal else len([i for i in erased if i < k or not data_only])
             ms = timeit(lambda: codec.verify_reconstruct_batch(buf, stride, S, nobj, pres, data_only, sums, vbad,
                                                                sums_out=hsum if heal else None))
             what = (f"RS({k}+{m}) {nobj} x 1 MiB: verify {k}" + (f" + rebuild {e}" if e else "") +
@@ -199,12 +201,13 @@ if "queue" in PATHS:
     codec = z.Codec(k, m)
     q = z.Queue(codec, max_batch=128, max_wait_us=200)
     queue_run(k, m, 4, 4, q, False)  # warm
-    for T in (1, 4, 16, 64):
+    for T in [int(x) for x in os.environ.get("QUEUE_T", "1,4,16,64").split(",")]:
         per = 32 if T <= 16 else 16
         b0, n0 = q.stats()
         g, p50, p99 = queue_run(k, m, T, per, q, False)
         b1, n1 = q.stats()
-        c, cp50, cp99 = queue_run(k, m, T, max(2, per // 4), None, True)
+        c, cp50, cp99 = (queue_run(k, m, T, max(2, per // 4), None, True) if os.environ.get("QUEUE_CPU", "1") == "1"
+                         else (0.0, 0.0, 0.0))
         print(json.dumps({"path": "queue_encode", "what": f"RS(8+4) 1 MiB blocks, {T} concurrent submitters",
                           "GiBps": round(g, 2), "block_latency_us_p50": round(p50, 1),
                           "block_latency_us_p99": round(p99, 1), "blocks_per_batch": round((n1 - n0) / max(1, b1 - b0), 1),
@@ -235,6 +238,7 @@ if "e2e" in PATHS:
             codec.stream_encode(src, total, par, sums, batch_blocks=512)
             dt = time.perf_counter() - t0
             print(json.dumps({"path": "stream_encode_e2e", "what": f"RS({k}+{m}) {gib:g} GiB stream, 1 MiB blocks",
+                              "driver": "zs3_stream_encode -> zs3_stream_encode_multi, 1 device",
                               "host_buffers": "pinned" if pinned else "pageable", "seconds": round(dt, 3),
                               "GiBps": round(total / dt / 2**30, 2),
                               "pcie_GBps": round((total + nblk * (m * S + 32 * (k + m))) / dt / 1e9, 1)}), flush=True)

@@ -18,12 +18,16 @@
 //                      one lets the next batch grow), when the oldest block has waited
 //                      max_wait_us, or on flush; then H2D -> kernels -> D2H on the
 //                      lane's stream, all asynchronous
-//   completer thread:  waits for each launched slot's event, copies every block's
-//                      results back into its caller's buffers (split over helper
-//                      threads for big batches), frees the slot, wakes the waiters
-//   zs3_req_wait:      the submitter waits for its block's completion flag
-// Slot reuse never depends on a waiter, so a thread may hold any number of
-// un-waited requests.
+//   completer thread:  waits for each launched slot's event, marks the slot ready and
+//                      wakes the waiters, then copies out every block nobody claimed
+//   zs3_req_wait:      once its slot is ready the submitter claims its own block and
+//                      copies the results into its buffers itself (as each goroutine
+//                      encodes its own block in the reference), in parallel with the
+//                      other waiters; if the completer claimed it first, it waits
+// Each block is claimed exactly once (an atomic flag per slot position); whoever
+// finishes the slot's last block frees the slot.  Slot reuse never depends on a
+// waiter (the completer claims what is not being waited for), so a thread may hold any
+// number of un-waited requests.
 //
 // Lanes: ENCODE (EncodeData + the k+m bitrot sums), GET (ReconstructData of the
 // missing data shards, with the survivors' bitrot sums verified in the same pass when
@@ -41,6 +45,7 @@
 #include <condition_variable>
 #include <cstring>
 #include <deque>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -90,7 +95,11 @@ struct Slot {
     std::vector<zs3_req*> reqs;
     Clock::time_point opened;
     hipEvent_t done_ev = nullptr;
+    hipStream_t stream = nullptr;  // per slot: batches overlap each other's copies and kernels
     int launch_status = ZS3_OK;
+    bool ready = false;                          // results are in the pinned slot
+    std::unique_ptr<std::atomic<uint8_t>[]> claimed;  // [cap] block copied out by one thread
+    std::atomic<int> pending{0};                 // blocks not yet finished (+1 completer)
 };
 
 }  // namespace
@@ -102,7 +111,7 @@ struct zs3_queue {
     int device = 0;
     int cap = 128;                // positions per slot
     int max_wait_us = 200;
-    int nslots = 3;
+    int nslots = 4;
 
     std::mutex mu;
     std::condition_variable cv_space;   // a slot became free / open
@@ -117,11 +126,13 @@ struct zs3_queue {
     bool flush = false;
     bool stop = false;       // dispatcher: drain the open slots and exit
     bool comp_stop = false;  // completer: exit once every launched slot is done
-    hipStream_t stream[NLANE] = {nullptr, nullptr, nullptr};
     std::thread disp, comp;
     std::atomic<int64_t> n_batches{0}, n_blocks{0};
 
-    // region offsets inside a slot (bytes)
+    // region offsets inside a slot (bytes).  ENCODE: [cap][k*S] data rows, then
+    // [cap][m*S] parity rows (each direction one contiguous DMA copy of the bytes that
+    // cross PCIe); GET / HEAL: [cap][(k+m)*S] stripes
+    size_t off_par() const { return (size_t)cap * k * S; }                     // ENCODE parity rows
     size_t off_sums() const { return (size_t)cap * E; }                       // [cap][R][32] sums / expect
     size_t off_bad() const { return off_sums() + (size_t)cap * R * 32; }      // [cap][R] int32
     size_t off_out() const { return off_bad() + (size_t)cap * R * 4; }        // [cap][R][32] heal sums
@@ -149,12 +160,15 @@ int ensure_lane(zs3_queue* q, int lane) {
         if (rc == ZS3_OK) rc = map_hip(hipHostMalloc((void**)&s.h, bytes, hipHostMallocDefault));
         if (rc == ZS3_OK) rc = map_hip(hipMalloc((void**)&s.d, bytes));
         if (rc == ZS3_OK) rc = map_hip(hipEventCreateWithFlags(&s.done_ev, hipEventDisableTiming));
+        if (rc == ZS3_OK) rc = map_hip(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+        s.claimed.reset(new std::atomic<uint8_t>[(size_t)q->cap]);
     }
     if (rc != ZS3_OK) {
         for (auto& s : v) {
             if (s.h) (void)hipHostFree(s.h);
             if (s.d) (void)hipFree(s.d);
             if (s.done_ev) (void)hipEventDestroy(s.done_ev);
+            if (s.stream) (void)hipStreamDestroy(s.stream);
         }
         q->alloc_failed[lane] = true;
     } else {
@@ -186,6 +200,7 @@ int reserve(zs3_queue* q, std::unique_lock<std::mutex>& lk, zs3_req* r, bool ful
                     x.front = x.back = x.copying = 0;
                     x.reqs.clear();
                     x.launch_status = ZS3_OK;
+                    x.ready = false;
                     x.opened = Clock::now();
                     q->open[r->lane] = &x;
                     break;
@@ -203,7 +218,7 @@ void copy_in_done(zs3_queue* q, Slot* s) {
 
 // ---- launch of a closed slot (dispatcher thread, no lock held) ----------------------
 void launch_slot(zs3_queue* q, Slot* s) {
-    hipStream_t st = q->stream[s->lane];
+    hipStream_t st = s->stream;
     const int k = q->k, m = q->m, R = q->R;
     const int64_t E = q->E, S = q->S;
     const int nf = s->front;
@@ -215,22 +230,20 @@ void launch_slot(zs3_queue* q, Slot* s) {
     uint8_t* hsum = s->h + q->off_sums();
     if (s->lane == ENC) {
         // full-size blocks: data rows in, one fused launch, parity rows + sums out
+        const size_t KS = (size_t)k * S, MS = (size_t)m * S, po = q->off_par();
         if (nf > 0) {
-            chk(map_hip(hipMemcpy2DAsync(s->d, (size_t)E, s->h, (size_t)E, (size_t)(k * S), (size_t)nf,
-                                         hipMemcpyHostToDevice, st)));
-            chk(zs3_encode_batch(q->c, s->d, E, q->B, nf, s->d + k * S, E, dsum, st));
-            chk(map_hip(hipMemcpy2DAsync(s->h + k * S, (size_t)E, s->d + k * S, (size_t)E, (size_t)(m * S),
-                                         (size_t)nf, hipMemcpyDeviceToHost, st)));
+            chk(map_hip(hipMemcpyAsync(s->d, s->h, (size_t)nf * KS, hipMemcpyHostToDevice, st)));
+            chk(zs3_encode_batch(q->c, s->d, (int64_t)KS, q->B, nf, s->d + po, (int64_t)MS, dsum, st));
+            chk(map_hip(hipMemcpyAsync(s->h + po, s->d + po, (size_t)nf * MS, hipMemcpyDeviceToHost, st)));
             chk(map_hip(hipMemcpyAsync(hsum, dsum, (size_t)nf * R * 32, hipMemcpyDeviceToHost, st)));
         }
         for (zs3_req* r : s->reqs) {
             if (r->pos < nf) continue;
-            const size_t o = (size_t)r->pos * E;
+            const size_t o = (size_t)r->pos * KS, op = po + (size_t)r->pos * MS;
             uint8_t* sb = dsum + (size_t)r->pos * R * 32;
             chk(map_hip(hipMemcpyAsync(s->d + o, s->h + o, (size_t)(k * r->S), hipMemcpyHostToDevice, st)));
-            chk(zs3_encode_batch(q->c, s->d + o, E, r->len, 1, s->d + o + k * r->S, E, sb, st));
-            chk(map_hip(hipMemcpyAsync(s->h + o + k * r->S, s->d + o + k * r->S, (size_t)(m * r->S),
-                                       hipMemcpyDeviceToHost, st)));
+            chk(zs3_encode_batch(q->c, s->d + o, (int64_t)KS, r->len, 1, s->d + op, (int64_t)MS, sb, st));
+            chk(map_hip(hipMemcpyAsync(s->h + op, s->d + op, (size_t)(m * r->S), hipMemcpyDeviceToHost, st)));
             chk(map_hip(hipMemcpyAsync(hsum + (size_t)r->pos * R * 32, sb, (size_t)R * 32, hipMemcpyDeviceToHost, st)));
         }
     } else {
@@ -290,7 +303,11 @@ void launch_slot(zs3_queue* q, Slot* s) {
 bool ready_to_close(zs3_queue* q, Slot* s, int lane, Clock::time_point now) {
     if (s->reqs.empty()) return false;
     if (s->front + s->back == q->cap || q->flush || q->stop) return true;
-    if (q->inflight[lane] == 0) return true;  // batch while busy
+    // batch while busy: launch at once while fewer than slots-1 batches are in flight
+    // (a small batch is bound by one hash chain's latency, ~0.5 ms for 128 KiB shards,
+    // not by its bytes, so concurrent batches on their own streams overlap almost
+    // fully); otherwise let the open slot grow until one completes
+    if (q->inflight[lane] < q->nslots - 1) return true;
     return now - s->opened >= std::chrono::microseconds(q->max_wait_us);
 }
 
@@ -338,7 +355,8 @@ void finish_req(zs3_queue* q, Slot* s, zs3_req* r) {
     const int k = q->k, R = q->R;
     if (rc == ZS3_OK) {
         if (r->lane == ENC) {
-            std::memcpy(r->h_buf + (size_t)k * r->S, s->h + o + (size_t)k * r->S, (size_t)(q->m * r->S));
+            std::memcpy(r->h_buf + (size_t)k * r->S, s->h + q->off_par() + (size_t)r->pos * q->m * q->S,
+                        (size_t)(q->m * r->S));
             if (k * r->S > r->len)
                 std::memset(r->h_buf + r->len, 0, (size_t)(k * r->S - r->len));  // Split zero-fill in place
             if (r->h_sums) std::memcpy(r->h_sums, s->h + q->off_sums() + (size_t)r->pos * R * 32, (size_t)R * 32);
@@ -361,6 +379,17 @@ void finish_req(zs3_queue* q, Slot* s, zs3_req* r) {
     r->result = rc;
 }
 
+// Drop one pending block of the slot; the last one frees the slot (caller holds no lock).
+void finish_one(zs3_queue* q, Slot* s) {
+    if (s->pending.fetch_sub(1) != 1) return;
+    std::lock_guard<std::mutex> g(q->mu);
+    s->reqs.clear();
+    s->state = Slot::FREE;
+    q->inflight[s->lane]--;
+    q->cv_space.notify_all();
+    q->cv_disp.notify_one();  // batch-while-busy: the next open slot may go now
+}
+
 void completer(zs3_queue* q) {
     std::unique_lock<std::mutex> lk(q->mu);
     for (;;) {
@@ -371,28 +400,31 @@ void completer(zs3_queue* q) {
         lk.unlock();
         if (hipEventSynchronize(s->done_ev) != hipSuccess && s->launch_status == ZS3_OK)
             s->launch_status = ZS3_ERR_DEVICE;
-        // scatter the results (big batches over helper threads: one PCIe-rate stream of
-        // host copies per ~16 blocks)
         const size_t n = s->reqs.size();
-        const size_t nt = std::min<size_t>(8, (n + 15) / 16);
-        if (nt <= 1) {
-            for (zs3_req* r : s->reqs) finish_req(q, s, r);
-        } else {
-            std::vector<std::thread> th;
-            for (size_t t = 0; t < nt; ++t)
-                th.emplace_back([=] {
-                    for (size_t i = t; i < n; i += nt) finish_req(q, s, s->reqs[i]);
-                });
-            for (auto& x : th) x.join();
+        std::vector<int> pos(n);  // read before any waiter can finish (and delete) its request
+        for (size_t i = 0; i < n; ++i) pos[i] = s->reqs[i]->pos;
+        for (size_t i = 0; i < (size_t)q->cap; ++i) s->claimed[i].store(0, std::memory_order_relaxed);
+        s->pending.store((int)n + 1);  // + 1: this thread's scan below
+        lk.lock();
+        s->ready = true;
+        q->cv_done.notify_all();  // waiters claim and copy out their own blocks
+        lk.unlock();
+        // copy out the blocks nobody claimed (un-waited async requests); a claimed
+        // request is never touched again here (its waiter may delete it)
+        std::vector<zs3_req*> mine;
+        for (size_t i = 0; i < n; ++i) {
+            if (s->claimed[pos[i]].exchange(1)) continue;
+            zs3_req* r = s->reqs[i];
+            finish_req(q, s, r);
+            mine.push_back(r);
         }
         lk.lock();
-        for (zs3_req* r : s->reqs) r->done = true;
-        s->reqs.clear();
-        s->state = Slot::FREE;
-        q->inflight[s->lane]--;
-        q->cv_done.notify_all();
-        q->cv_space.notify_all();
-        q->cv_disp.notify_one();  // batch-while-busy: the next open slot may go now
+        for (zs3_req* r : mine) r->done = true;
+        if (!mine.empty()) q->cv_done.notify_all();
+        lk.unlock();
+        for (size_t i = 0; i < mine.size(); ++i) finish_one(q, s);
+        finish_one(q, s);  // the scan itself
+        lk.lock();
     }
 }
 
@@ -427,12 +459,6 @@ int zs3_queue_new(const zs3_codec* c, const zs3_queue_opts* opts, zs3_queue** ou
         delete q;
         return ZS3_ERR_DEVICE;
     }
-    for (auto& s : q->stream)
-        if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
-            (void)hipSetDevice(prev);
-            delete q;
-            return ZS3_ERR_DEVICE;
-        }
     (void)hipSetDevice(prev);
     q->disp = std::thread(dispatcher, q);
     q->comp = std::thread(completer, q);
@@ -460,9 +486,8 @@ void zs3_queue_free(zs3_queue* q) {
             if (s.h) (void)hipHostFree(s.h);
             if (s.d) (void)hipFree(s.d);
             if (s.done_ev) (void)hipEventDestroy(s.done_ev);
+            if (s.stream) (void)hipStreamDestroy(s.stream);
         }
-    for (auto& s : q->stream)
-        if (s) (void)hipStreamDestroy(s);
     delete q;
 }
 
@@ -491,7 +516,7 @@ int zs3_queue_submit_encode(zs3_queue* q, uint8_t* h_buf, int64_t len, int64_t c
         s = r->slot;
     }
     // Split (reedsolomon): data rows are the input bytes, zero-padded to k*S
-    uint8_t* dst = s->h + (size_t)r->pos * q->E;
+    uint8_t* dst = s->h + (size_t)r->pos * q->k * q->S;
     std::memcpy(dst, h_buf, (size_t)len);
     if (q->k * Sb > len) std::memset(dst + len, 0, (size_t)(q->k * Sb - len));
     copy_in_done(q, s);
@@ -541,10 +566,18 @@ int zs3_queue_submit_decode(zs3_queue* q, uint8_t* h_shards, int64_t shard_len, 
 int64_t zs3_req_wait(zs3_req* r) {
     if (!r) return ZS3_OK;  // the empty-block case returned no handle
     zs3_queue* q = r->q;
+    Slot* s = r->slot;  // not freed before r is finished
+    bool own = false;
     {
         std::unique_lock<std::mutex> lk(q->mu);
         if (!r->done) q->cv_disp.notify_one();  // a lone waiter: the device may be idle
-        q->cv_done.wait(lk, [&] { return r->done; });
+        q->cv_done.wait(lk, [&] { return r->done || s->ready; });
+        if (!r->done) own = s->claimed[r->pos].exchange(1) == 0;
+        if (!own) q->cv_done.wait(lk, [&] { return r->done; });
+    }
+    if (own) {  // copy this block's results out on the calling thread
+        finish_req(q, s, r);
+        finish_one(q, s);
     }
     const int64_t rc = r->result;
     delete r;

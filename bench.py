@@ -210,7 +210,7 @@ def main() -> None:
                        "block_bytes": blen, "k": k, "m": m,
                        "parallelism": f"objects partitioned over {world} GPU(s), no collectives",
                        "kernel_path": {0: "generic", 1: "first-generation", 2: "warp-specialised",
-                                       3: "mixed-wave"}.get(path, str(path))},
+                                       3: "mixed-wave", 4: "small-batch latency"}.get(path, str(path))},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,

@@ -332,12 +332,14 @@ int zs3_selftest(void);
 /* Which kernel family served the last batch call on this thread (ZS3_PATH_*):
  * 0 = generic byte kernel, 1 = first-generation specialised (k, m) kernel,
  * 2 = warp-specialised kernel (k_ehx_ws / k_vr_ws), 3 = mixed-wave second-generation
- * encode (k_ehx); -1 = nothing launched. */
+ * encode (k_ehx), 4 = small-batch latency path (encode-only pass, then one chain per
+ * quad straight from HBM: k_hash_lat); -1 = nothing launched. */
 #define ZS3_PATH_NONE      -1
 #define ZS3_PATH_GENERIC    0
 #define ZS3_PATH_FIRSTGEN   1
 #define ZS3_PATH_WS         2
 #define ZS3_PATH_PIPE       3
+#define ZS3_PATH_LATENCY    4
 int zs3_last_path(void);
 
 #ifdef __cplusplus

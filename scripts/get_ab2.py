@@ -1,7 +1,8 @@
 """A/B of the GET / heal launches for the RS(4+2), RS(8+4) and RS(16+4) shapes
 (variant 0 = product default dispatch; others forced through the diagnostics build,
 e.g. 200 = first-generation kernel, 216/217 = scalar coefficient tables), interleaved
-rounds.  SHAPES=4,8,16 selects the shapes, CASES=heal filters the case names."""
+rounds.  SHAPES=4,8,16 selects the shapes, CASES=heal filters the case names, NOBJ=n
+overrides the batch size."""
 import contextlib
 import json
 import os
@@ -44,6 +45,7 @@ def ctx(v):
 
 
 for k, m, nobj, cases in [c for c in ALL if c[0] in shapes]:
+    nobj = int(os.environ.get("NOBJ", nobj))  # e.g. NOBJ=16: the small-batch regime
     blen = 1 << 20
     S = blen // k
     R = k + m

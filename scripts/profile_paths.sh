@@ -21,4 +21,6 @@ REPS=3 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/ppw -o p --output-
     python scripts/bench_paths.py > $OUT/ppw.log 2>&1 || { tail -5 $OUT/ppw.log; exit 6; }
 python scripts/pmc_paths.py $(find $OUT/ppf -name '*counter_collection.csv' | head -1) \
     $(find $OUT/ppw -name '*counter_collection.csv' | head -1) $P/paths_kernel_stats.csv $P/paths_pmc_traffic.json
+python scripts/paths_traffic_join.py $(find $OUT/ppf -name '*counter_collection.csv' | head -1) \
+    $(find $OUT/ppw -name '*counter_collection.csv' | head -1) $P/bench_paths.jsonl $P/bench_paths_roofline.jsonl
 echo "done $(date +%T)"

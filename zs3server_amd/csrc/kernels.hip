@@ -559,6 +559,131 @@ __global__ void __launch_bounds__(256) k_encode_only(EncArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Latency-regime bitrot sums (small batches): a HighwayHash chain over one shard row
+// is S/32 dependent packets, so with fewer chains than SIMDs a launch costs one chain's
+// latency whatever its size (~0.55 ms for 128 KiB rows through the tiled kernels, whose
+// chains wait on one 256-byte tile of prefetch per step).  Here one quad owns one chain
+// (hh256_dev.hpp quad form: the shortest dependent path per packet) and reads it
+// straight from global memory, NS*D packets of loads in flight per lane, no LDS, no
+// barriers, one wave per workgroup so the chains spread over the SIMDs.  The loop has
+// no stores, so the compiler's in-order vmcnt waits are exact.  Chain c = (block
+// c / (k+m), row c % (k+m)); data rows at data + b*data_stride + r*S, parity rows at
+// parity + b*parity_stride + (r-k)*S (EncArgs addressing, no Split padding), sums as
+// k_encode_hash.  Runs after k_encode_only on the same stream.
+// One chain per quad straight from global memory: this lane's 64-bit digest word of
+// HighwayHash-256(row[0..S)).  All 64 lanes of the wave must call it (DPP).
+template <int D, int NS>
+__device__ __forceinline__ uint64_t hash_chain_lat(const uint8_t* row, int64_t S, int lane, const uint64_t* key) {
+    const uint32_t sel = zipper_sel(lane);
+    HHLane st = hh_init(lane, key[0], key[1], key[2], key[3]);
+    const uint64_t* p = reinterpret_cast<const uint64_t*>(row) + lane;  // packet q: p[4q]
+    const int64_t npk = S >> 5;
+    uint64_t w[NS][D];
+    // A stage wholly inside the row loads through one pointer with immediate offsets
+    // (no per-load address VALU on the lone wave's critical path); the last stages clamp
+    // (a packet past the end re-reads the last one and is not hashed).
+    auto load = [&](uint64_t (&x)[D], int64_t q0) {
+        if (q0 + D <= npk) {
+            const uint64_t* q = p + 4 * q0;
+#pragma unroll
+            for (int j = 0; j < D; ++j) x[j] = __builtin_nontemporal_load(q + 4 * j);
+        } else {
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+                const int64_t q = q0 + j < npk ? q0 + j : npk - 1;
+                x[j] = __builtin_nontemporal_load(p + 4 * q);
+            }
+        }
+    };
+    if (npk > 0) {
+#pragma unroll
+        for (int s = 0; s < NS - 1; ++s) load(w[s], (int64_t)s * D);
+        for (int64_t q0 = 0; q0 < npk; q0 += (int64_t)NS * D) {
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                const int64_t base = q0 + (int64_t)s * D;
+                if (base >= npk) break;
+                load(w[(s + NS - 1) % NS], base + (int64_t)(NS - 1) * D);
+                if (base + D <= npk) {
+#pragma unroll
+                    for (int j = 0; j < D; ++j) hh_update(st, w[s][j], sel);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < D; ++j)
+                        if (base + j < npk) hh_update(st, w[s][j], sel);
+                }
+            }
+        }
+    }
+    const uint32_t rem = (uint32_t)(S & 31);
+    if (rem) hh_remainder(st, row + (npk << 5), rem, lane, sel);
+    return hh_finalize256(st, lane, sel);
+}
+
+template <int D, int NS>
+__global__ void __launch_bounds__(64) k_hash_lat(EncArgs a) {
+    const int R = a.k + a.m;
+    const int tid = threadIdx.x, lane = tid & 3;
+    const int64_t nch = a.n_blocks * R;
+    int64_t c = (int64_t)blockIdx.x * 16 + (tid >> 2);
+    const bool live = c < nch;
+    if (!live) c = nch - 1;  // dead quads re-hash the last chain (all lanes stay active)
+    const int64_t b = c / R;
+    const int r = (int)(c % R);
+    const uint8_t* row = r < a.k ? a.data + b * a.data_stride + (int64_t)r * a.S
+                                 : a.parity + b * a.parity_stride + (int64_t)(r - a.k) * a.S;
+    const uint64_t h = hash_chain_lat<D, NS>(row, a.S, lane, a.key);
+    if (live) *reinterpret_cast<uint64_t*>(a.sums + (b * R + r) * 32 + 8 * lane) = h;
+}
+
+// GET / heal in the latency regime, after k_reconstruct has rebuilt the missing rows:
+// chain (block b, i) hashes row rows[i] of block slot(b); i < k verifies a survivor
+// against its stored sum (bad flag = errFileCorrupt, a quad ballot), i >= k (heal) writes
+// the rebuilt row's new sum.  nr = k (GET) or k + e (heal).
+template <int D, int NS>
+__global__ void __launch_bounds__(64) k_vr_hash_lat(VrArgs a, int nr) {
+    const int R = a.k + a.m;
+    const int tid = threadIdx.x, lane = tid & 3;
+    const int64_t nch = a.n_blocks * nr;
+    int64_t c = (int64_t)blockIdx.x * 16 + (tid >> 2);
+    const bool live = c < nch;
+    if (!live) c = nch - 1;
+    const int64_t b = c / nr;
+    const int i = (int)(c % nr);
+    const int64_t slot = a.ids ? (int64_t)a.ids[b] : b;
+    const int row = a.rows[i];
+    const uint8_t* rp = a.shards + slot * a.block_stride + (int64_t)row * a.S;
+    const uint64_t h = hash_chain_lat<D, NS>(rp, a.S, lane, a.key);
+    const int64_t so = (slot * R + row) * 32 + 8 * lane;
+    if (i < a.k) {
+        const bool mis = h != *reinterpret_cast<const uint64_t*>(a.expect + so);
+        const uint64_t bal = __ballot(mis);
+        if (live && lane == 0) a.bad[slot * R + row] = ((bal >> (tid & ~3)) & 0xF) ? 1 : 0;
+    } else if (live) {
+        *reinterpret_cast<uint64_t*>(a.sums_out + so) = h;
+    }
+}
+
+// Crossover of the split path against the fused kernels (sweep_sizes_small.txt):
+// RS(8+4) between 512 and 768 blocks (~1 GB of stripes), RS(16+4) between 256 and 512.
+template <int K, int M>
+static bool small_batch(int64_t n_blocks, int64_t S) {
+    if (K == 4 && M == 2) return false;
+    if (K == 16 && M == 4) return n_blocks <= 384;
+    return n_blocks * (K + M) * S <= (int64_t)640 * 12 * 131072;
+}
+
+template <int K, int M>
+static void launch_encode_lat(const EncArgs& a, hipStream_t s) {
+    const int64_t cols = (a.S + 15) >> 4;
+    const unsigned gx = (unsigned)((cols + 255) / 256);
+    const unsigned gy = (unsigned)(a.n_blocks < 65535 ? a.n_blocks : 65535);
+    hipLaunchKernelGGL((k_encode_only<K, M>), dim3(gx, gy), dim3(256), 0, s, a);
+    const int64_t nch = a.n_blocks * (K + M);
+    hipLaunchKernelGGL((k_hash_lat<16, 3>), dim3((unsigned)((nch + 15) / 16)), dim3(64), 0, s, a);
+}
+
+// ---------------------------------------------------------------------------
 // Reconstruct: E_MAX output rows, each a GF combination of the K valid rows.
 template <int K, int EMAX, int NC = 1>
 __global__ void __launch_bounds__(256) k_reconstruct(RecArgs a) {
@@ -1139,14 +1264,29 @@ static hipError_t run_encode_fast(const EncArgs& a, hipStream_t s, int* path) {
         constexpr int G = pick_G<R>();
         constexpr int NBUF = 2;
         constexpr int T = pick_T<G * R, NBUF>();
+        // Small batches are bound by one hash chain's latency, not by bytes: the split
+        // path (encode-only pass + k_hash_lat) halves that (RS(8+4) 1 block: 0.23 vs
+        // 0.53 ms; profiles/r02/sweep_sizes_small.txt).  Not for RS(4+2), whose
+        // quad-form k_ehx_ws chains run faster than k_hash_lat's at every size.
+        if (a.variant == 0 && small_batch<K, M>(a.n_blocks, a.S)) {
+            launch_encode_lat<K, M>(a, s);
+            p = PATH_LATENCY;
+        }
+        // diagnostics 99: the product dispatch without the latency path (tests keep the
+        // small-batch fused instances covered)
+        const int fv = (ZS3_DIAG && a.variant == 99) ? 0 : a.variant;
 #if ZS3_DIAG
+        if (a.variant == 49) {  // force the small-batch split path
+            launch_encode_lat<K, M>(a, s);
+            p = PATH_LATENCY;
+        }
         if constexpr ((K == 8 && M == 4) || (K == 4 && M == 2) || (K == 16 && M == 4)) {
-            if (a.variant > 0) p = launch_variant<K, M>(a.variant, a, s);
+            if (fv > 0 && p == PATH_NONE) p = launch_variant<K, M>(fv, a, s);
         }
 #endif
         // Dyadic shapes (RS(4+2), RS(8+4), RS(16+4), ...): the second-generation
         // kernels of fused_v2.hip pick their launch shape from (k, m, n_blocks).
-        if (p == PATH_NONE && a.variant == 0) p = launch_ehx(0, a, s);
+        if (p == PATH_NONE && fv == 0) p = launch_ehx(0, a, s);
         if (p == PATH_NONE) {
             // First-generation kernel (profiles/r01 tuning): 8-byte columns so every
             // thread encodes, one 384-byte tile per step.  k <= 8: one LDS tile.
@@ -1310,14 +1450,55 @@ static hipError_t hash_rebuilt_rows(const VrArgs& a, hipStream_t s) {
     return hipSuccess;
 }
 
+// GET / heal small-batch path: k_reconstruct rebuilds the missing rows, then one chain
+// per quad verifies the survivors (and, for heal, hashes the rebuilt rows).
+static hipError_t launch_vr_lat(const VrArgs& a, hipStream_t s) {
+    if (a.e > 0) {
+        RecArgs r{};
+        r.shards = a.shards;
+        r.block_stride = a.block_stride;
+        r.S = a.S;
+        r.n_blocks = a.n_blocks;
+        r.tables = a.tables;
+        r.coef = a.coef;
+        r.rows = a.rows;
+        r.k = a.k;
+        r.e = a.e;
+        r.ids = a.ids;
+        hipError_t e = launch_reconstruct(r, s, nullptr);
+        if (e != hipSuccess) return e;
+    }
+    const int nr = a.k + (a.sums_out ? a.e : 0);
+    const int64_t nch = a.n_blocks * nr;
+    hipLaunchKernelGGL((k_vr_hash_lat<16, 3>), dim3((unsigned)((nch + 15) / 16)), dim3(64), 0, s, a, nr);
+    return hipGetLastError();
+}
+
+// Crossover of the GET / heal latency path against the fused kernels (NOBJ sweeps of
+// scripts/get_ab2.py, profiles/r02/get_lat.txt).  RS(4+2): the quad-form k_vr_ws
+// chains are faster at every size.
+static bool small_get(int k, int m, int e, bool heal, int64_t n, int64_t S) {
+    if (k == 4 && m == 2) return false;
+    if (k == 16 && m == 4) return n <= (e <= 1 ? 512 : (heal && e == 4) ? 2048 : 1024);
+    if (k == 8 && m == 4) return n <= ((e <= 1 || (e == 2 && !heal)) ? 1024 : 2048);
+    return n * k * S <= ((int64_t)1 << 30);
+}
+
 template <int K>
 static hipError_t run_vr_k(const VrArgs& a, hipStream_t s, int* path) {
+    if ((a.variant == 0 && small_get(a.k, a.m, a.e, a.sums_out != nullptr, a.n_blocks, a.S)) ||
+        (ZS3_DIAG && a.variant == 230)) {  // 230: force it
+        if (path) *path = PATH_LATENCY;
+        return launch_vr_lat(a, s);
+    }
     // Default for the RS(8+4)-, RS(4+2)- and RS(16+4)-shaped GETs: the warp-specialised
     // k_vr_ws (fused_v2.hip): RS(8+4) verify 0.85 -> 0.70 ms, verify + rebuild 2
     // 1.41 -> 1.13 ms on 4096 x 1 MiB (scripts/get_ab.py).  Variants 200-209 (diagnostics)
     // force the first-generation kernel.
-    if (a.variant == 0 || (ZS3_DIAG && a.variant >= 210 && a.variant <= 219))
-        if (launch_vr_ws(a.variant, a, s)) {
+    // diagnostics 231: the product dispatch without the latency path
+    const int wv = (ZS3_DIAG && a.variant == 231) ? 0 : a.variant;
+    if (wv == 0 || (ZS3_DIAG && wv >= 210 && wv <= 219))
+        if (launch_vr_ws(wv, a, s)) {
             if (path) *path = PATH_WS;
             return hipGetLastError();
         }

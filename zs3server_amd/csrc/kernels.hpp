@@ -23,6 +23,7 @@ enum Path : int {
     PATH_FIRSTGEN = 1,  // first-generation specialised kernels (kernels.hip)
     PATH_WS = 2,        // warp-specialised kernels (fused_v2.hip k_ehx_ws / k_vr_ws)
     PATH_PIPE = 3,      // mixed-wave second-generation encode (fused_v2.hip k_ehx)
+    PATH_LATENCY = 4,   // small batches: k_encode_only + k_hash_lat (kernels.hip)
 };
 
 // Batched Split+Encode(+HH256) over n_blocks independent blocks.

@@ -76,7 +76,7 @@ WS_CASES = [(8, 4, 1 << 16, []), (8, 4, 1 << 16, [0, 5]), (8, 4, 1 << 16, [3, 9]
 @pytest.mark.parametrize("k,m,blen,erased", WS_CASES)
 @pytest.mark.parametrize("data_only", [True, False])
 @pytest.mark.parametrize("heal", [False, True])
-@pytest.mark.parametrize("variant", [0, 210, 211, 212, 213, 216, 218, 230, 231])
+@pytest.mark.parametrize("variant", [0, 210, 211, 212, 213, 214, 216, 218, 230, 231])
 def test_verify_reconstruct_ws(oracle, k, m, blen, erased, data_only, heal, variant):
     """Variant 0: the product dispatch; at 17 blocks it takes the small-batch latency
     path (k_reconstruct + one chain per quad).  231 = the product dispatch without that
@@ -141,12 +141,12 @@ WS16_GET_CASES = [(16, 4, blen, erased, data_only)
 
 
 @pytest.mark.parametrize("k,m,blen,erased,data_only", WS16_GET_CASES)
-@pytest.mark.parametrize("variant", [0, 216, 231])
+@pytest.mark.parametrize("variant", [0, 216, 217, 219, 231])
 def test_verify_reconstruct_ws_rs164(oracle, k, m, blen, erased, data_only, variant):
     """The RS(16+4) rebuild-1..4 defaults (231: without the small-batch latency path
     that variant 0 takes at 11 blocks) run the warp-specialised kernel (asserted through
     zs3_last_path) and are bit-exact vs the oracle; 216 = the rebuild role with scalar
-    (SGPR) coefficient tables."""
+    (SGPR) coefficient tables, 217 = 4-byte rebuild columns (twice the rebuild waves)."""
     with variant_ctx(variant):
         run_verify_case(oracle, k, m, blen, erased, data_only, False, nb=11, want_path=4 if variant == 0 else 2)
 

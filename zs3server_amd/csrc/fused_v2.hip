@@ -1245,6 +1245,24 @@ bool launch_vr_ws(int v, const VrArgs& a, hipStream_t s) {
         return false;
     }
 #endif
+#if ZS3_DIAG
+    if (a.k == 16 && v == 219 && a.sums_out == nullptr) {  // 217 + scalar coefficient tables
+        if (a.e == 1) return launch_vr_ws_t<16, 1, false, 8, 256, 1, 4, false, true>(a, s);
+        if (a.e == 2) return launch_vr_ws_t<16, 2, false, 8, 256, 1, 4, false, true>(a, s);
+        if (a.e == 3) return launch_vr_ws_t<16, 3, false, 8, 256, 1, 4, false, true>(a, s);
+        if (a.e == 4) return launch_vr_ws_t<16, 4, false, 8, 256, 1, 4, false, true>(a, s);
+        return false;
+    }
+    if (a.k == 16 && v == 217 && a.sums_out == nullptr) {
+        // twice the rebuild waves (12 waves, 3 per SIMD): 4-byte columns of 256-byte
+        // tiles (8-byte columns of 512-byte tiles spill in the hash role)
+        if (a.e == 1) return launch_vr_ws_t<16, 1, false, 8, 256, 1, 4>(a, s);
+        if (a.e == 2) return launch_vr_ws_t<16, 2, false, 8, 256, 1, 4>(a, s);
+        if (a.e == 3) return launch_vr_ws_t<16, 3, false, 8, 256, 1, 4>(a, s);
+        if (a.e == 4) return launch_vr_ws_t<16, 4, false, 8, 256, 1, 4>(a, s);
+        return false;
+    }
+#endif
     if (a.k == 16 && (v == 0 || v == 210 || v == 215 || v == 216)) {
         // RS(16+4)-shaped GET: 8 stripes, 256-byte tiles; rebuilds with 8-byte columns
         // (16-byte columns spill: 16 survivors x 2 tiles beside 32-64 generic products).
@@ -1327,6 +1345,13 @@ bool launch_vr_ws(int v, const VrArgs& a, hipStream_t s) {
         case 211:
             if (a.e == 0) return launch_vr_ws_t<8, 0, false, 16, 256, 1>(a, s);
             if (a.e == 2) return launch_vr_ws_t<8, 2, false, 16, 256, 1>(a, s);
+            return false;
+        case 214:  // twice the rebuild waves: 8-byte columns (12 waves, 3 per SIMD);
+                   // e >= 2 with scalar coefficient tables (VGPR tables spill at 168)
+            if (a.e == 1) return launch_vr_ws_t<8, 1, false, 16, 256, 1, 8>(a, s);
+            if (a.e == 2) return launch_vr_ws_t<8, 2, false, 16, 256, 1, 8, false, true>(a, s);
+            if (a.e == 3) return launch_vr_ws_t<8, 3, false, 16, 256, 1, 8, false, true>(a, s);
+            if (a.e == 4) return launch_vr_ws_t<8, 4, false, 16, 256, 1, 8, false, true>(a, s);
             return false;
         case 216:
             if (a.e == 1) return launch_vr_ws_t<8, 1, false, 16, 256, 2, 16, false, true>(a, s);

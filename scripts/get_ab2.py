@@ -33,7 +33,8 @@ ALL = ((4, 2, 2048, (("verify 4", [], False), ("verify + rebuild 2", [0, 3], Fal
                      ("verify + rebuild 1", [1], False), ("heal 2", [1, 5], True))),
        (8, 4, 4096, (("verify 8", [], False), ("verify + rebuild 1", [3], False),
                      ("verify + rebuild 2", [0, 5], False), ("verify + rebuild 3", [0, 5, 6], False),
-                     ("verify + rebuild 4", [1, 2, 5, 7], False), ("heal 1", [4], True), ("heal 2", [2, 10], True))),
+                     ("verify + rebuild 4", [1, 2, 5, 7], False), ("heal 1", [4], True), ("heal 2", [2, 10], True),
+                     ("heal 3", [0, 6, 9], True), ("heal 4", [1, 3, 8, 11], True))),
        (16, 4, 2048, (("verify 16", [], False), ("verify + rebuild 1", [6], False), ("verify + rebuild 2", [0, 9], False),
                       ("verify + rebuild 3", [1, 7, 15], False), ("verify + rebuild 4", [1, 7, 14, 15], False),
                       ("heal 1", [5], True), ("heal 2", [0, 17], True), ("heal 3", [2, 11, 18], True),

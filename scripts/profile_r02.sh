@@ -31,6 +31,19 @@ cp $P/pmc_traffic.json profiles/r02/pmc_traffic.json 2>/dev/null
 echo "bench $(date +%T)"
 timeout -k 10 300 python bench.py > $OUT/bench.log 2>&1 || { cat $OUT/bench.log; exit 16; }
 grep '"metric"' $OUT/bench.log | tee $P/bench.json
+echo "native queue $(date +%T)"
+timeout -k 10 200 tools/queue_bench 1,4,16,64,256 32 > $P/queue_native.jsonl || exit 18
+echo "size sweeps $(date +%T)"
+SIZES=1,64,256,512,640,641,1000,2047,2048,2304,2305,3001,4096,8192,16384 VARIANTS=0 ROUNDS=2 REPS=7 \
+    timeout -k 10 300 python -u scripts/sweep_sizes.py > $P/sweep_sizes_final_rs84.jsonl || exit 19
+K=16 M=4 SIZES=1,64,256,384,385,1024,2047,2048,4096,8192 VARIANTS=0 ROUNDS=2 REPS=7 \
+    timeout -k 10 300 python -u scripts/sweep_sizes.py > $P/sweep_sizes_final_rs164.jsonl || exit 20
+K=4 M=2 SIZES=1,64,256,1024,2048,2049,4096,8192 VARIANTS=0 ROUNDS=2 REPS=7 \
+    timeout -k 10 300 python -u scripts/sweep_sizes.py > $P/sweep_sizes_final_rs42.jsonl || exit 21
+echo "GET small batches $(date +%T)"
+for n in 1 64 512; do
+  NOBJ=$n VARIANTS=0,231 SHAPES=4,8,16 timeout -k 10 200 python -u scripts/get_ab2.py >> $P/get_small_batches.jsonl || exit 22
+done
 echo "queue + e2e $(date +%T)"
 PATHS=queue,e2e timeout -k 10 600 python scripts/bench_paths.py > $P/bench_paths_host.jsonl 2>$OUT/bph.err || { tail $OUT/bph.err; exit 17; }
 echo "done $(date +%T)"

@@ -76,19 +76,20 @@ WS_CASES = [(8, 4, 1 << 16, []), (8, 4, 1 << 16, [0, 5]), (8, 4, 1 << 16, [3, 9]
 @pytest.mark.parametrize("k,m,blen,erased", WS_CASES)
 @pytest.mark.parametrize("data_only", [True, False])
 @pytest.mark.parametrize("heal", [False, True])
-@pytest.mark.parametrize("variant", [0, 210, 211, 212, 213, 214, 216, 218, 230, 231])
+@pytest.mark.parametrize("variant", [0, 210, 211, 212, 213, 214, 216, 218, 230, 231, 232])
 def test_verify_reconstruct_ws(oracle, k, m, blen, erased, data_only, heal, variant):
     """Variant 0: the product dispatch; at 17 blocks it takes the small-batch latency
     path (k_reconstruct + one chain per quad).  231 = the product dispatch without that
-    path, asserted to run k_vr_ws for every RS(8+4) GET with 0-4 rebuilt rows and every
-    heal of 0-2 rows (zs3_last_path); heals of 3-4 rows run the first-generation
-    kernel.  218 = split heal (GET rebuild + hash kernel)."""
+    path, asserted to run k_vr_ws for every RS(8+4) GET and heal with 0-4 rebuilt rows
+    (zs3_last_path).  218 = split heal (GET rebuild + hash kernel)."""
     e = len(erased) if heal else len([i for i in erased if i < k or not data_only])
     want = None
     if variant == 0:
         want = 4
     if variant == 231:
-        want = 2 if (not heal or e <= 2) else 1
+        want = 2
+    if variant == 232 and heal and e >= 3:  # heal 3-4 on k_vr_ws (padded pair form)
+        want = 2
     with variant_ctx(variant):
         run_verify_case(oracle, k, m, blen, erased, data_only, heal, nb=17, want_path=want)
 
@@ -116,17 +117,18 @@ WS16_HEAL_CASES = [(16, 4, 1 << 16, [0, 5]), (16, 4, 1 << 16, [3, 17]), (16, 4, 
 
 
 @pytest.mark.parametrize("k,m,blen,erased", WS16_HEAL_CASES)
-@pytest.mark.parametrize("variant", [0, 215, 216, 218, 231])
+@pytest.mark.parametrize("variant", [0, 215, 216, 218, 231, 232])
 def test_heal_ws_rs164(oracle, k, m, blen, erased, variant):
-    """RS(16+4) heal (rebuild 1-4 shards and hash them) on k_vr_ws: the default for one
-    lost shard (padded pair-form hash waves; 231 = the product dispatch without the
-    small-batch latency path that variant 0 takes at 11 blocks), 215 (quad-form hash waves,
-    e = 2 / 4), 216 (pair form, e = 1..4) and 218 (split: GET rebuild + hash kernel);
-    the default runs the first-generation kernel for 2-4 lost shards.  The launched
-    family is asserted: tile edges, ragged tails and dead stripes of the 8-stripe
-    workgroup."""
+    """RS(16+4) heal (rebuild 1-4 shards and hash them) on k_vr_ws: the defaults (231 =
+    the product dispatch without the small-batch latency path that variant 0 takes at 11
+    blocks): padded pair-form hash waves, 8-byte rebuild columns for one lost shard and
+    4-byte columns of 128-byte tiles for 2-4 (232 forces the latter); 215 (quad-form
+    hash waves, e = 2 / 4), 216 (pair form, 8-byte columns, e = 1..4) and 218 (split:
+    GET rebuild + hash kernel).  The launched family is asserted: tile edges, ragged
+    tails and dead stripes of the 8-stripe workgroup."""
     e = len(erased)
-    want = {0: 4, 231: 2 if e == 1 else 1, 215: 2 if e in (2, 4) else None, 216: 2, 218: 2}[variant]
+    want = {0: 4, 231: 2, 215: 2 if e in (2, 4) else None, 216: 2, 218: 2,
+            232: 2 if e >= 2 else 1}[variant]
     with variant_ctx(variant):
         run_verify_case(oracle, k, m, blen, erased, False, True, nb=11, want_path=want)
 

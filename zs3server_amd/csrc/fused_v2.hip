@@ -1245,14 +1245,36 @@ bool launch_vr_ws(int v, const VrArgs& a, hipStream_t s) {
         return false;
     }
 #endif
-#if ZS3_DIAG
-    if (a.k == 16 && v == 219 && a.sums_out == nullptr) {  // 217 + scalar coefficient tables
+    if (a.k == 16 && (v == 0 || v == 219) && a.sums_out == nullptr && a.e >= 1) {
+        // RS(16+4) GET rebuild 1-4: 4-byte rebuild columns (8 rebuild waves beside the 4
+        // hash waves, 3 waves per SIMD) with scalar coefficient tables.  2048 x 1 MiB:
+        // rebuild 1/2/3/4 0.50/0.55/0.66/0.75 ms vs 0.52/0.62/0.75/0.85 with 8-byte
+        // columns (4 rebuild waves); profiles/r02/get_ab_waves.txt
         if (a.e == 1) return launch_vr_ws_t<16, 1, false, 8, 256, 1, 4, false, true>(a, s);
         if (a.e == 2) return launch_vr_ws_t<16, 2, false, 8, 256, 1, 4, false, true>(a, s);
         if (a.e == 3) return launch_vr_ws_t<16, 3, false, 8, 256, 1, 4, false, true>(a, s);
         if (a.e == 4) return launch_vr_ws_t<16, 4, false, 8, 256, 1, 4, false, true>(a, s);
         return false;
     }
+    if ((v == 0 || v == 232) && a.k == 16 && a.sums_out != nullptr && a.e >= 2) {
+        // RS(16+4) heal 2-4: 4-byte rebuild columns of 128-byte tiles (4 rebuild waves
+        // beside 5 pair-form hash waves, scalar tables).  2048 x 1 MiB: heal 2/3/4
+        // 0.82/0.99/1.17 ms vs 0.95/1.13/1.31 for the first-generation kernel
+        // (profiles/r02/get_ab_waves.txt)
+        if (a.e == 2) return launch_vr_ws_t<16, 2, true, 8, 128, 1, 4, false, true>(a, s);
+        if (a.e == 3) return launch_vr_ws_t<16, 3, true, 8, 128, 1, 4, false, true>(a, s);
+        if (a.e == 4) return launch_vr_ws_t<16, 4, true, 8, 128, 1, 4, false, true>(a, s);
+        return false;
+    }
+    if ((v == 0 || v == 232) && a.k == 8 && a.sums_out != nullptr && a.e >= 3) {
+        // RS(8+4) heal 3-4: padded pair-form hash waves (11 / 12 hashed rows x 16 stripes)
+        // beside 4 rebuild waves; 4096 x 1 MiB: 1.50 / 1.80 ms vs 2.01 / 2.32 for the
+        // first-generation kernel (profiles/r02/get_ab_waves.txt)
+        if (a.e == 3) return launch_vr_ws_t<8, 3, true, 16, 128, 2, 8, false, true>(a, s);
+        if (a.e == 4) return launch_vr_ws_t<8, 4, true, 16, 128, 2, 8, false, true>(a, s);
+        return false;
+    }
+#if ZS3_DIAG
     if (a.k == 16 && v == 217 && a.sums_out == nullptr) {
         // twice the rebuild waves (12 waves, 3 per SIMD): 4-byte columns of 256-byte
         // tiles (8-byte columns of 512-byte tiles spill in the hash role)
@@ -1297,11 +1319,11 @@ bool launch_vr_ws(int v, const VrArgs& a, hipStream_t s) {
             return false;
         }
         if (v == 215) return false;
-        if (v == 0) {
+#if ZS3_DIAG
+        if (v == 210) {  // 8-byte rebuild columns (4 rebuild waves), the round-2 first cut
             if (a.e == 1) return launch_vr_ws_t<16, 1, false, 8, 256, 1, 8>(a, s);
             if (a.e == 3) return launch_vr_ws_t<16, 3, false, 8, 256, 1, 8>(a, s);
         }
-#if ZS3_DIAG
         if (v == 216) {  // scalar coefficient tables in the rebuild role
             if (a.e == 1) return launch_vr_ws_t<16, 1, false, 8, 256, 1, 8, false, true>(a, s);
             if (a.e == 3) return launch_vr_ws_t<16, 3, false, 8, 256, 1, 8, false, true>(a, s);
@@ -1311,8 +1333,10 @@ bool launch_vr_ws(int v, const VrArgs& a, hipStream_t s) {
         }
 #endif
         if (a.e == 0) return launch_vr_ws_t<16, 0, false, 8, 256, 2>(a, s);
+#if ZS3_DIAG
         if (a.e == 2) return launch_vr_ws_t<16, 2, false, 8, 256, 1, 8>(a, s);
         if (a.e == 4) return launch_vr_ws_t<16, 4, false, 8, 256, 1, 8>(a, s);
+#endif
         return false;
     }
     if (a.k != 8) return false;
@@ -1338,8 +1362,14 @@ bool launch_vr_ws(int v, const VrArgs& a, hipStream_t s) {
             if (a.e == 0) return launch_vr_ws_t<8, 0, false, 16, 256, 2>(a, s);
             if (a.e == 1) return launch_vr_ws_t<8, 1, false, 16, 256, 2>(a, s);
             if (a.e == 2) return launch_vr_ws_t<8, 2, false, 16, 256, 2>(a, s);
+            // rebuild 3/4: 8-byte columns (8 rebuild waves, scalar tables): 4096 x 1 MiB
+            // 1.27 / 1.42 ms vs 1.35 / 1.58 with 16-byte columns (get_ab_waves.txt)
+            if (v == 0 && a.e == 3) return launch_vr_ws_t<8, 3, false, 16, 256, 1, 8, false, true>(a, s);
+            if (v == 0 && a.e == 4) return launch_vr_ws_t<8, 4, false, 16, 256, 1, 8, false, true>(a, s);
+#if ZS3_DIAG
             if (a.e == 3) return launch_vr_ws_t<8, 3, false, 16, 256, 1>(a, s);
             if (a.e == 4) return launch_vr_ws_t<8, 4, false, 16, 256, 1>(a, s);
+#endif
             return false;
 #if ZS3_DIAG
         case 211:

@@ -1479,7 +1479,7 @@ static hipError_t launch_vr_lat(const VrArgs& a, hipStream_t s) {
 // chains are faster at every size.
 static bool small_get(int k, int m, int e, bool heal, int64_t n, int64_t S) {
     if (k == 4 && m == 2) return false;
-    if (k == 16 && m == 4) return n <= (e <= 1 ? 512 : (heal && e == 4) ? 2048 : 1024);
+    if (k == 16 && m == 4) return n <= (e <= 1 ? 512 : 1024);
     if (k == 8 && m == 4) return n <= ((e <= 1 || (e == 2 && !heal)) ? 1024 : 2048);
     return n * k * S <= ((int64_t)1 << 30);
 }
@@ -1497,7 +1497,7 @@ static hipError_t run_vr_k(const VrArgs& a, hipStream_t s, int* path) {
     // force the first-generation kernel.
     // diagnostics 231: the product dispatch without the latency path
     const int wv = (ZS3_DIAG && a.variant == 231) ? 0 : a.variant;
-    if (wv == 0 || (ZS3_DIAG && wv >= 210 && wv <= 219))
+    if (wv == 0 || (ZS3_DIAG && ((wv >= 210 && wv <= 219) || wv == 232)))
         if (launch_vr_ws(wv, a, s)) {
             if (path) *path = PATH_WS;
             return hipGetLastError();

@@ -210,7 +210,9 @@ def main():
             funcs.append(cur)
             continue
         if cur is not None:
-            if l.strip().startswith("s_endpgm"):
+            # a kernel may hold several s_endpgm (warp-specialised roles return early);
+            # the function ends at its .Lfunc_end label
+            if l.startswith(".Lfunc_end"):
                 cur = None
                 continue
             cur[1].append((i, l))

@@ -457,8 +457,14 @@ constexpr int ws_cwe() {
 // younger partner finishes alone.
 // NTM (memory policy, bit mask): 1 = data loads non-temporal, 2 = parity stores non-temporal.
 // STB: encode role reads the coefficient tables with scalar loads (SGPRs) instead of LDS.
+// EP = 1 (early prefetch): the encode wave first copies its data columns into the LDS
+// tile, issues the next tile's loads into the freed registers, and then encodes from the
+// LDS copy (one block of M rows at a time): the loads get a whole step to land instead of
+// the parity stores + barrier.  EP = 2 (early data write): the data columns go to LDS
+// before the encode instead of after it, so the LDS drains the tile's data rows while
+// the VALU encodes and only the parity rows are written between encode and barrier.
 template <int K, int M, int G, int T, int PF, bool BUF = false, bool HQ = false, bool WT = false, int PM = 0,
-          int CWX = 0, bool RING = false, int NTM = 0, bool STB = false>
+          int CWX = 0, bool RING = false, int NTM = 0, bool STB = false, int EP = 0>
 __global__ void __launch_bounds__((ws_nh<K, M, G, T, HQ>() + G * (T / ws_cwe<K, CWX>()))) __attribute__((amdgpu_waves_per_eu(3)))
 k_ehx_ws(EncArgs a) {
     constexpr int R = K + M;
@@ -662,6 +668,7 @@ k_ehx_ws(EncArgs a) {
     const uint32_t vo_p = (uint32_t)((b - blk0) * a.parity_stride + o);
 
     VT x[PF][K];
+    CoefTab ptab[EP == 3 ? K : 1];  // EP = 3: coefficient tables held in registers
     // rows j of tile offset t0u (wave-uniform) at per-lane byte offset vo within the row
     auto load_buf = [&](VT (&xs)[K], uint32_t vo, int64_t t0u) {
 #pragma unroll
@@ -711,7 +718,33 @@ k_ehx_ws(EncArgs a) {
         Col<NWd> xs[K];
 #pragma unroll
         for (int j = 0; j < K; ++j) xs[j] = to_col<NWd>(xr[j]);
-        if constexpr (PM == 4) {
+        if constexpr (EP == 9) {
+            // timing ablation (diagnostics only; output differs): no GF arithmetic
+#pragma unroll
+            for (int r = 0; r < M; ++r)
+#pragma unroll
+                for (int w = 0; w < NWd; ++w) par[r].w[w] = xs[r].w[w] ^ xs[r + M].w[w];
+        } else if constexpr (EP == 8) {
+            // timing ablation: only the first half of the data rows enter the parity
+            Col<NWd> xh[K];
+#pragma unroll
+            for (int j = 0; j < K; ++j) xh[j] = xs[j % (K / 2)];
+            encode_dyadic<NWd, K / 2, M, true, false, STB>(*reinterpret_cast<const Col<NWd>(*)[K / 2]>(xh), par, tabs,
+                                                            const_tables(a.dtables));
+        } else if constexpr (EP == 3) {
+            // tables held in registers: the data rows go to LDS first and drain under the encode
+#pragma unroll
+            for (int j = 0; j < K; ++j) st_col<NWd>(tl + col_off + j * TS, xs[j]);
+            encode_dyadic_f<NWd, K, M, true, false, false, true>(
+                [&](int j) { return xs[j]; }, par, tabs, nullptr, NoHook{}, ptab);
+        } else if constexpr (EP == 2) {
+            // data rows written right after the first block's table reads
+            encode_dyadic_f<NWd, K, M, true, false, STB>(
+                [&](int j) { return xs[j]; }, par, tabs, const_tables(a.dtables), [&]() {
+#pragma unroll
+                    for (int j = 0; j < K; ++j) st_col<NWd>(tl + col_off + j * TS, xs[j]);
+                });
+        } else if constexpr (PM == 4) {
             __builtin_amdgcn_s_setprio(3);
             encode_dyadic<NWd, K, M, true, true>(xs, par, tabs);
             __builtin_amdgcn_sched_barrier(0);
@@ -719,8 +752,10 @@ k_ehx_ws(EncArgs a) {
         } else {
             encode_dyadic<NWd, K, M, true, false, STB>(xs, par, tabs, const_tables(a.dtables));
         }
+        if constexpr (EP != 2 && EP != 3) {
 #pragma unroll
-        for (int j = 0; j < K; ++j) st_col<NWd>(tl + col_off + j * TS, xs[j]);
+            for (int j = 0; j < K; ++j) st_col<NWd>(tl + col_off + j * TS, xs[j]);
+        }
 #pragma unroll
         for (int r = 0; r < M; ++r) st_col<NWd>(tl + col_off + (K + r) * TS, par[r]);
     };
@@ -753,9 +788,22 @@ k_ehx_ws(EncArgs a) {
         Col<NWd> par[M];
         slot_free(ti);
         vm_wait<M + (PF - 1) * (K + M)>(xs);
-        encode(xs, tile[ti & 1], par);
-        if constexpr (RING) ring_signal(&ring[ti & 1]);
-        load(xs, (ti + PF) * T);
+        if constexpr (EP == 1) {
+            static_assert(PF == 1 && !RING && PM != 4, "early prefetch: PF = 1, barrier hand-off");
+            uint8_t* tl = tile[ti & 1];
+#pragma unroll
+            for (int j = 0; j < K; ++j) st_col<NWd>(tl + col_off + j * TS, to_col<NWd>(xs[j]));
+            load(xs, (ti + PF) * T);
+            // read back this wave's own columns (LDS keeps one wave's accesses in order)
+            encode_dyadic_f<NWd, K, M, true, false, STB>(
+                [&](int j) { return ld_col<NWd>(tl + col_off + j * TS); }, par, tabs, const_tables(a.dtables));
+#pragma unroll
+            for (int r = 0; r < M; ++r) st_col<NWd>(tl + col_off + (K + r) * TS, par[r]);
+        } else {
+            encode(xs, tile[ti & 1], par);
+            if constexpr (RING) ring_signal(&ring[ti & 1]);
+            load(xs, (ti + PF) * T);
+        }
         store_par(par, ti * T);
         if constexpr (!RING) bar();
     };
@@ -771,6 +819,14 @@ k_ehx_ws(EncArgs a) {
         if constexpr (!RING) bar();
     };
     bar();  // tables visible
+    if constexpr (EP == 3) {
+#pragma unroll
+        for (int i = 0; i < K; ++i) ptab[i] = load_coef(tabs, i);
+        // consume them here, so the LDS-counter wait for the table reads sits before the
+        // loop rather than at the first use inside every step
+#pragma unroll
+        for (int i = 0; i < K; ++i) asm volatile("" ::"v"(ptab[i].ab.x), "v"(ptab[i].ab.y), "v"(ptab[i].ab.z), "v"(ptab[i].ab.w), "v"(ptab[i].c));
+    }
 #pragma unroll
     for (int p = 0; p < PF; ++p) prefetch_any(x[p], p);
 #pragma unroll
@@ -791,7 +847,7 @@ k_ehx_ws(EncArgs a) {
 }
 
 template <int K, int M, int G, int T, int PF, bool BUF = false, bool HQ = false, int LDSMIN = 0, bool WT = false,
-          int PM = 0, int CWX = 0, bool RING = false, int NTM = 0, bool STB = false>
+          int PM = 0, int CWX = 0, bool RING = false, int NTM = 0, bool STB = false, int EP = 0>
 static bool launch_ws_t(const EncArgs& a, hipStream_t s) {
     constexpr int R = K + M;
     constexpr int NT = ws_nh<K, M, G, T, HQ>() + G * (T / ws_cwe<K, CWX>());
@@ -804,7 +860,7 @@ static bool launch_ws_t(const EncArgs& a, hipStream_t s) {
         if (BUF && ((G - 1) * a.data_stride + K * a.S > 0x7FFFFFFF ||
                     (G - 1) * a.parity_stride + M * a.S > 0x7FFFFFFF || a.data_stride < 0 || a.parity_stride < 0))
             return false;
-        auto kern = k_ehx_ws<K, M, G, T, PF, BUF, HQ, WT, PM, CWX, RING, NTM, STB>;
+        auto kern = k_ehx_ws<K, M, G, T, PF, BUF, HQ, WT, PM, CWX, RING, NTM, STB, EP>;
         if (ensure_dyn_lds((const void*)kern, dyn) != hipSuccess) return false;
         const int64_t grid = (a.n_blocks + G - 1) / G;
         hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), dyn, s, a);
@@ -854,8 +910,10 @@ static bool launch_ehx_t(const EncArgs& a, hipStream_t s) {
 //           n < 2048:  PATH_NONE -> the first-generation kernel (4 stripes per
 //                      workgroup, quad-form hash lanes: more threads per stripe when
 //                      there are too few stripes to fill 256 CUs with 16 each)
-//  RS(16+4) n >= 2048: k_ehx_ws G = 8 (variant 122: 5 pair-form hash waves + 6 encode
-//                      waves with 8-byte buffer-addressed columns, nt policy)
+//  RS(16+4) n >= 2048: k_ehx_ws G = 8 (variant 162: 5 pair-form hash waves + 6 encode
+//                      waves with 8-byte buffer-addressed columns, nt policy, data rows
+//                      written to LDS before the encode (EP = 2): 0.577 -> 0.590 of HBM
+//                      spec at 8192 stripes, profiles/r02/ab_encode_ep.jsonl)
 //           n <  2048: G = 4 with quad-form hash waves (variant 121)
 //  RS(4+2)  n <= 2048: k_ehx_ws G = 4, quad-form hash waves, nt stores (variant 116;
 //                      BASELINE config 2: the hash chains' latency sets the pace)
@@ -870,7 +928,7 @@ static int launch_ehx_default(const EncArgs& a, hipStream_t s) {
             return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3>(a, s) ? PATH_WS : PATH_NONE;
     } else if constexpr (K == 16 && M == 4) {
         if (n >= 8 * 256)
-            return launch_ws_t<K, M, 8, 384, 1, true, false, 0, false, 0, 0, false, 3>(a, s) ? PATH_WS : PATH_NONE;
+            return launch_ws_t<K, M, 8, 384, 1, true, false, 0, false, 0, 0, false, 3, false, 2>(a, s) ? PATH_WS : PATH_NONE;
         return launch_ws_t<K, M, 4, 512, 1, true, true>(a, s) ? PATH_WS : PATH_NONE;
     } else if constexpr (K == 4 && M == 2) {
         if (n <= 8 * 256)
@@ -921,6 +979,15 @@ static bool launch_ehx_km(int v, const EncArgs& a, hipStream_t s) {
         case 155: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, true>(a, s); else return false;
         case 153: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 2>(a, s); else return false;
         case 154: if constexpr (deep) return launch_ws_t<K, M, 8, 384, 1, false, false, 0, false, 1, 0, false, 2>(a, s); else return false;
+        case 156: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 1>(a, s); else return false;
+        case 157: if constexpr (few) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 1>(a, s); else return false;
+        case 160: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 2>(a, s); else return false;
+        case 161: if constexpr (few) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 2>(a, s); else return false;
+        case 163: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 3>(a, s); else return false;
+        case 164: if constexpr (few) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 3>(a, s); else return false;
+        case 168: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 8>(a, s); else return false;
+        case 169: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 9>(a, s); else return false;
+        case 162: if constexpr (K == 16 && M == 4) return launch_ws_t<K, M, 8, 384, 1, true, false, 0, false, 0, 0, false, 3, false, 2>(a, s); else return false;
         case 152: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 2, false, false, 0, false, 1>(a, s); else return false;
         case 140: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, true>(a, s); else return false;
         case 141: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 0, 0, true>(a, s); else return false;
@@ -967,7 +1034,12 @@ constexpr int vr_nh() {
 // ST: the rebuild role reads its coefficient tables with scalar loads (SGPRs) instead of
 // from LDS (gf_dev.hpp load_coef_s): rebuilding e rows from k survivors needs e*k
 // tables per column, which from LDS is ~10x the column's own bytes for RS(16+4), e = 4.
-template <int K, int EX, bool HOUT, int G, int T, int PF, int CW = 16, bool HQ = false, bool ST = false>
+// BT (with ST): the scalar tables are read in batches of 4 coefficients, double-buffered
+// in SGPRs: batch i+1's s_loads are issued right after the wait for batch i and land
+// while batch i's 4 products are computed.  (Scalar loads return out of order, so every
+// wait is lgkmcnt(0); one table per wait serialises the rebuild on scalar-cache latency.)
+template <int K, int EX, bool HOUT, int G, int T, int PF, int CW = 16, bool HQ = false, bool ST = false,
+          bool BT = false>
 __global__ void __launch_bounds__((vr_nh<G, K + (HOUT ? EX : 0), HQ>() + G * (T / CW))) __attribute__((amdgpu_waves_per_eu(2)))
 k_vr_ws(VrArgs a) {
     constexpr int RH = K + (HOUT ? EX : 0);
@@ -1129,6 +1201,24 @@ k_vr_ws(VrArgs a) {
             // opaque offset: the tables are reloaded per tile (scalar cache hits), not
             // hoisted out of the tile loop into e*k*5 SGPRs
             const ctab_ptr tg = const_tables(a.tables) + opaque_zero();
+            constexpr int NB = 4;  // BT: coefficients per scalar batch
+            CoefTab tbat[2][NB];
+            auto load_batch = [&](CoefTab (&d)[NB], int c0) {
+#pragma unroll
+                for (int i = 0; i < NB; ++i) d[i] = load_coef_s(tg, c0 + i);
+            };
+            // BT: consume batch d (the wait for its scalar loads sits here), then issue the
+            // next batch's loads, then compute; the scheduling barriers keep that order
+            auto wait_batch = [&](const CoefTab (&d)[NB]) {
+#pragma unroll
+                for (int i = 0; i < NB; ++i)
+                    asm volatile("" ::"s"(d[i].ab.x), "s"(d[i].ab.y), "s"(d[i].ab.z), "s"(d[i].ab.w), "s"(d[i].c));
+                __builtin_amdgcn_sched_barrier(0);
+            };
+            if constexpr (ST && BT) {
+                static_assert(K % NB == 0, "whole batches per rebuilt row");
+                load_batch(tbat[0], 0);
+            }
 #pragma unroll
             for (int r = 0; r < EX; ++r) {
                 GfAcc acc[NWd];
@@ -1136,7 +1226,17 @@ k_vr_ws(VrArgs a) {
                 for (int w = 0; w < NWd; ++w) acc_init(acc[w]);
 #pragma unroll
                 for (int j = 0; j < K; ++j) {
-                    if constexpr (ST) {
+                    if constexpr (ST && BT) {
+                        const int c = r * K + j, bi = c / NB, cur = bi & 1;
+                        if (c % NB == 0) {
+                            wait_batch(tbat[cur]);
+                            if (c + NB < EX * K) load_batch(tbat[cur ^ 1], c + NB);
+                            __builtin_amdgcn_sched_barrier(0);
+                        }
+                        const CoefTab t = tbat[cur][c % NB];
+#pragma unroll
+                        for (int w = 0; w < NWd; ++w) acc_add(acc[w], gf_lookup_s(split_nibbles(xs[j].w[w]), t));
+                    } else if constexpr (ST) {
                         const CoefTab t = load_coef_s(tg, r * K + j);
 #pragma unroll
                         for (int w = 0; w < NWd; ++w) acc_add(acc[w], gf_lookup_s(split_nibbles(xs[j].w[w]), t));
@@ -1149,7 +1249,7 @@ k_vr_ws(VrArgs a) {
 #pragma unroll
                 for (int w = 0; w < NWd; ++w) y[r].w[w] = acc_done(acc[w]);
                 // one rebuilt row at a time: its K coefficient tables, not all E*K, live
-                __builtin_amdgcn_sched_barrier(0);
+                if constexpr (!(ST && BT)) __builtin_amdgcn_sched_barrier(0);
             }
         }
 #pragma unroll
@@ -1199,8 +1299,21 @@ k_vr_ws(VrArgs a) {
     for (int p = 0; p < PF; ++p) vm_wait<0>(x[p]);
 }
 
-template <int K, int EX, bool HOUT, int G, int T, int PF, int CW = 16, bool HQ = false, bool ST = false>
+template <int K, int EX, bool HOUT, int G, int T, int PF, int CW, bool HQ, bool ST, bool BT>
+static bool launch_vr_ws_bt(const VrArgs& a, hipStream_t s);
+
+template <int K, int EX, bool HOUT, int G, int T, int PF, int CW = 16, bool HQ = false, bool ST = false,
+          bool BT = false>
 static bool launch_vr_ws_t(const VrArgs& a, hipStream_t s) {
+    // diagnostics 240: the same launch with the scalar-table batching flipped (A/B)
+    if constexpr (ZS3_DIAG && ST) {
+        if (a.variant == 240) return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, !BT>(a, s);
+    }
+    return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, BT>(a, s);
+}
+
+template <int K, int EX, bool HOUT, int G, int T, int PF, int CW, bool HQ, bool ST, bool BT>
+static bool launch_vr_ws_bt(const VrArgs& a, hipStream_t s) {
     constexpr int RH = K + (HOUT ? EX : 0);
     constexpr int NT = vr_nh<G, RH, HQ>() + G * (T / CW);
     constexpr size_t tiles = (size_t)2 * G * RH * (HQ ? T + 32 : T + 16);
@@ -1210,7 +1323,7 @@ static bool launch_vr_ws_t(const VrArgs& a, hipStream_t s) {
         return false;
     } else {
         if (a.e != EX || (a.S % 16) != 0 || a.k != K || (HOUT != (a.sums_out != nullptr) && EX > 0)) return false;
-        auto kern = k_vr_ws<K, EX, HOUT, G, T, PF, CW, HQ, ST>;
+        auto kern = k_vr_ws<K, EX, HOUT, G, T, PF, CW, HQ, ST, BT>;
         if (ensure_dyn_lds((const void*)kern, dyn) != hipSuccess) return false;
         const int64_t grid = (a.n_blocks + G - 1) / G;
         hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), dyn, s, a);
@@ -1249,7 +1362,8 @@ bool launch_vr_ws(int v, const VrArgs& a, hipStream_t s) {
         // RS(16+4) GET rebuild 1-4: 4-byte rebuild columns (8 rebuild waves beside the 4
         // hash waves, 3 waves per SIMD) with scalar coefficient tables.  2048 x 1 MiB:
         // rebuild 1/2/3/4 0.50/0.55/0.66/0.75 ms vs 0.52/0.62/0.75/0.85 with 8-byte
-        // columns (4 rebuild waves); profiles/r02/get_ab_waves.txt
+        // columns (4 rebuild waves); profiles/r02/get_ab_waves.jsonl.  Batched scalar tables
+        // (diagnostics 240) measured 2-4 % slower here (get_ab_bt.jsonl)
         if (a.e == 1) return launch_vr_ws_t<16, 1, false, 8, 256, 1, 4, false, true>(a, s);
         if (a.e == 2) return launch_vr_ws_t<16, 2, false, 8, 256, 1, 4, false, true>(a, s);
         if (a.e == 3) return launch_vr_ws_t<16, 3, false, 8, 256, 1, 4, false, true>(a, s);
@@ -1258,20 +1372,22 @@ bool launch_vr_ws(int v, const VrArgs& a, hipStream_t s) {
     }
     if ((v == 0 || v == 232) && a.k == 16 && a.sums_out != nullptr && a.e >= 2) {
         // RS(16+4) heal 2-4: 4-byte rebuild columns of 128-byte tiles (4 rebuild waves
-        // beside 5 pair-form hash waves, scalar tables).  2048 x 1 MiB: heal 2/3/4
-        // 0.82/0.99/1.17 ms vs 0.95/1.13/1.31 for the first-generation kernel
-        // (profiles/r02/get_ab_waves.txt)
-        if (a.e == 2) return launch_vr_ws_t<16, 2, true, 8, 128, 1, 4, false, true>(a, s);
-        if (a.e == 3) return launch_vr_ws_t<16, 3, true, 8, 128, 1, 4, false, true>(a, s);
-        if (a.e == 4) return launch_vr_ws_t<16, 4, true, 8, 128, 1, 4, false, true>(a, s);
+        // beside 5 pair-form hash waves, scalar tables read in double-buffered batches).
+        // 2048 x 1 MiB: heal 2/3/4 0.81/0.93/1.06 ms vs 0.82/0.99/1.17 with one table
+        // per scalar wait and 0.95/1.13/1.31 for the first-generation kernel
+        // (profiles/r02/get_ab_bt.jsonl, get_ab_waves.jsonl)
+        if (a.e == 2) return launch_vr_ws_t<16, 2, true, 8, 128, 1, 4, false, true, true>(a, s);
+        if (a.e == 3) return launch_vr_ws_t<16, 3, true, 8, 128, 1, 4, false, true, true>(a, s);
+        if (a.e == 4) return launch_vr_ws_t<16, 4, true, 8, 128, 1, 4, false, true, true>(a, s);
         return false;
     }
     if ((v == 0 || v == 232) && a.k == 8 && a.sums_out != nullptr && a.e >= 3) {
         // RS(8+4) heal 3-4: padded pair-form hash waves (11 / 12 hashed rows x 16 stripes)
-        // beside 4 rebuild waves; 4096 x 1 MiB: 1.50 / 1.80 ms vs 2.01 / 2.32 for the
-        // first-generation kernel (profiles/r02/get_ab_waves.txt)
-        if (a.e == 3) return launch_vr_ws_t<8, 3, true, 16, 128, 2, 8, false, true>(a, s);
-        if (a.e == 4) return launch_vr_ws_t<8, 4, true, 16, 128, 2, 8, false, true>(a, s);
+        // beside 4 rebuild waves, batched scalar tables; 4096 x 1 MiB: 1.41 / 1.61 ms vs
+        // 1.49 / 1.79 unbatched and 2.01 / 2.32 for the first-generation kernel
+        // (profiles/r02/get_ab_bt.jsonl, get_ab_waves.jsonl)
+        if (a.e == 3) return launch_vr_ws_t<8, 3, true, 16, 128, 2, 8, false, true, true>(a, s);
+        if (a.e == 4) return launch_vr_ws_t<8, 4, true, 16, 128, 2, 8, false, true, true>(a, s);
         return false;
     }
 #if ZS3_DIAG
@@ -1345,9 +1461,9 @@ bool launch_vr_ws(int v, const VrArgs& a, hipStream_t s) {
         // 9-wave workgroup inside 168 VGPRs (1.50 -> 1.25 ms, 1 data + 1 parity)
         // (scalar coefficient tables, variant 216: 1.28 -> 1.18 ms on 4096 x 1 MiB,
         // profiles/r02/get_ab.txt)
-        if ((v == 0 || v == 216) && a.e == 1) return launch_vr_ws_t<8, 1, true, 16, 128, 2, 8, false, true>(a, s);
+        if ((v == 0 || v == 216) && a.e == 1) return launch_vr_ws_t<8, 1, true, 16, 128, 2, 8, false, true, true>(a, s);
         if (a.e != 2) return false;
-        if (v == 0 || v == 216) return launch_vr_ws_t<8, 2, true, 16, 128, 2, 8, false, true>(a, s);
+        if (v == 0 || v == 216) return launch_vr_ws_t<8, 2, true, 16, 128, 2, 8, false, true, true>(a, s);
 #if ZS3_DIAG
         if (v == 212) return launch_vr_ws_t<8, 2, true, 16, 128, 2, 8>(a, s);
 #endif
@@ -1363,9 +1479,9 @@ bool launch_vr_ws(int v, const VrArgs& a, hipStream_t s) {
             if (a.e == 1) return launch_vr_ws_t<8, 1, false, 16, 256, 2>(a, s);
             if (a.e == 2) return launch_vr_ws_t<8, 2, false, 16, 256, 2>(a, s);
             // rebuild 3/4: 8-byte columns (8 rebuild waves, scalar tables): 4096 x 1 MiB
-            // 1.27 / 1.42 ms vs 1.35 / 1.58 with 16-byte columns (get_ab_waves.txt)
-            if (v == 0 && a.e == 3) return launch_vr_ws_t<8, 3, false, 16, 256, 1, 8, false, true>(a, s);
-            if (v == 0 && a.e == 4) return launch_vr_ws_t<8, 4, false, 16, 256, 1, 8, false, true>(a, s);
+            // 1.27 / 1.42 ms vs 1.35 / 1.58 with 16-byte columns (get_ab_waves.jsonl); batched scalar tables: 1.34 vs 1.40 ms for rebuild 4
+            if (v == 0 && a.e == 3) return launch_vr_ws_t<8, 3, false, 16, 256, 1, 8, false, true, true>(a, s);
+            if (v == 0 && a.e == 4) return launch_vr_ws_t<8, 4, false, 16, 256, 1, 8, false, true, true>(a, s);
 #if ZS3_DIAG
             if (a.e == 3) return launch_vr_ws_t<8, 3, false, 16, 256, 1>(a, s);
             if (a.e == 4) return launch_vr_ws_t<8, 4, false, 16, 256, 1>(a, s);

@@ -16,6 +16,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace zs3dev {
 
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
@@ -174,21 +176,40 @@ __device__ __forceinline__ int opaque_zero() {
 // PRS: lower the wave's issue priority by one after each block (progress-equalising
 // priority, fused_v2.hip PM = 4; the caller sets the starting priority).
 // ST: tables by scalar loads (ctabs, SGPR operands) instead of LDS (dtabs).
-template <int NWd, int K, int M, bool SB = true, bool PRS = false, bool ST = false>
-__device__ __forceinline__ void encode_dyadic(const Col<NWd> (&x)[K], Col<NWd> (&out)[M], const uint32_t* dtabs,
-                                              ctab_ptr ctabs = nullptr) {
+// XF: getx(j) returns data column j; called for a block's M columns at the start of the
+// block (a register array, or reads from LDS placed per block so that only one block's
+// columns are live).
+// H0: called once, after the first block's coefficient-table reads are issued and before
+// its arithmetic (scheduling barriers on both sides): LDS writes placed there do not sit
+// in front of the table reads in the in-order LDS counter.
+struct NoHook {
+    __device__ void operator()() const {}
+};
+// PRE: the K coefficient tables were read once into registers (pre[0..K-1]) before the
+// tile loop: no LDS reads (and no LDS-counter waits) inside the encode.
+template <int NWd, int K, int M, bool SB = true, bool PRS = false, bool ST = false, bool PRE = false, typename XF,
+          typename H0 = NoHook>
+__device__ __forceinline__ void encode_dyadic_f(XF&& getx, Col<NWd> (&out)[M], const uint32_t* dtabs,
+                                                ctab_ptr ctabs = nullptr, H0&& hook0 = NoHook{},
+                                                const CoefTab* pre = nullptr) {
     static_assert(M == 2 || M == 4, "dyadic block");
     uint32_t Y[M][NWd];
 #pragma unroll
     for (int q = 0; q < K / M; ++q) {
         if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
+        Col<NWd> xb[M];
+#pragma unroll
+        for (int i = 0; i < M; ++i) xb[i] = getx(q * M + i);
         if constexpr (PRS) {
             if (q == 1) __builtin_amdgcn_s_setprio(2);
             if (q == 2) __builtin_amdgcn_s_setprio(1);
             if (q > 0) __builtin_amdgcn_sched_barrier(0);
         }
         CoefTab t[M];
-        if constexpr (ST) {
+        if constexpr (PRE) {
+#pragma unroll
+            for (int i = 0; i < M; ++i) t[i] = pre[q * M + i];
+        } else if constexpr (ST) {
 #pragma unroll
             for (int i = 0; i < M; ++i) t[i] = load_coef_s(ctabs, q * M + i);
         } else {
@@ -196,13 +217,20 @@ __device__ __forceinline__ void encode_dyadic(const Col<NWd> (&x)[K], Col<NWd> (
 #pragma unroll
             for (int i = 0; i < M; ++i) t[i] = load_coef(tq, i);
         }
+        if constexpr (!std::is_same<std::decay_t<H0>, NoHook>::value) {
+            if (q == 0) {
+                __builtin_amdgcn_sched_barrier(0);
+                hook0();
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
         auto gf_lookup = [](const Nib& n, const CoefTab& c) { return ST ? gf_lookup_s(n, c) : zs3dev::gf_lookup(n, c); };
 #pragma unroll
         for (int w = 0; w < NWd; ++w) {
             if constexpr (M == 4) {
-                const uint32_t x3 = x[4 * q + 3].w[w];
-                const uint32_t X1 = x[4 * q + 1].w[w] ^ x3, X2 = x[4 * q + 2].w[w] ^ x3;
-                const uint32_t X0 = xor3(x[4 * q + 0].w[w], X1, x[4 * q + 2].w[w]);
+                const uint32_t x3 = xb[3].w[w];
+                const uint32_t X1 = xb[1].w[w] ^ x3, X2 = xb[2].w[w] ^ x3;
+                const uint32_t X0 = xor3(xb[0].w[w], X1, xb[2].w[w]);
                 const Nib n0 = split_nibbles(X0), n1 = split_nibbles(X1);
                 const Nib n2 = split_nibbles(X2), n3 = split_nibbles(x3);
                 const Prod3 P00 = gf_lookup(n0, t[0]), P01 = gf_lookup(n1, t[0]);
@@ -224,8 +252,8 @@ __device__ __forceinline__ void encode_dyadic(const Col<NWd> (&x)[K], Col<NWd> (
                                               P21.a, P21.b, P21.c, P30.a, P30.b, P30.c});
                 }
             } else {
-                const uint32_t x1 = x[2 * q + 1].w[w];
-                const uint32_t X0 = x[2 * q + 0].w[w] ^ x1;
+                const uint32_t x1 = xb[1].w[w];
+                const uint32_t X0 = xb[0].w[w] ^ x1;
                 const Nib n0 = split_nibbles(X0), n1 = split_nibbles(x1);
                 const Prod3 P00 = gf_lookup(n0, t[0]), P01 = gf_lookup(n1, t[0]), P10 = gf_lookup(n0, t[1]);
                 if (q == 0) {
@@ -250,6 +278,12 @@ __device__ __forceinline__ void encode_dyadic(const Col<NWd> (&x)[K], Col<NWd> (
             out[1].w[w] = Y[1][w];
         }
     }
+}
+
+template <int NWd, int K, int M, bool SB = true, bool PRS = false, bool ST = false>
+__device__ __forceinline__ void encode_dyadic(const Col<NWd> (&x)[K], Col<NWd> (&out)[M], const uint32_t* dtabs,
+                                              ctab_ptr ctabs = nullptr) {
+    encode_dyadic_f<NWd, K, M, SB, PRS, ST>([&](int j) { return x[j]; }, out, dtabs, ctabs);
 }
 
 // Scalar GF multiply with log/exp tables (generic byte path).

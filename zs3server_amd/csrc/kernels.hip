@@ -1496,7 +1496,8 @@ static hipError_t run_vr_k(const VrArgs& a, hipStream_t s, int* path) {
     // 1.41 -> 1.13 ms on 4096 x 1 MiB (scripts/get_ab.py).  Variants 200-209 (diagnostics)
     // force the first-generation kernel.
     // diagnostics 231: the product dispatch without the latency path
-    const int wv = (ZS3_DIAG && a.variant == 231) ? 0 : a.variant;
+    // diagnostics 240: the product dispatch without that path, batched scalar tables
+    const int wv = (ZS3_DIAG && (a.variant == 231 || a.variant == 240)) ? 0 : a.variant;
     if (wv == 0 || (ZS3_DIAG && ((wv >= 210 && wv <= 219) || wv == 232)))
         if (launch_vr_ws(wv, a, s)) {
             if (path) *path = PATH_WS;

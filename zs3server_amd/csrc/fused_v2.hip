@@ -903,18 +903,21 @@ static bool launch_ehx_t(const EncArgs& a, hipStream_t s) {
 // monotonically with the batch).  Data loads and parity stores of the 16-stripe
 // kernels carry the non-temporal cache policy (NTM = 3: each byte is touched once;
 // +2-3 % over the default policy at 4096-65536 stripes, profiles/r02/sweep_sizes_nt*.txt).
-//  RS(8+4)  n >= 2048: k_ehx_ws G = 16 (variant 151: 6 pair-form hash waves + 6 encode
+// The grid is one workgroup per CU: the stripes per workgroup G are the smallest that
+// keep ceil(n / G) <= 256 (a second, partial round of workgroups costs a whole
+// workgroup time: profiles/r02/sweep_cliffs.jsonl).
+//  RS(8+4)  n > 2048:  k_ehx_ws G = 16 (variant 151: 6 pair-form hash waves + 6 encode
 //                      waves with 16-byte columns, encode waves at s_setprio 1, nt policy;
 //                      one workgroup of 12 waves per CU)
-//           2048 <= n <= 2304: G = 8 (variant 130: 256-288 workgroups, one per CU)
-//           n < 2048:  PATH_NONE -> the first-generation kernel (4 stripes per
+//           1024 < n <= 2048: G = 8 (variant 130: 129-256 workgroups, one per CU)
+//           n <= 1024: PATH_NONE -> the first-generation kernel (4 stripes per
 //                      workgroup, quad-form hash lanes: more threads per stripe when
-//                      there are too few stripes to fill 256 CUs with 16 each)
-//  RS(16+4) n >= 2048: k_ehx_ws G = 8 (variant 162: 5 pair-form hash waves + 6 encode
+//                      there are too few stripes to fill 256 CUs with 8 each)
+//  RS(16+4) n > 1024:  k_ehx_ws G = 8 (variant 162: 5 pair-form hash waves + 6 encode
 //                      waves with 8-byte buffer-addressed columns, nt policy, data rows
 //                      written to LDS before the encode (EP = 2): 0.577 -> 0.590 of HBM
 //                      spec at 8192 stripes, profiles/r02/ab_encode_ep.jsonl)
-//           n <  2048: G = 4 with quad-form hash waves (variant 121)
+//           n <= 1024: G = 4 with quad-form hash waves (variant 121)
 //  RS(4+2)  n <= 2048: k_ehx_ws G = 4, quad-form hash waves, nt stores (variant 116;
 //                      BASELINE config 2: the hash chains' latency sets the pace)
 //           n >  2048: k_ehx_ws G = 16, pair-form hash waves, nt policy (variant 115)
@@ -922,12 +925,12 @@ template <int K, int M>
 static int launch_ehx_default(const EncArgs& a, hipStream_t s) {
     const int64_t n = a.n_blocks;
     if constexpr (K == 8 && M == 4) {
-        if (n >= 2048 && n <= 2304)
-            return launch_ws_t<K, M, 8, 384, 1, false, false, 0, false, 1>(a, s) ? PATH_WS : PATH_NONE;
-        if (n >= 2048)
+        if (n > 2048)
             return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3>(a, s) ? PATH_WS : PATH_NONE;
+        if (n > 1024)
+            return launch_ws_t<K, M, 8, 384, 1, false, false, 0, false, 1>(a, s) ? PATH_WS : PATH_NONE;
     } else if constexpr (K == 16 && M == 4) {
-        if (n >= 8 * 256)
+        if (n > 4 * 256)
             return launch_ws_t<K, M, 8, 384, 1, true, false, 0, false, 0, 0, false, 3, false, 2>(a, s) ? PATH_WS : PATH_NONE;
         return launch_ws_t<K, M, 4, 512, 1, true, true>(a, s) ? PATH_WS : PATH_NONE;
     } else if constexpr (K == 4 && M == 2) {

@@ -664,12 +664,13 @@ __global__ void __launch_bounds__(64) k_vr_hash_lat(VrArgs a, int nr) {
     }
 }
 
-// Crossover of the split path against the fused kernels (sweep_sizes_small.txt):
-// RS(8+4) between 512 and 768 blocks (~1 GB of stripes), RS(16+4) between 256 and 512.
+// Crossover of the split path against the fused kernels (sweep_sizes_small.txt,
+// sweep_cliffs.jsonl): RS(8+4) between 512 and 768 blocks (~1 GB of stripes), RS(16+4)
+// at 512 (448: 1516 vs 1463 GiB/s, 512: 1634 vs 1662).
 template <int K, int M>
 static bool small_batch(int64_t n_blocks, int64_t S) {
     if (K == 4 && M == 2) return false;
-    if (K == 16 && M == 4) return n_blocks <= 384;
+    if (K == 16 && M == 4) return n_blocks < 512;
     return n_blocks * (K + M) * S <= (int64_t)640 * 12 * 131072;
 }
 

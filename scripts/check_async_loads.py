@@ -198,6 +198,69 @@ def check(body, name):
     return bad
 
 
+def valu_sgpr_dests(code):
+    """SGPRs a VALU instruction writes: its first operand when that is an SGPR
+    (v_readlane / v_readfirstlane / v_cmp_*_e64 / v_*_co_* carry-out in VOP3b form take
+    the SGPR as destination), plus the carry-out of v_*_co_* / v_div_scale."""
+    op = code.split()[0]
+    if not op.startswith("v_"):
+        return set()
+    ops = [x.strip() for x in code[len(op):].split(",")]
+    out = set()
+    if ops and ops[0].startswith(("s", "vcc")):
+        out |= sregs(ops[0]) if ops[0].startswith("s") else {-1}
+    if ("_co_" in op or op.startswith("v_div_scale")) and len(ops) > 1:
+        if ops[1].startswith("s"):
+            out |= sregs(ops[1])
+        elif ops[1].startswith("vcc"):
+            out.add(-1)
+    return out
+
+
+def sgpr_hazards(body, name, report=True):
+    """gfx9 hazard the compiler does not guard for inline asm: a VALU write of an SGPR
+    read by a vector-memory instruction needs 5 wait states in between (the asm loads'
+    buffer resource / soffset / saddr).  Scans back over the linear instruction stream
+    (over-approximating across labels); s_nop N counts N + 1 states."""
+    insns = []
+    in_asm = False
+    for ln, raw in body:
+        t = raw.strip()
+        if t.startswith(";;#ASMSTART"):
+            in_asm = True
+            continue
+        if t.startswith(";;#ASMEND"):
+            in_asm = False
+            continue
+        code = t.split(";")[0].strip()
+        if not code or code.startswith(".") or code.endswith(":"):
+            continue
+        insns.append((ln, code, in_asm))
+    bad = 0
+    for i, (ln, code, is_asm) in enumerate(insns):
+        op = code.split()[0]
+        if not (is_asm and op.startswith(VMEM)):
+            continue
+        used = sregs(code[len(op):])
+        if not used:
+            continue
+        states, j = 0, i - 1
+        while j >= 0 and states < 5:
+            pc = insns[j][1]
+            pop = pc.split()[0]
+            w = valu_sgpr_dests(pc) & used
+            if w:
+                bad += 1
+                if report:
+                    print(f"{name}:{ln}: VALU SGPR write {sorted(w)} {states} wait states before asm VMEM: "
+                          f"{pc} -> {code}")
+                break
+            m = re.match(r"s_nop\s+(\d+)", pc)
+            states += int(m.group(1)) + 1 if m else 1
+            j -= 1
+    return bad
+
+
 def main():
     path = sys.argv[1]
     want = sys.argv[2] if len(sys.argv) > 2 else "k_ehx"
@@ -220,7 +283,7 @@ def main():
     for name, body in funcs:
         if want in name:
             n += 1
-            b = check(body, name[:70])
+            b = check(body, name[:70]) + sgpr_hazards(body, name[:70])
             total += b
             print(f"{name[:70]}: {b} violations")
     print(f"checked {n} kernels, {total} violations")

@@ -51,7 +51,7 @@ def test_untracked_loads_never_touched_in_flight(tmp_path, diag):
             cur[1].append((i, line))
     kernels = [(n, b) for n, b in funcs if "k_ehx" in n or "k_vr_ws" in n]
     assert kernels, "no k_ehx instance found in the assembly"
-    bad = {n: cal.check(b, n) for n, b in kernels}
+    bad = {n: cal.check(b, n) + cal.sgpr_hazards(b, n) for n, b in kernels}
     assert all(v == 0 for v in bad.values()), bad
 
 
@@ -90,3 +90,26 @@ def test_guard_specializes_loop_entered_flag():
     assert cal.check(_body(swapped), "bad") == 1
     unknown = LOOP_FLAG.replace("s_mov_b64 s[0:1], 0", "s_mov_b64 s[0:1], s[4:5]")
     assert cal.check(_body(unknown), "unknown") == 1
+
+
+HAZARD = """
+	v_readfirstlane_b32 s6, v4
+	;;#ASMSTART
+	buffer_load_dword v19, v2, s[28:31], s6 offen
+	;;#ASMEND
+"""
+
+
+def test_guard_flags_valu_sgpr_write_before_asm_vmem():
+    """A VALU write of an SGPR (v_readfirstlane / v_readlane spill restore) read by an
+    inline-asm buffer load needs 5 wait states (gfx9 hazard the compiler does not guard
+    for asm): reported without them, accepted after s_nop 4 or 5 other instructions, and
+    a compiler-emitted (non-asm) load is not the guard's business."""
+    import check_async_loads as cal
+    assert cal.sgpr_hazards(_body(HAZARD), "bad", report=False) == 1
+    nop = HAZARD.replace("\t;;#ASMSTART", "\ts_nop 4\n\t;;#ASMSTART")
+    assert cal.sgpr_hazards(_body(nop), "nop", report=False) == 0
+    other = HAZARD.replace("\t;;#ASMSTART", "\ts_add_u32 s0, s1, s2\n" * 5 + "\t;;#ASMSTART")
+    assert cal.sgpr_hazards(_body(other), "five", report=False) == 0
+    plain = HAZARD.replace("\t;;#ASMSTART\n", "").replace("\t;;#ASMEND\n", "")
+    assert cal.sgpr_hazards(_body(plain), "plain", report=False) == 0

@@ -1042,7 +1042,7 @@ constexpr int vr_nh() {
 // while batch i's 4 products are computed.  (Scalar loads return out of order, so every
 // wait is lgkmcnt(0); one table per wait serialises the rebuild on scalar-cache latency.)
 template <int K, int EX, bool HOUT, int G, int T, int PF, int CW = 16, bool HQ = false, bool ST = false,
-          bool BT = false>
+          int BT = 0>
 __global__ void __launch_bounds__((vr_nh<G, K + (HOUT ? EX : 0), HQ>() + G * (T / CW))) __attribute__((amdgpu_waves_per_eu(2)))
 k_vr_ws(VrArgs a) {
     constexpr int RH = K + (HOUT ? EX : 0);
@@ -1178,12 +1178,13 @@ k_vr_ws(VrArgs a) {
     uint8_t* blk = a.shards + b * a.block_stride + o;
     const int col_off = g * RH * TS + o;
     lds_barrier2();  // tables / rows visible
-    int64_t roff[K];
+    // row offsets in 32 bits (the launch requires (k + m) * S < 2^31): half the SGPRs
+    uint32_t roff[K];
 #pragma unroll
-    for (int j = 0; j < K; ++j) roff[j] = (int64_t)__builtin_amdgcn_readfirstlane(srows[j]) * S;
-    int64_t ooff[EX > 0 ? EX : 1];
+    for (int j = 0; j < K; ++j) roff[j] = (uint32_t)__builtin_amdgcn_readfirstlane(srows[j]) * (uint32_t)S;
+    uint32_t ooff[EX > 0 ? EX : 1];
 #pragma unroll
-    for (int r = 0; r < EX; ++r) ooff[r] = (int64_t)__builtin_amdgcn_readfirstlane(srows[K + r]) * S;
+    for (int r = 0; r < EX; ++r) ooff[r] = (uint32_t)__builtin_amdgcn_readfirstlane(srows[K + r]) * (uint32_t)S;
 
     VT x[PF][K];
     auto load = [&](VT (&xs)[K], int64_t t0) {
@@ -1204,7 +1205,7 @@ k_vr_ws(VrArgs a) {
             // opaque offset: the tables are reloaded per tile (scalar cache hits), not
             // hoisted out of the tile loop into e*k*5 SGPRs
             const ctab_ptr tg = const_tables(a.tables) + opaque_zero();
-            constexpr int NB = 4;  // BT: coefficients per scalar batch
+            constexpr int NB = BT > 0 ? BT : 4;  // BT: coefficients per scalar batch
             CoefTab tbat[2][NB];
             auto load_batch = [&](CoefTab (&d)[NB], int c0) {
 #pragma unroll
@@ -1302,20 +1303,22 @@ k_vr_ws(VrArgs a) {
     for (int p = 0; p < PF; ++p) vm_wait<0>(x[p]);
 }
 
-template <int K, int EX, bool HOUT, int G, int T, int PF, int CW, bool HQ, bool ST, bool BT>
+template <int K, int EX, bool HOUT, int G, int T, int PF, int CW, bool HQ, bool ST, int BT>
 static bool launch_vr_ws_bt(const VrArgs& a, hipStream_t s);
 
 template <int K, int EX, bool HOUT, int G, int T, int PF, int CW = 16, bool HQ = false, bool ST = false,
-          bool BT = false>
+          int BT = 0>
 static bool launch_vr_ws_t(const VrArgs& a, hipStream_t s) {
-    // diagnostics 240: the same launch with the scalar-table batching flipped (A/B)
+    // diagnostics 240: the same launch with the scalar-table batching flipped (off <-> 4
+    // coefficients per batch); 241: batches of 2
     if constexpr (ZS3_DIAG && ST) {
-        if (a.variant == 240) return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, !BT>(a, s);
+        if (a.variant == 240) return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, BT ? 0 : 4>(a, s);
+        if (a.variant == 241) return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, 2>(a, s);
     }
     return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, BT>(a, s);
 }
 
-template <int K, int EX, bool HOUT, int G, int T, int PF, int CW, bool HQ, bool ST, bool BT>
+template <int K, int EX, bool HOUT, int G, int T, int PF, int CW, bool HQ, bool ST, int BT>
 static bool launch_vr_ws_bt(const VrArgs& a, hipStream_t s) {
     constexpr int RH = K + (HOUT ? EX : 0);
     constexpr int NT = vr_nh<G, RH, HQ>() + G * (T / CW);
@@ -1326,6 +1329,7 @@ static bool launch_vr_ws_bt(const VrArgs& a, hipStream_t s) {
         return false;
     } else {
         if (a.e != EX || (a.S % 16) != 0 || a.k != K || (HOUT != (a.sums_out != nullptr) && EX > 0)) return false;
+        if ((int64_t)(a.k + a.m) * a.S >= ((int64_t)1 << 31)) return false;  // 32-bit row offsets
         auto kern = k_vr_ws<K, EX, HOUT, G, T, PF, CW, HQ, ST, BT>;
         if (ensure_dyn_lds((const void*)kern, dyn) != hipSuccess) return false;
         const int64_t grid = (a.n_blocks + G - 1) / G;
@@ -1379,9 +1383,9 @@ bool launch_vr_ws(int v, const VrArgs& a, hipStream_t s) {
         // 2048 x 1 MiB: heal 2/3/4 0.81/0.93/1.06 ms vs 0.82/0.99/1.17 with one table
         // per scalar wait and 0.95/1.13/1.31 for the first-generation kernel
         // (profiles/r02/get_ab_bt.jsonl, get_ab_waves.jsonl)
-        if (a.e == 2) return launch_vr_ws_t<16, 2, true, 8, 128, 1, 4, false, true, true>(a, s);
-        if (a.e == 3) return launch_vr_ws_t<16, 3, true, 8, 128, 1, 4, false, true, true>(a, s);
-        if (a.e == 4) return launch_vr_ws_t<16, 4, true, 8, 128, 1, 4, false, true, true>(a, s);
+        if (a.e == 2) return launch_vr_ws_t<16, 2, true, 8, 128, 1, 4, false, true, 4>(a, s);
+        if (a.e == 3) return launch_vr_ws_t<16, 3, true, 8, 128, 1, 4, false, true, 4>(a, s);
+        if (a.e == 4) return launch_vr_ws_t<16, 4, true, 8, 128, 1, 4, false, true, 4>(a, s);
         return false;
     }
     if ((v == 0 || v == 232) && a.k == 8 && a.sums_out != nullptr && a.e >= 3) {
@@ -1389,8 +1393,8 @@ bool launch_vr_ws(int v, const VrArgs& a, hipStream_t s) {
         // beside 4 rebuild waves, batched scalar tables; 4096 x 1 MiB: 1.41 / 1.61 ms vs
         // 1.49 / 1.79 unbatched and 2.01 / 2.32 for the first-generation kernel
         // (profiles/r02/get_ab_bt.jsonl, get_ab_waves.jsonl)
-        if (a.e == 3) return launch_vr_ws_t<8, 3, true, 16, 128, 2, 8, false, true, true>(a, s);
-        if (a.e == 4) return launch_vr_ws_t<8, 4, true, 16, 128, 2, 8, false, true, true>(a, s);
+        if (a.e == 3) return launch_vr_ws_t<8, 3, true, 16, 128, 2, 8, false, true, 4>(a, s);
+        if (a.e == 4) return launch_vr_ws_t<8, 4, true, 16, 128, 2, 8, false, true, 4>(a, s);
         return false;
     }
 #if ZS3_DIAG
@@ -1464,9 +1468,9 @@ bool launch_vr_ws(int v, const VrArgs& a, hipStream_t s) {
         // 9-wave workgroup inside 168 VGPRs (1.50 -> 1.25 ms, 1 data + 1 parity)
         // (scalar coefficient tables, variant 216: 1.28 -> 1.18 ms on 4096 x 1 MiB,
         // profiles/r02/get_ab.txt)
-        if ((v == 0 || v == 216) && a.e == 1) return launch_vr_ws_t<8, 1, true, 16, 128, 2, 8, false, true, true>(a, s);
+        if ((v == 0 || v == 216) && a.e == 1) return launch_vr_ws_t<8, 1, true, 16, 128, 2, 8, false, true, 4>(a, s);
         if (a.e != 2) return false;
-        if (v == 0 || v == 216) return launch_vr_ws_t<8, 2, true, 16, 128, 2, 8, false, true, true>(a, s);
+        if (v == 0 || v == 216) return launch_vr_ws_t<8, 2, true, 16, 128, 2, 8, false, true, 4>(a, s);
 #if ZS3_DIAG
         if (v == 212) return launch_vr_ws_t<8, 2, true, 16, 128, 2, 8>(a, s);
 #endif
@@ -1483,8 +1487,8 @@ bool launch_vr_ws(int v, const VrArgs& a, hipStream_t s) {
             if (a.e == 2) return launch_vr_ws_t<8, 2, false, 16, 256, 2>(a, s);
             // rebuild 3/4: 8-byte columns (8 rebuild waves, scalar tables): 4096 x 1 MiB
             // 1.27 / 1.42 ms vs 1.35 / 1.58 with 16-byte columns (get_ab_waves.jsonl); batched scalar tables: 1.34 vs 1.40 ms for rebuild 4
-            if (v == 0 && a.e == 3) return launch_vr_ws_t<8, 3, false, 16, 256, 1, 8, false, true, true>(a, s);
-            if (v == 0 && a.e == 4) return launch_vr_ws_t<8, 4, false, 16, 256, 1, 8, false, true, true>(a, s);
+            if (v == 0 && a.e == 3) return launch_vr_ws_t<8, 3, false, 16, 256, 1, 8, false, true, 4>(a, s);
+            if (v == 0 && a.e == 4) return launch_vr_ws_t<8, 4, false, 16, 256, 1, 8, false, true, 4>(a, s);
 #if ZS3_DIAG
             if (a.e == 3) return launch_vr_ws_t<8, 3, false, 16, 256, 1>(a, s);
             if (a.e == 4) return launch_vr_ws_t<8, 4, false, 16, 256, 1>(a, s);

@@ -106,9 +106,10 @@ RECON_PATTERNS = [
 
 @pytest.mark.parametrize("k,m,erased", RECON_PATTERNS)
 @pytest.mark.parametrize("data_only", [True, False])
-@pytest.mark.parametrize("variant", [0, 220, 221])
+@pytest.mark.parametrize("variant", [0, 220, 221, 222])
 def test_reconstruct_batch(oracle, k, m, erased, data_only, variant):
-    """variant 220/221: the reconstruct kernel with 2/4 columns per thread (e <= 2)."""
+    """variant 220/221: the reconstruct kernel with 2/4 columns per thread (e <= 2); 222:
+    non-temporal loads and stores."""
     with variant_ctx(variant):
         run_reconstruct_case(oracle, k, m, erased, data_only)
 
@@ -152,11 +153,17 @@ def test_reconstruct_errors():
 
 @pytest.mark.parametrize("lens", [list(range(0, 161)), [10, 10, 10, 5], [1 << 20, 131072, 131072 + 17, 999]])
 def test_hh256_batch_lengths(oracle, lens):
-    """Every HH remainder branch (size_mod32 = 0..31, & 16, & 3) vs the oracle."""
+    """Every HH remainder branch (size_mod32 = 0..31, & 16, & 3) vs the oracle, on
+    unaligned and 16-byte aligned strides."""
+    for align in (3, 16):
+        _hh256_lengths(oracle, lens, align)
+
+
+def _hh256_lengths(oracle, lens, align):
     rng = np.random.default_rng(len(lens))
     for L in sorted(set(lens)):
         n = 5
-        stride = max(L, 1) + 3  # unaligned stride
+        stride = max(L, 1) + 3 if align == 3 else -(-max(L, 1) // 16) * 16  # unaligned / aligned stride
         host = rng.integers(0, 256, n * stride, dtype=np.uint8)
         d = torch.from_numpy(host).to(DEV)
         out = torch.zeros(n * 32, dtype=torch.uint8, device=DEV)

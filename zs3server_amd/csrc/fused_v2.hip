@@ -1041,8 +1041,9 @@ constexpr int vr_nh() {
 // in SGPRs: batch i+1's s_loads are issued right after the wait for batch i and land
 // while batch i's 4 products are computed.  (Scalar loads return out of order, so every
 // wait is lgkmcnt(0); one table per wait serialises the rebuild on scalar-cache latency.)
+// NTL: non-temporal survivor loads and rebuilt-row stores.
 template <int K, int EX, bool HOUT, int G, int T, int PF, int CW = 16, bool HQ = false, bool ST = false,
-          int BT = 0>
+          int BT = 0, bool NTL = false>
 __global__ void __launch_bounds__((vr_nh<G, K + (HOUT ? EX : 0), HQ>() + G * (T / CW))) __attribute__((amdgpu_waves_per_eu(2)))
 k_vr_ws(VrArgs a) {
     constexpr int RH = K + (HOUT ? EX : 0);
@@ -1189,7 +1190,12 @@ k_vr_ws(VrArgs a) {
     VT x[PF][K];
     auto load = [&](VT (&xs)[K], int64_t t0) {
 #pragma unroll
-        for (int j = 0; j < K; ++j) ld_async<NWd>(xs[j], blk + roff[j] + t0);
+        for (int j = 0; j < K; ++j) {
+            if constexpr (NTL)
+                ld_async_nt<NWd>(xs[j], blk + roff[j] + t0);
+            else
+                ld_async<NWd>(xs[j], blk + roff[j] + t0);
+        }
     };
     auto prefetch_any = [&](VT (&xs)[K], int64_t tn) {
         const bool ok = tn < nfull || (tn == nfull && o < tail);
@@ -1265,7 +1271,12 @@ k_vr_ws(VrArgs a) {
     };
     auto store_rows = [&](const Col<NWd> (&y)[EX > 0 ? EX : 1], int64_t t0) {
 #pragma unroll
-        for (int r = 0; r < EX; ++r) st_col<NWd>(blk + ooff[r] + t0, y[r]);
+        for (int r = 0; r < EX; ++r) {
+            if constexpr (NTL)
+                st_col_nt<NWd>(blk + ooff[r] + t0, y[r]);
+            else
+                st_col<NWd>(blk + ooff[r] + t0, y[r]);
+        }
     };
     auto step = [&](VT (&xs)[K], int64_t ti) {
         Col<NWd> y[EX > 0 ? EX : 1];
@@ -1303,7 +1314,7 @@ k_vr_ws(VrArgs a) {
     for (int p = 0; p < PF; ++p) vm_wait<0>(x[p]);
 }
 
-template <int K, int EX, bool HOUT, int G, int T, int PF, int CW, bool HQ, bool ST, int BT>
+template <int K, int EX, bool HOUT, int G, int T, int PF, int CW, bool HQ, bool ST, int BT, bool NTL = false>
 static bool launch_vr_ws_bt(const VrArgs& a, hipStream_t s);
 
 template <int K, int EX, bool HOUT, int G, int T, int PF, int CW = 16, bool HQ = false, bool ST = false,
@@ -1312,13 +1323,19 @@ static bool launch_vr_ws_t(const VrArgs& a, hipStream_t s) {
     // diagnostics 240: the same launch with the scalar-table batching flipped (off <-> 4
     // coefficients per batch); 241: batches of 2
     if constexpr (ZS3_DIAG && ST) {
-        if (a.variant == 240) return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, BT ? 0 : 4>(a, s);
-        if (a.variant == 241) return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, 2>(a, s);
+        if (a.variant == 240) return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, (BT ? 0 : 4), true>(a, s);
+        if (a.variant == 241) return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, 2, true>(a, s);
     }
-    return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, BT>(a, s);
+    // Survivor loads and rebuilt-row stores are non-temporal (each byte is touched once):
+    // RS(8+4) verify 0.706 -> 0.627 ms, RS(16+4) verify 0.386 -> 0.351, rebuild 1-4 and
+    // heals 1-5 % faster (profiles/r02/ab_get_nt.jsonl).  Diagnostics 246: plain loads.
+    if constexpr (ZS3_DIAG) {
+        if (a.variant == 246) return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, BT, false>(a, s);
+    }
+    return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, BT, true>(a, s);
 }
 
-template <int K, int EX, bool HOUT, int G, int T, int PF, int CW, bool HQ, bool ST, int BT>
+template <int K, int EX, bool HOUT, int G, int T, int PF, int CW, bool HQ, bool ST, int BT, bool NTL>
 static bool launch_vr_ws_bt(const VrArgs& a, hipStream_t s) {
     constexpr int RH = K + (HOUT ? EX : 0);
     constexpr int NT = vr_nh<G, RH, HQ>() + G * (T / CW);
@@ -1330,7 +1347,7 @@ static bool launch_vr_ws_bt(const VrArgs& a, hipStream_t s) {
     } else {
         if (a.e != EX || (a.S % 16) != 0 || a.k != K || (HOUT != (a.sums_out != nullptr) && EX > 0)) return false;
         if ((int64_t)(a.k + a.m) * a.S >= ((int64_t)1 << 31)) return false;  // 32-bit row offsets
-        auto kern = k_vr_ws<K, EX, HOUT, G, T, PF, CW, HQ, ST, BT>;
+        auto kern = k_vr_ws<K, EX, HOUT, G, T, PF, CW, HQ, ST, BT, NTL>;
         if (ensure_dyn_lds((const void*)kern, dyn) != hipSuccess) return false;
         const int64_t grid = (a.n_blocks + G - 1) / G;
         hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), dyn, s, a);

@@ -58,6 +58,16 @@ __device__ __forceinline__ uint4 ld16(const uint8_t* p) {
     return v;
 }
 __device__ __forceinline__ void st16(uint8_t* p, const uint4& v) { __builtin_memcpy(p, &v, 16); }
+// Non-temporal forms (bytes streamed once: nt cache policy).  p must be 16-byte aligned.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ld16_nt(const uint8_t* p) {
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void st16_nt(uint8_t* p, const uint4& v) {
+    const u32x4 t = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(t, reinterpret_cast<u32x4*>(p));
+}
 
 
 constexpr int gcd_c(int a, int b) { return b ? gcd_c(b, a % b) : a; }
@@ -686,7 +696,9 @@ static void launch_encode_lat(const EncArgs& a, hipStream_t s) {
 
 // ---------------------------------------------------------------------------
 // Reconstruct: E_MAX output rows, each a GF combination of the K valid rows.
-template <int K, int EMAX, int NC = 1>
+// NTP: non-temporal survivor loads and rebuilt-row stores (launch: S % 16 == 0 and a
+// 16-byte aligned base, so every access is aligned).
+template <int K, int EMAX, int NC = 1, bool NTP = false>
 __global__ void __launch_bounds__(256) k_reconstruct(RecArgs a) {
     // NC columns per thread (256 apart, so every load instruction stays coalesced): all
     // NC*K survivor loads are issued before the first product (more bytes in flight).
@@ -708,7 +720,8 @@ __global__ void __launch_bounds__(256) k_reconstruct(RecArgs a) {
                 const int64_t c = c0 + 256 * i;
                 const int64_t o = (c < cols ? c : c0) * 16;
 #pragma unroll
-                for (int t = 0; t < K; ++t) x[i][t] = ld16(blk + (int64_t)rows[t] * S + o);
+                for (int t = 0; t < K; ++t)
+                    x[i][t] = NTP ? ld16_nt(blk + (int64_t)rows[t] * S + o) : ld16(blk + (int64_t)rows[t] * S + o);
             }
 #pragma unroll
             for (int i = 0; i < NC; ++i) {
@@ -740,7 +753,10 @@ __global__ void __launch_bounds__(256) k_reconstruct(RecArgs a) {
                     if (r < E) {
                         const uint4 p = make_uint4(acc_done(acc[r][0]), acc_done(acc[r][1]),
                                                    acc_done(acc[r][2]), acc_done(acc[r][3]));
-                        st16(blk + (int64_t)rows[K + r] * S + o, p);
+                        if (NTP)
+                            st16_nt(blk + (int64_t)rows[K + r] * S + o, p);
+                        else
+                            st16(blk + (int64_t)rows[K + r] * S + o, p);
                     }
                 }
             }
@@ -890,6 +906,8 @@ __device__ __forceinline__ MsgGeom msg_geom(const HashArgs& a, int64_t i) {
     return g;
 }
 
+// NTP: non-temporal loads for 16-byte aligned message columns (bytes read once).
+template <bool NTP = false>
 __global__ void __launch_bounds__(256) k_hash_batch(HashArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t tile[2][HB_CH * HB_TS];
     __shared__ int64_t s_len[HB_CH];
@@ -927,7 +945,7 @@ __global__ void __launch_bounds__(256) k_hash_batch(HashArgs a) {
             if (o < L) {
                 const uint8_t* src = rp[q] + t0 + o;
                 if (o + 16 <= L) {
-                    v[q] = ld16(src);
+                    v[q] = (NTP && ((uintptr_t)src & 15) == 0) ? ld16_nt(src) : ld16(src);
                 } else {
                     uint32_t w4[4] = {0, 0, 0, 0};
 #pragma unroll
@@ -1367,7 +1385,25 @@ static hipError_t run_rec_fast(const RecArgs& a, hipStream_t s) {
             hipLaunchKernelGGL((k_reconstruct<K, 2, 4>), dim3(gx2, gy), dim3(256), 0, s, a);
         return hipGetLastError();
     }
+    // 222: the default launch with plain (temporal) loads and stores
+    if (a.variant == 222) {
+        if (a.e <= 2)
+            hipLaunchKernelGGL((k_reconstruct<K, 2>), dim3(gx, gy), dim3(256), 0, s, a);
+        else
+            hipLaunchKernelGGL((k_reconstruct<K, 4>), dim3(gx, gy), dim3(256), 0, s, a);
+        return hipGetLastError();
+    }
 #endif
+    // Default: non-temporal survivor loads and rebuilt-row stores (each byte is touched
+    // once): RS(8+4) 4096 x 1 MiB {0,5} 1.016 -> 0.93 ms, {2,10} 0.905 -> 0.823 ms
+    // (profiles/r02/ab_reconstruct_nt.jsonl).  Needs 16-byte aligned rows.
+    if (((uintptr_t)a.shards & 15) == 0 && (a.block_stride & 15) == 0) {
+        if (a.e <= 2)
+            hipLaunchKernelGGL((k_reconstruct<K, 2, 1, true>), dim3(gx, gy), dim3(256), 0, s, a);
+        else
+            hipLaunchKernelGGL((k_reconstruct<K, 4, 1, true>), dim3(gx, gy), dim3(256), 0, s, a);
+        return hipGetLastError();
+    }
     if (a.e <= 2)
         hipLaunchKernelGGL((k_reconstruct<K, 2>), dim3(gx, gy), dim3(256), 0, s, a);
     else
@@ -1498,7 +1534,7 @@ static hipError_t run_vr_k(const VrArgs& a, hipStream_t s, int* path) {
     // force the first-generation kernel.
     // diagnostics 231: the product dispatch without the latency path
     // diagnostics 240: the product dispatch without that path, batched scalar tables
-    const int wv = (ZS3_DIAG && (a.variant == 231 || a.variant == 240 || a.variant == 241)) ? 0 : a.variant;
+    const int wv = (ZS3_DIAG && (a.variant == 231 || a.variant == 240 || a.variant == 241 || a.variant == 246)) ? 0 : a.variant;
     if (wv == 0 || (ZS3_DIAG && ((wv >= 210 && wv <= 219) || wv == 232)))
         if (launch_vr_ws(wv, a, s)) {
             if (path) *path = PATH_WS;
@@ -1602,7 +1638,9 @@ hipError_t launch_verify_reconstruct(const VrArgs& a, hipStream_t s, int* path) 
 hipError_t launch_hash(const HashArgs& a, hipStream_t s) {
     if (a.n <= 0) return hipSuccess;
     const int64_t grid = (a.n + HB_CH - 1) / HB_CH;
-    hipLaunchKernelGGL(k_hash_batch, dim3((unsigned)grid), dim3(256), 0, s, a);
+    // (non-temporal loads here measured 1.11 -> 1.28 ms for 49 152 x 128 KiB and 0.70 ->
+    // 1.28 ms for the deep scan: profiles/r02/ab_hash_nt.jsonl; not kept)
+    hipLaunchKernelGGL(k_hash_batch<false>, dim3((unsigned)grid), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

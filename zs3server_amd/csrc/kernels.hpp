@@ -89,6 +89,7 @@ struct HashArgs {
     int64_t chunk;            // chunked-file mode: shard size (0 = off)
     int64_t nchunks;          // chunks per file
     int64_t last_len;         // length of each file's last chunk
+    int variant;              // diagnostics build only (0 = tuned default)
 };
 
 // GET / heal pass: verify the k survivor shards the decode reads

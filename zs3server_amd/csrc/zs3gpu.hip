@@ -691,6 +691,7 @@ int zs3_hh256_batch(const uint8_t* key, const uint8_t* d_msgs, int64_t stride, i
                     uint8_t* d_sums, void* stream) {
     if (len < 0 || n < 0 || (n > 0 && !d_sums)) return ZS3_ERR_INVALID_ARG;
     zs3k::HashArgs a{};
+    a.variant = call_variant();
     a.msgs = d_msgs;
     a.stride = stride;
     a.len = len;
@@ -704,6 +705,7 @@ int zs3_hh256_verify_batch(const uint8_t* key, const uint8_t* d_msgs, int64_t st
                            const uint8_t* d_want, int32_t* d_bad, void* stream) {
     if (len < 0 || n < 0 || (n > 0 && (!d_want || !d_bad))) return ZS3_ERR_INVALID_ARG;
     zs3k::HashArgs a{};
+    a.variant = call_variant();
     a.msgs = d_msgs;
     a.stride = stride;
     a.len = len;
@@ -798,6 +800,7 @@ int zs3_hh256_batch_ragged(const uint8_t* key, const uint8_t* const* d_ptrs, con
                            uint8_t* d_sums, void* stream) {
     if (n < 0 || (n > 0 && (!d_ptrs || !d_lens || !d_sums))) return ZS3_ERR_INVALID_ARG;
     zs3k::HashArgs a{};
+    a.variant = call_variant();
     a.ptrs = d_ptrs;
     a.lens = d_lens;
     a.n = n;
@@ -821,6 +824,7 @@ int zs3_bitrot_verify_file_batch(const uint8_t* key, const uint8_t* d_files, int
     }
     if (!d_files || !d_bad || file_stride < want_size) return ZS3_ERR_INVALID_ARG;
     zs3k::HashArgs a{};
+    a.variant = call_variant();
     a.msgs = d_files;
     a.stride = file_stride;
     a.n = n_files * chunks;

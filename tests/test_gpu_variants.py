@@ -20,7 +20,7 @@ DEV = "cuda:0"
 # RS(8+4) fused_v2 tile = 384 B per shard row
 SIZES_84 = [8 * 16, 8 * 384, 8 * 384 * 3, 8 * (384 * 2 + 32), 8 * (384 * 5 + 16), 1 << 20]
 VARIANTS = [0, 49, 99, 50, 51, 52, 53, 55, 70, 71, 80, 81, 82, 83, 84, 100, 102, 103, 104, 105, 106, 107, 108, 109, 130,
-            140, 141, 150, 151, 152, 153, 154, 155, 156, 160, 163]
+            140, 141, 150, 151, 152, 153, 154, 155, 156, 160, 163, 133]
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -71,7 +71,7 @@ def test_rs84_variant_dead_stripes(oracle, variant, nb):
 
 
 @pytest.mark.parametrize("variant", [0, 49, 99, 50, 51, 55, 70, 82, 90, 91, 92, 93, 94, 110, 111, 112, 113, 114, 115, 116, 120, 121, 122, 123, 124,
-                                     157, 161, 162, 164])
+                                     157, 161, 162, 164, 117, 125])
 @pytest.mark.parametrize("k,m,blen", [(4, 2, 4 * 16), (4, 2, 4 * (384 * 3 + 48)), (4, 2, 1 << 20),
                                       (16, 4, 16 * 640 * 2), (16, 4, 1 << 20)])
 def test_other_shapes_variants(oracle, variant, k, m, blen):

@@ -909,7 +909,9 @@ static bool launch_ehx_t(const EncArgs& a, hipStream_t s) {
 //  RS(8+4)  n > 2048:  k_ehx_ws G = 16 (variant 151: 6 pair-form hash waves + 6 encode
 //                      waves with 16-byte columns, encode waves at s_setprio 1, nt policy;
 //                      one workgroup of 12 waves per CU)
-//           1024 < n <= 2048: G = 8 (variant 130: 129-256 workgroups, one per CU)
+//           1024 < n <= 2048: G = 8 (variant 133: 129-256 workgroups, one per CU, nt
+//                      loads and stores: 2048 stripes 0.737 -> 0.710 ms over variant 130,
+//                      profiles/r02/ab_encode_nt_small.jsonl)
 //           n <= 1024: PATH_NONE -> the first-generation kernel (4 stripes per
 //                      workgroup, quad-form hash lanes: more threads per stripe when
 //                      there are too few stripes to fill 256 CUs with 8 each)
@@ -917,9 +919,11 @@ static bool launch_ehx_t(const EncArgs& a, hipStream_t s) {
 //                      waves with 8-byte buffer-addressed columns, nt policy, data rows
 //                      written to LDS before the encode (EP = 2): 0.577 -> 0.590 of HBM
 //                      spec at 8192 stripes, profiles/r02/ab_encode_ep.jsonl)
-//           n <= 1024: G = 4 with quad-form hash waves (variant 121)
+//           n <= 1024: G = 4 with quad-form hash waves, nt loads and stores (variant
+//                      125; 1-2 % over 121)
 //  RS(4+2)  n <= 2048: k_ehx_ws G = 4, quad-form hash waves, nt stores (variant 116;
-//                      BASELINE config 2: the hash chains' latency sets the pace)
+//                      BASELINE config 2: the hash chains' latency sets the pace); nt loads
+//                      too from 1024 stripes (variant 117: config 2 0.410 -> 0.400 ms)
 //           n >  2048: k_ehx_ws G = 16, pair-form hash waves, nt policy (variant 115)
 template <int K, int M>
 static int launch_ehx_default(const EncArgs& a, hipStream_t s) {
@@ -928,12 +932,14 @@ static int launch_ehx_default(const EncArgs& a, hipStream_t s) {
         if (n > 2048)
             return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3>(a, s) ? PATH_WS : PATH_NONE;
         if (n > 1024)
-            return launch_ws_t<K, M, 8, 384, 1, false, false, 0, false, 1>(a, s) ? PATH_WS : PATH_NONE;
+            return launch_ws_t<K, M, 8, 384, 1, false, false, 0, false, 1, 0, false, 3>(a, s) ? PATH_WS : PATH_NONE;
     } else if constexpr (K == 16 && M == 4) {
         if (n > 4 * 256)
             return launch_ws_t<K, M, 8, 384, 1, true, false, 0, false, 0, 0, false, 3, false, 2>(a, s) ? PATH_WS : PATH_NONE;
-        return launch_ws_t<K, M, 4, 512, 1, true, true>(a, s) ? PATH_WS : PATH_NONE;
+        return launch_ws_t<K, M, 4, 512, 1, true, true, 0, false, 0, 0, false, 3>(a, s) ? PATH_WS : PATH_NONE;
     } else if constexpr (K == 4 && M == 2) {
+        if (n >= 1024 && n <= 8 * 256)
+            return launch_ws_t<K, M, 4, 512, 4, false, true, 83968, false, 0, 0, false, 3>(a, s) ? PATH_WS : PATH_NONE;
         if (n <= 8 * 256)
             return launch_ws_t<K, M, 4, 512, 4, false, true, 83968, false, 0, 0, false, 2>(a, s) ? PATH_WS : PATH_NONE;
         return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3>(a, s) ? PATH_WS : PATH_NONE;
@@ -982,6 +988,9 @@ static bool launch_ehx_km(int v, const EncArgs& a, hipStream_t s) {
         case 155: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, true>(a, s); else return false;
         case 153: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 2>(a, s); else return false;
         case 154: if constexpr (deep) return launch_ws_t<K, M, 8, 384, 1, false, false, 0, false, 1, 0, false, 2>(a, s); else return false;
+        case 117: if constexpr (few) return launch_ws_t<K, M, 4, 512, 4, false, true, 83968, false, 0, 0, false, 3>(a, s); else return false;
+        case 133: if constexpr (deep) return launch_ws_t<K, M, 8, 384, 1, false, false, 0, false, 1, 0, false, 3>(a, s); else return false;
+        case 125: if constexpr (K == 16 && M == 4) return launch_ws_t<K, M, 4, 512, 1, true, true, 0, false, 0, 0, false, 3>(a, s); else return false;
         case 156: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 1>(a, s); else return false;
         case 157: if constexpr (few) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 1>(a, s); else return false;
         case 160: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 2>(a, s); else return false;

@@ -523,7 +523,9 @@ __global__ void __launch_bounds__(NT) k_encode_hash_pipe(EncArgs a) {
 
 // ---------------------------------------------------------------------------
 // Encode only (no hash): one thread per 16-byte column, K loads -> M stores.
-template <int K, int M>
+// NTP: non-temporal data loads and parity stores (the encode-only call; not the
+// latency path, whose hash pass re-reads both from the cache).  Launch: 16-byte aligned.
+template <int K, int M, bool NTP = false>
 __global__ void __launch_bounds__(256) k_encode_only(EncArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t tabs[M * K * 8];
     for (int i = threadIdx.x; i < M * K * 8; i += 256) tabs[i] = a.tables[i];
@@ -538,7 +540,7 @@ __global__ void __launch_bounds__(256) k_encode_only(EncArgs a) {
             const uint32_t* tb = tabs + opaque_zero();
             uint4 x[K];
 #pragma unroll
-            for (int j = 0; j < K; ++j) x[j] = ld16(blk + (int64_t)j * S + o);
+            for (int j = 0; j < K; ++j) x[j] = NTP ? ld16_nt(blk + (int64_t)j * S + o) : ld16(blk + (int64_t)j * S + o);
             GfAcc acc[M][4];
 #pragma unroll
             for (int r = 0; r < M; ++r)
@@ -562,7 +564,10 @@ __global__ void __launch_bounds__(256) k_encode_only(EncArgs a) {
             for (int r = 0; r < M; ++r) {
                 const uint4 p = make_uint4(acc_done(acc[r][0]), acc_done(acc[r][1]),
                                            acc_done(acc[r][2]), acc_done(acc[r][3]));
-                st16(pb + (int64_t)r * S + o, p);
+                if (NTP)
+                    st16_nt(pb + (int64_t)r * S + o, p);
+                else
+                    st16(pb + (int64_t)r * S + o, p);
             }
         }
     }
@@ -1326,7 +1331,13 @@ static hipError_t run_encode_fast(const EncArgs& a, hipStream_t s, int* path) {
         const int64_t cols = (a.S + 15) >> 4;
         const unsigned gx = (unsigned)((cols + 255) / 256);
         const unsigned gy = (unsigned)(a.n_blocks < 65535 ? a.n_blocks : 65535);
-        hipLaunchKernelGGL((k_encode_only<K, M>), dim3(gx, gy), dim3(256), 0, s, a);
+        // non-temporal when every row is 16-byte aligned (diagnostics 98: plain)
+        const bool al = (((uintptr_t)a.data | (uintptr_t)a.parity | (uint64_t)a.data_stride |
+                          (uint64_t)a.parity_stride | (uint64_t)a.S) & 15) == 0;
+        if (al && !(ZS3_DIAG && a.variant == 98))
+            hipLaunchKernelGGL((k_encode_only<K, M, true>), dim3(gx, gy), dim3(256), 0, s, a);
+        else
+            hipLaunchKernelGGL((k_encode_only<K, M>), dim3(gx, gy), dim3(256), 0, s, a);
         p = PATH_FIRSTGEN;
     }
     if (path) *path = p;

@@ -1512,7 +1512,8 @@ bool launch_vr_ws(int v, const VrArgs& a, hipStream_t s) {
             if (a.e == 1) return launch_vr_ws_t<8, 1, false, 16, 256, 2>(a, s);
             if (a.e == 2) return launch_vr_ws_t<8, 2, false, 16, 256, 2>(a, s);
             // rebuild 3/4: 8-byte columns (8 rebuild waves, scalar tables): 4096 x 1 MiB
-            // 1.27 / 1.42 ms vs 1.35 / 1.58 with 16-byte columns (get_ab_waves.jsonl); batched scalar tables: 1.34 vs 1.40 ms for rebuild 4
+            // 1.27 / 1.42 ms vs 1.35 / 1.58 with 16-byte columns (get_ab_waves.jsonl);
+            // batched scalar tables: 1.34 vs 1.40 ms for rebuild 4
             if (v == 0 && a.e == 3) return launch_vr_ws_t<8, 3, false, 16, 256, 1, 8, false, true, 4>(a, s);
             if (v == 0 && a.e == 4) return launch_vr_ws_t<8, 4, false, 16, 256, 1, 8, false, true, 4>(a, s);
 #if ZS3_DIAG

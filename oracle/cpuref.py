@@ -4,9 +4,9 @@ v1.0.2, blocks sequential, encode split by byte range over T threads, then the k
 HighwayHash-256 sums; oracle/cpu_ref.cpp).
 
 TEST INFRASTRUCTURE ONLY: bench.py's cpu_baseline leg times it, and the full-size GPU
-tests use it as the fast checker of whole batches (it is cross-checked against the
-scalar oracle, oracle/zs3_oracle.c, in tests/test_oracle_kats.py).  Never used by the
-product path.
+tests use it as the fast checker of whole batches; tests/test_cpuref_pin.py pins its
+parity rows and sums byte for byte to the scalar oracle, oracle/zs3_oracle.c).  Never
+used by the product path.
 """
 from __future__ import annotations
 

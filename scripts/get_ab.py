@@ -1,5 +1,6 @@
 """A/B of the GET / heal kernel launch shapes on one device (variant 0 = default,
 200 = small-workgroup launch), interleaved rounds."""
+import contextlib
 import json
 import os
 import sys
@@ -39,11 +40,11 @@ for rnd in range(3):
     for erased, data_only, heal, label in cases:
         pres = [i not in erased for i in range(k + m)]
         for v in variants:
-            z.set_variant(v)
-            ms = timeit(lambda: codec.verify_reconstruct_batch(buf, stride, S, nobj, pres, data_only, sums, vbad,
-                                                               sums_out=hsum if heal else None))
+            with (z.diag(v) if v else contextlib.nullcontext()):
+                cv = z.Codec(k, m)  # a codec belongs to the library (product / diagnostics) that made it
+                ms = timeit(lambda: cv.verify_reconstruct_batch(buf, stride, S, nobj, pres, data_only, sums, vbad,
+                                                                sums_out=hsum if heal else None))
             e = len(erased)
             ab = nobj * (k * S + e * S + 32 * k + (32 * e if heal else 0))
             print(json.dumps({"round": rnd, "case": label, "variant": v, "ms": round(ms, 4),
                               "hbm_frac": round(ab / ms / 1e6 / 8000, 3), "bad": int(vbad.sum())}), flush=True)
-z.set_variant(0)

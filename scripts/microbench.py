@@ -12,11 +12,13 @@ import zs3server_amd as z  # noqa: E402
 k, m, blen, nobj = 8, 4, 1 << 20, int(os.environ.get("MB_OBJ", "4096"))
 S = blen // k
 stride = (k + m) * S
+_V = int(os.environ.get("MB_VARIANT", "0"))
+if _V:
+    z.diag(_V).__enter__()  # this thread runs on the diagnostics build with variant _V
 codec = z.Codec(k, m)
 buf = torch.empty(nobj * stride, dtype=torch.uint8, device="cuda")
 sums = torch.empty(nobj * (k + m) * 32, dtype=torch.uint8, device="cuda")
 z.fill_batch(buf, stride, blen, nobj, seed=5)
-z.set_variant(int(os.environ.get("MB_VARIANT", "0")))
 
 
 def timeit(fn, steps=10):

@@ -23,7 +23,9 @@ G = 4
 nwave = nobj // G * 3
 dbg = torch.zeros(nwave * 5, dtype=torch.int64, device="cuda")
 for v in [int(x) for x in os.environ.get("VARIANTS", "50").split(",")]:
-    z.set_variant(v)
+    ctx = z.diag(v)
+    ctx.__enter__()
+    codec = z.Codec(k, m)  # a codec belongs to the library that made it
     z.set_debug_buffer(None)
     for _ in range(3):
         codec.encode_batch(buf, st, blen, nobj, parity=buf, parity_offset=k * S, parity_stride=st, sums=sums)
@@ -76,5 +78,5 @@ for v in [int(x) for x in os.environ.get("VARIANTS", "50").split(",")]:
     for n in sorted(set(int(t) for t in load)):
         sel = load == n
         print(f"  CUs with {n} waves: wave life mean {float(life[sel].mean()):.1f} us")
-z.set_debug_buffer(None)
-z.set_variant(0)
+    z.set_debug_buffer(None)
+    ctx.__exit__(None, None, None)

@@ -1,0 +1,238 @@
+"""Parity on exactly the workloads the measured numbers come from (bench.py).
+
+* BASELINE config 4 as bench.py runs it: the N = 1 share (65 536 x 1 MiB RS(8+4)
+  objects, one launch, seed 1234) and an N = 2 share (32 768 objects starting at object
+  32 768), every parity byte and bitrot sum compared chunk by chunk with cpu_ref
+  (itself pinned to the scalar oracle by tests/test_cpuref_pin.py), three blocks per
+  share against the scalar oracle.
+* The profiled GET / heal shapes: 1 MiB blocks, RS(8+4) x 4 096 and RS(16+4) x 2 048
+  stripes through the product dispatch (k_vr_ws): verify + rebuild 2, heal 2 and
+  heal 4, every rebuilt row and heal sum against oracle stripes.
+* SURVEY.md §8(d) synthetic edge inputs: all-zero and all-0xFF batches at the BASELINE
+  shapes RS(4+2) x 1 024, RS(8+4) x 4 096 and RS(16+4) x 2 048, encode + sums and a
+  reconstruct round trip.
+* Per-block erasure patterns on the warp-specialised GET kernel (block-id lists through
+  k_vr_ws, groups larger than the small-batch path takes).
+
+Reference: cmd/erasure-encode.go:83-111, cmd/erasure-coding.go:77-119,
+cmd/bitrot-streaming.go:43-65, 142-189, cmd/erasure-decode.go:165-179, 287-332.
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+import zs3server_amd as z  # noqa: E402
+from oracle import cpuref  # noqa: E402
+
+KEY = z.MAGIC_HH256_KEY
+DEV = "cuda:0"
+MiB = 1 << 20
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    z.lib()
+
+
+@pytest.fixture(autouse=True)
+def _release_cache():
+    yield
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()  # the tests' multi-GiB buffers are garbage once they return
+
+
+def chunked_check(oracle, k, m, d, sums, nb, S, seed, obj0, chunk=1024, samples=3):
+    """Every block's parity rows and sums vs cpu_ref on the same data rows, chunk by
+    chunk (np.array_equal), plus `samples` blocks vs the scalar oracle from oracle_fill."""
+    R = k + m
+    mat = oracle.build_matrix(k, m)
+    T = cpuref.threads_available()
+    for b0 in range(0, nb, chunk):
+        n = min(chunk, nb - b0)
+        blk = d[b0 * R * S:(b0 + n) * R * S].cpu().numpy()
+        sm = sums[b0 * R * 32:(b0 + n) * R * 32].cpu().numpy()
+        par = np.empty(n * m * S, np.uint8)
+        sref = np.empty(n * R * 32, np.uint8)
+        cpuref.encode_hash(k, m, mat, blk, k * S, n, R * S, par, m * S, sref, KEY, T)
+        assert np.array_equal(blk.reshape(n, R, S)[:, k:], par.reshape(n, m, S)), f"parity, blocks {b0}..{b0 + n}"
+        assert np.array_equal(sm, sref), f"sums, blocks {b0}..{b0 + n}"
+    for b in np.linspace(0, nb - 1, samples).astype(int).tolist():
+        v = d[b * R * S:(b + 1) * R * S].cpu().numpy().reshape(R, S)
+        want = oracle.encode_data(k, m, oracle.fill(seed, obj0 + b, k * S), mat)
+        assert np.array_equal(v, want), b
+        assert np.array_equal(sums[b * R * 32:(b + 1) * R * 32].cpu().numpy().reshape(R, 32),
+                              oracle.hh256_rows(KEY, want)), b
+
+
+@pytest.mark.parametrize("nb,obj0", [(65536, 0), (32768, 32768)], ids=["N1-share", "N2-rank1-share"])
+def test_config4_bench_share(oracle, nb, obj0):
+    """bench.py's own sequence (fill_batch seed 1234 at the rank's first object, one
+    encode_batch over the share in the in-place layout) on the N = 1 and N = 2 shares."""
+    k, m = 8, 4
+    S = MiB // k
+    R = k + m
+    codec = z.Codec(k, m, MiB)
+    d = torch.empty(nb * R * S, dtype=torch.uint8, device=DEV)
+    sums = torch.zeros(nb * R * 32, dtype=torch.uint8, device=DEV)
+    z.fill_batch(d, R * S, MiB, nb, seed=1234, obj0=obj0)
+    codec.encode_batch(d, R * S, MiB, nb, parity=d, parity_offset=k * S, parity_stride=R * S, sums=sums)
+    torch.cuda.synchronize()
+    assert z.last_path() == 2, "config 4 runs on the warp-specialised kernel"
+    chunked_check(oracle, k, m, d, sums, nb, S, 1234, obj0)
+
+
+@pytest.mark.parametrize("k,m,nb", [(4, 2, 1024), (16, 4, 2048), (8, 4, 4096)])
+def test_profiled_encode_shapes_full_check(oracle, k, m, nb):
+    """BASELINE config 2 (RS(4+2) x 1 024), RS(16+4) x 2 048 and config 3's encode
+    (RS(8+4) x 4 096) as profiled: every parity byte and sum vs cpu_ref."""
+    S = MiB // k
+    R = k + m
+    codec = z.Codec(k, m, MiB)
+    d = torch.empty(nb * R * S, dtype=torch.uint8, device=DEV)
+    sums = torch.zeros(nb * R * 32, dtype=torch.uint8, device=DEV)
+    z.fill_batch(d, R * S, MiB, nb, seed=42, obj0=0)
+    codec.encode_batch(d, R * S, MiB, nb, parity=d, parity_offset=k * S, parity_stride=R * S, sums=sums)
+    torch.cuda.synchronize()
+    assert z.last_path() == 2
+    chunked_check(oracle, k, m, d, sums, nb, S, 42, 0)
+
+
+def _tiled_stripes(oracle, k, m, blen, nb, seed, distinct=64):
+    R = k + m
+    S = -(-blen // k)
+    mat = oracle.build_matrix(k, m)
+    base = np.stack([oracle.encode_data(k, m, oracle.fill(seed, b, blen), mat).reshape(R, S)
+                     for b in range(distinct)])
+    bsum = np.stack([oracle.hh256_rows(KEY, s) for s in base])
+    reps = nb // distinct
+    return base, bsum, reps
+
+
+@pytest.mark.parametrize("k,m,nb,erased,heal", [
+    (8, 4, 4096, [0, 5], False), (8, 4, 4096, [2, 10], True), (8, 4, 4096, [1, 3, 8, 11], True),
+    (16, 4, 2048, [0, 5], False), (16, 4, 2048, [3, 17], True), (16, 4, 2048, [0, 1, 16, 19], True),
+    (16, 4, 2048, [2, 7, 9, 12], False),
+], ids=lambda v: str(v))
+def test_get_heal_profiled_shape(oracle, k, m, nb, erased, heal):
+    """GET (verify the survivors + rebuild the lost data rows) and heal (rebuild every
+    lost row + hash it) at the profiled shape: 1 MiB blocks, product dispatch, one
+    rotted survivor flagged exactly."""
+    R = k + m
+    base, bsum, reps = _tiled_stripes(oracle, k, m, MiB, nb, seed=17)
+    S = base.shape[2]
+    codec = z.Codec(k, m, MiB)
+    d = torch.from_numpy(base).to(DEV).repeat(reps, 1, 1).contiguous()
+    for e in erased:
+        d[:, e, :] = 0x5A
+    surv = [i for i in range(R) if i not in erased][:k]
+    bad_blk, bad_row = nb - 3, surv[-1]
+    d[bad_blk, bad_row, 12345] ^= 1
+    exp = torch.from_numpy(bsum).to(DEV).repeat(reps, 1, 1).contiguous()
+    bad = torch.full((nb, R), 7, dtype=torch.int32, device=DEV)
+    out = torch.zeros((nb, R, 32), dtype=torch.uint8, device=DEV) if heal else None
+    present = [i not in erased for i in range(R)]
+    codec.verify_reconstruct_batch(d, R * S, S, nb, present, not heal, exp, bad, sums_out=out)
+    torch.cuda.synchronize()
+    assert z.last_path() == 2, "profiled shape runs k_vr_ws"
+    want_bad = np.zeros((nb, R), np.int32)
+    want_bad[bad_blk, bad_row] = 1
+    assert np.array_equal(bad.cpu().numpy(), want_bad)
+    rebuilt = [i for i in erased if i < k or heal]
+    ok = torch.ones(nb, dtype=torch.bool, device=DEV)
+    ok[bad_blk] = False  # rebuilt from a rotted survivor: garbage by design
+    ref = torch.from_numpy(base).to(DEV)
+    refs = torch.from_numpy(bsum).to(DEV)
+    dv = d.view(reps, 64, R, S)
+    okv = ok.view(reps, 64)
+    for i in rebuilt:
+        same = (dv[:, :, i, :] == ref[None, :, i, :]).all(dim=2)
+        assert bool(same[okv].all()), f"rebuilt shard {i}"
+        if heal:
+            sv = out.view(reps, 64, R, 32)[:, :, i, :]
+            assert bool((sv == refs[None, :, i, :]).all(dim=2)[okv].all()), f"heal sum of shard {i}"
+    for i in range(R):
+        if i in erased and i not in rebuilt:
+            assert bool((dv[:, :, i, :] == 0x5A).all()), "ReconstructData leaves lost parity untouched"
+
+
+@pytest.mark.parametrize("fillv", [0x00, 0xFF], ids=["zero", "ff"])
+@pytest.mark.parametrize("k,m,nb", [(4, 2, 1024), (8, 4, 4096), (16, 4, 2048), (8, 4, 300)])
+def test_constant_input_batches(oracle, k, m, nb, fillv):
+    """All-zero and all-0xFF objects through the default encode dispatch
+    of each BASELINE shape, then ReconstructData of two lost data rows and heal of a
+    lost parity row; every block equals the oracle's encode of one such block."""
+    R = k + m
+    S = MiB // k
+    codec = z.Codec(k, m, MiB)
+    d = torch.full((nb, R, S), fillv, dtype=torch.uint8, device=DEV)
+    d[:, k:, :] = 0x3C
+    sums = torch.zeros((nb, R, 32), dtype=torch.uint8, device=DEV)
+    codec.encode_batch(d, R * S, MiB, nb, parity=d, parity_offset=k * S, parity_stride=R * S, sums=sums)
+    torch.cuda.synchronize()
+    want = oracle.encode_data(k, m, np.full(MiB, fillv, np.uint8))
+    wsum = oracle.hh256_rows(KEY, want)
+    wt = torch.from_numpy(want).to(DEV)
+    assert bool((d == wt[None]).all()), "parity"
+    assert bool((sums == torch.from_numpy(wsum).to(DEV)[None]).all()), "sums"
+    erased = [1, k - 1]
+    for e in erased:
+        d[:, e, :] = 0x11
+    codec.reconstruct_batch(d, R * S, S, nb, [i not in erased for i in range(R)], True)
+    d[:, k, :] = 0x22
+    codec.reconstruct_batch(d, R * S, S, nb, [i != k for i in range(R)], False)
+    torch.cuda.synchronize()
+    assert bool((d == wt[None]).all()), "reconstruct round trip"
+
+
+@pytest.mark.parametrize("k,m,blen", [(8, 4, 1 << 16), (16, 4, 1 << 16)])
+@pytest.mark.parametrize("heal", [False, True])
+def test_masks_on_ws_kernel(oracle, k, m, blen, heal):
+    """Per-block patterns whose groups exceed the small-batch path (> 2 048 blocks per
+    pattern), so every group runs k_vr_ws with its block-id list: three
+    interleaved patterns over 7 680 blocks, one rotted survivor flagged exactly."""
+    R = k + m
+    nb = 7680
+    base, bsum, reps = _tiled_stripes(oracle, k, m, blen, nb, seed=23)
+    S = base.shape[2]
+    pats_list = [[0, 5], [k, R - 1], [2]] if not heal else [[0, 5], [k, R - 1], [2, k + 1]]
+    rng = np.random.default_rng(k + heal)
+    which = rng.integers(0, len(pats_list), nb)
+    pats = np.ones((nb, R), dtype=bool)
+    for b in range(nb):
+        pats[b, pats_list[which[b]]] = False
+    d = torch.from_numpy(base).to(DEV).repeat(reps, 1, 1).contiguous()
+    pt = torch.from_numpy(pats).to(DEV)
+    d[~pt] = 0x66
+    rb = 4000
+    surv = [i for i in range(R) if pats[rb, i]][:k]
+    d[rb, surv[0], S - 1] ^= 0x80
+    exp = torch.from_numpy(bsum).to(DEV).repeat(reps, 1, 1).contiguous()
+    bad = torch.full((nb, R), 9, dtype=torch.int32, device=DEV)
+    out = torch.zeros((nb, R, 32), dtype=torch.uint8, device=DEV) if heal else None
+    codec = z.Codec(k, m, blen)
+    status = np.full(nb, 99, np.int32)
+    rc = codec.verify_reconstruct_batch_masks(d, R * S, S, nb, pats, not heal, exp, bad, sums_out=out, status=status)
+    torch.cuda.synchronize()
+    assert rc == 0 and not status.any()
+    assert z.last_path() == 2, "large pattern groups run k_vr_ws"
+    want_bad = np.zeros((nb, R), np.int32)
+    want_bad[rb, surv[0]] = 1
+    assert np.array_equal(bad.cpu().numpy(), want_bad)
+    ref = torch.from_numpy(base).to(DEV).repeat(reps, 1, 1)
+    ok = torch.ones(nb, dtype=torch.bool, device=DEV)
+    ok[rb] = False
+    rows_ok = (d == ref).all(dim=2)  # [nb, R]
+    expect_rows = pt.clone()
+    expect_rows[:, :k] = True
+    if heal:
+        expect_rows[:] = True
+    assert bool(rows_ok[ok][expect_rows[ok]].all()), "rebuilt rows"
+    if heal:
+        lost = ~pt
+        eq = (out == exp).all(dim=2)
+        assert bool(eq[ok][lost[ok]].all()), "heal sums of the rebuilt rows"

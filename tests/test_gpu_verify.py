@@ -350,9 +350,12 @@ def test_reconstruct_batch_masks(oracle, k, m, blen, data_only):
 
 @pytest.mark.parametrize("k,m,blen", MASK_SHAPES)
 @pytest.mark.parametrize("heal", [False, True])
-def test_verify_reconstruct_batch_masks(oracle, k, m, blen, heal):
+@pytest.mark.parametrize("variant", [0, 231])
+def test_verify_reconstruct_batch_masks(oracle, k, m, blen, heal, variant):
     """GET / heal pass with per-block patterns: survivors verified per block (one rotted
-    survivor flagged exactly), missing shards rebuilt, heal sums of the rebuilt shards."""
+    survivor flagged exactly), missing shards rebuilt, heal sums of the rebuilt shards.
+    231: the product dispatch without the small-batch path, so the block-id lists of
+    the RS(8+4) / RS(16+4) groups go through k_vr_ws."""
     nb = 41
     rng = np.random.default_rng(k * 7 + m)
     sh, sums = stripes(oracle, k, m, blen, nb, seed=13)
@@ -373,9 +376,12 @@ def test_verify_reconstruct_batch_masks(oracle, k, m, blen, heal):
     bad = torch.full((nb, R), 9, dtype=torch.int32, device=DEV)
     out = torch.zeros((nb, R, 32), dtype=torch.uint8, device=DEV) if heal else None
     status = np.full(nb, 99, np.int32)
-    rc = codec.verify_reconstruct_batch_masks(d, R * S, S, nb, pats, not heal, exp, bad, sums_out=out,
-                                              status=status)
-    torch.cuda.synchronize()
+    with variant_ctx(variant):
+        if variant:
+            codec = z.Codec(k, m)
+        rc = codec.verify_reconstruct_batch_masks(d, R * S, S, nb, pats, not heal, exp, bad, sums_out=out,
+                                                  status=status)
+        torch.cuda.synchronize()
     assert rc == 0 and not status.any()
     want_bad = np.zeros((nb, R), np.int32)
     want_bad[rb, surv[0]] = 1

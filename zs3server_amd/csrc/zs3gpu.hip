@@ -23,7 +23,7 @@
 #if ZS3_DIAG
 #include "../../include/zs3gpu_diag.h"
 #endif
-#include "gf256.hpp"
+#include "codec_host.hpp"
 #include "kernels.hpp"
 
 namespace {
@@ -80,26 +80,16 @@ struct DevBuf {
     }
 };
 
-// Cached reconstruct plan for one erasure pattern.
-struct RecPlan {
-    int status = ZS3_OK;          // error for this pattern, or OK
-    bool noop = false;
-    int e = 0;
-    std::vector<int32_t> rows;    // k valid rows, then e output rows
-    std::vector<uint8_t> coef;    // e x k
-    std::vector<uint32_t> tables; // e x k x 8
+// Cached reconstruct plan for one erasure pattern (host part: codec_host.hpp).
+struct RecPlan : zs3::PlanData {
     std::map<int, std::shared_ptr<DevBuf>> dev;  // device -> [tables | coef | rows]
 };
 
 }  // namespace
 
-struct zs3_codec {
+struct zs3_codec : zs3::CodecTables {
     int k, m;
     int64_t block_size;
-    std::vector<uint8_t> matrix;   // (k+m) x k
-    std::vector<uint32_t> tables;  // m x k x 8 (parity rows), then dyadic tables if dyb
-    int dyb = 0;                   // 2 or 4 when the parity block is dyadic (see below)
-    size_t dyadic_off = 0;         // dword offset of the dyadic tables in `tables`
     std::mutex mu;
     std::map<int, std::shared_ptr<DevBuf>> dev;  // device -> [tables | matrix]
     std::map<std::string, std::shared_ptr<RecPlan>> plans;
@@ -132,57 +122,7 @@ int codec_device(zs3_codec* c, const uint32_t** tabs, const uint8_t** mat) {
 // reedsolomon reconstruct() argument checks + inversion for one pattern.
 std::shared_ptr<RecPlan> make_plan(const zs3_codec* c, const uint8_t* present, int data_only) {
     auto p = std::make_shared<RecPlan>();
-    const int k = c->k, n = c->k + c->m;
-    int np = 0, dp = 0;
-    for (int i = 0; i < n; ++i)
-        if (present[i]) {
-            ++np;
-            if (i < k) ++dp;
-        }
-    if (np == 0) {
-        p->status = ZS3_ERR_SHARD_NO_DATA;
-        return p;
-    }
-    std::vector<int32_t> valid;  // the k shards ReconstructData reads
-    for (int i = 0; i < n && (int)valid.size() < k; ++i)
-        if (present[i]) valid.push_back(i);
-    if (np == n || (data_only && dp == k)) {
-        p->noop = true;
-        p->rows = valid;  // verify-only pass (zs3_verify_reconstruct_batch)
-        return p;
-    }
-    if (np < k) {
-        p->status = ZS3_ERR_TOO_FEW_SHARDS;
-        return p;
-    }
-    std::vector<uint8_t> sub((size_t)k * k), dec((size_t)k * k);
-    for (int r = 0; r < k; ++r) std::memcpy(&sub[(size_t)r * k], &c->matrix[(size_t)valid[r] * k], k);
-    if (!zs3::gf_invert(sub.data(), k, dec.data())) {
-        p->status = ZS3_ERR_SINGULAR;
-        return p;
-    }
-    const zs3::GF& g = zs3::gf();
-    p->rows = valid;
-    for (int d = 0; d < k; ++d) {
-        if (present[d]) continue;
-        p->rows.push_back(d);
-        p->coef.insert(p->coef.end(), &dec[(size_t)d * k], &dec[(size_t)d * k] + k);
-    }
-    if (!data_only) {
-        // missing parity row p = M[p] * data = (M[p] * dec) * valid rows
-        for (int r = k; r < n; ++r) {
-            if (present[r]) continue;
-            p->rows.push_back(r);
-            for (int t = 0; t < k; ++t) {
-                uint8_t acc = 0;
-                for (int j = 0; j < k; ++j) acc ^= g.mul(c->matrix[(size_t)r * k + j], dec[(size_t)j * k + t]);
-                p->coef.push_back(acc);
-            }
-        }
-    }
-    p->e = (int)p->rows.size() - k;
-    p->tables.assign((size_t)p->e * k * 8, 0);
-    for (int i = 0; i < p->e * k; ++i) zs3::perm_tables(p->coef[i], &p->tables[(size_t)i * 8]);
+    zs3::make_plan_data(c->k, c->m, c->matrix.data(), present, data_only, *p);
     return p;
 }
 
@@ -221,51 +161,70 @@ int plan_device(zs3_codec* c, RecPlan* p, const uint32_t** tabs, const uint8_t**
     return ZS3_OK;
 }
 
-// Per-OS-thread pinned staging for block-id lists (per-block erasure patterns): the
-// list is copied into pinned memory, then stream-ordered into a hipMallocAsync'd
-// device buffer that is freed (hipFreeAsync) behind the kernels that read it.
+// Block-id lists of the per-block-pattern calls (zs3_*_batch_masks): every group's ids
+// go into ONE pinned staging slot per call, then one stream-ordered copy into a
+// hipMallocAsync'd device buffer that is freed (hipFreeAsync) behind the kernels that
+// read it.  Each OS thread keeps a small ring of slots per device, so a call waits
+// only for the copy out of the slot it reuses (kIdsSlots calls back), never for its
+// own or the previous call's copy queued behind a large H2D on the same stream.
+constexpr int kIdsSlots = 4;
 struct IdsStage {
-    int32_t* h = nullptr;
-    size_t cap = 0;
-    hipEvent_t ev = nullptr;  // last copy out of h
+    int32_t* h[kIdsSlots] = {};
+    size_t cap[kIdsSlots] = {};
+    hipEvent_t ev[kIdsSlots] = {};  // last copy out of h[i]
+    bool used[kIdsSlots] = {};
+    int next = 0;
     ~IdsStage() {
-        if (ev) (void)hipEventDestroy(ev);
-        if (h) (void)hipHostFree(h);
+        for (int i = 0; i < kIdsSlots; ++i) {
+            if (ev[i]) (void)hipEventDestroy(ev[i]);
+            if (h[i]) (void)hipHostFree(h[i]);
+        }
     }
 };
 thread_local std::map<int, std::unique_ptr<IdsStage>> t_ids;
-
-int upload_ids(const int32_t* ids, size_t n, hipStream_t s, int32_t** d_out) {
-    const int d = current_device();
-    if (d < 0) return ZS3_ERR_DEVICE;
-    auto& sp = t_ids[d];
-    if (!sp) {
-        sp.reset(new IdsStage());
-        if (hipEventCreateWithFlags(&sp->ev, hipEventDisableTiming) != hipSuccess) return ZS3_ERR_DEVICE;
-    } else if (hipEventSynchronize(sp->ev) != hipSuccess) {  // the previous copy out of h is done
-        return ZS3_ERR_DEVICE;
-    }
-    const size_t bytes = n * sizeof(int32_t);
-    if (sp->cap < bytes) {
-        if (sp->h) (void)hipHostFree(sp->h);
-        sp->h = nullptr;
-        sp->cap = 0;
-        if (hipHostMalloc((void**)&sp->h, bytes, hipHostMallocDefault) != hipSuccess) return ZS3_ERR_NOMEM;
-        sp->cap = bytes;
-    }
-    std::memcpy(sp->h, ids, bytes);
-    if (hipMallocAsync((void**)d_out, bytes, s) != hipSuccess) return ZS3_ERR_NOMEM;
-    if (hipMemcpyAsync(*d_out, sp->h, bytes, hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipEventRecord(sp->ev, s) != hipSuccess)
-        return ZS3_ERR_DEVICE;
-    return ZS3_OK;
-}
 
 // Blocks of a batch grouped by erasure pattern (zs3_*_batch_masks).
 struct PatternGroup {
     std::shared_ptr<RecPlan> plan;
     std::vector<int32_t> blocks;
+    size_t ids_off = 0;  // offset of this group's ids in the call's device id list
 };
+
+// One upload of every launched group's block ids (see IdsStage).
+int upload_group_ids(std::vector<PatternGroup>& groups, bool skip_noop, hipStream_t s, int32_t** d_out) {
+    *d_out = nullptr;
+    size_t n = 0;
+    for (auto& g : groups) {
+        g.ids_off = n;
+        if (!g.blocks.empty() && !(skip_noop && g.plan->noop)) n += g.blocks.size();
+    }
+    if (n == 0) return ZS3_OK;
+    const int d = current_device();
+    if (d < 0) return ZS3_ERR_DEVICE;
+    auto& sp = t_ids[d];
+    if (!sp) sp.reset(new IdsStage());
+    const int i = sp->next;
+    sp->next = (i + 1) % kIdsSlots;
+    if (!sp->ev[i] && hipEventCreateWithFlags(&sp->ev[i], hipEventDisableTiming) != hipSuccess) return ZS3_ERR_DEVICE;
+    if (sp->used[i] && hipEventSynchronize(sp->ev[i]) != hipSuccess) return ZS3_ERR_DEVICE;
+    const size_t bytes = n * sizeof(int32_t);
+    if (sp->cap[i] < bytes) {
+        if (sp->h[i]) (void)hipHostFree(sp->h[i]);
+        sp->h[i] = nullptr;
+        sp->cap[i] = 0;
+        if (hipHostMalloc((void**)&sp->h[i], bytes, hipHostMallocDefault) != hipSuccess) return ZS3_ERR_NOMEM;
+        sp->cap[i] = bytes;
+    }
+    for (auto& g : groups)
+        if (!g.blocks.empty() && !(skip_noop && g.plan->noop))
+            std::memcpy(sp->h[i] + g.ids_off, g.blocks.data(), g.blocks.size() * sizeof(int32_t));
+    if (hipMallocAsync((void**)d_out, bytes, s) != hipSuccess) return ZS3_ERR_NOMEM;
+    if (hipMemcpyAsync(*d_out, sp->h[i], bytes, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipEventRecord(sp->ev[i], s) != hipSuccess)
+        return ZS3_ERR_DEVICE;
+    sp->used[i] = true;
+    return ZS3_OK;
+}
 
 int group_patterns(zs3_codec* c, const uint8_t* present, int64_t n, int data_only, int32_t* status,
                    std::vector<PatternGroup>& groups) {
@@ -340,69 +299,6 @@ Staging* staging(size_t dbytes, size_t hbytes) {
 
 size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
-// ---- XXH64 (for erasureSelfTest, which hashes with cespare/xxhash/v2) -------
-constexpr uint64_t P1 = 11400714785074694791ULL, P2 = 14029467366897019727ULL,
-                   P3 = 1609587929392839161ULL, P4 = 9650029242287828579ULL,
-                   P5 = 2870177450012600261ULL;
-inline uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
-inline uint64_t rd64(const uint8_t* p) {
-    uint64_t v;
-    std::memcpy(&v, p, 8);
-    return v;
-}
-inline uint32_t rd32(const uint8_t* p) {
-    uint32_t v;
-    std::memcpy(&v, p, 4);
-    return v;
-}
-inline uint64_t xround(uint64_t acc, uint64_t in) { return rotl64(acc + in * P2, 31) * P1; }
-inline uint64_t xmerge(uint64_t acc, uint64_t v) { return (acc ^ xround(0, v)) * P1 + P4; }
-
-uint64_t xxh64(const uint8_t* p, size_t len) {
-    const uint8_t* end = p + len;
-    uint64_t h;
-    if (len >= 32) {
-        uint64_t v1 = P1 + P2, v2 = P2, v3 = 0, v4 = 0 - P1;
-        const uint8_t* lim = end - 32;
-        do {
-            v1 = xround(v1, rd64(p));
-            v2 = xround(v2, rd64(p + 8));
-            v3 = xround(v3, rd64(p + 16));
-            v4 = xround(v4, rd64(p + 24));
-            p += 32;
-        } while (p <= lim);
-        h = rotl64(v1, 1) + rotl64(v2, 7) + rotl64(v3, 12) + rotl64(v4, 18);
-        h = xmerge(h, v1);
-        h = xmerge(h, v2);
-        h = xmerge(h, v3);
-        h = xmerge(h, v4);
-    } else {
-        h = P5;
-    }
-    h += (uint64_t)len;
-    while (p + 8 <= end) {
-        h ^= xround(0, rd64(p));
-        h = rotl64(h, 27) * P1 + P4;
-        p += 8;
-    }
-    if (p + 4 <= end) {
-        h ^= (uint64_t)rd32(p) * P1;
-        h = rotl64(h, 23) * P2 + P3;
-        p += 4;
-    }
-    while (p < end) {
-        h ^= (*p) * P5;
-        h = rotl64(h, 11) * P1;
-        ++p;
-    }
-    h ^= h >> 33;
-    h *= P2;
-    h ^= h >> 29;
-    h *= P3;
-    h ^= h >> 32;
-    return h;
-}
-
 }  // namespace
 
 extern "C" {
@@ -460,41 +356,8 @@ int zs3_codec_new(int k, int m, int64_t block_size, zs3_codec** out) {
     c->k = k;
     c->m = m;
     c->block_size = block_size;
-    if (!zs3::build_matrix(k, m, c->matrix)) return ZS3_ERR_SINGULAR;
-    c->tables.assign((size_t)m * k * 8, 0);
-    for (int r = 0; r < m; ++r)
-        for (int j = 0; j < k; ++j)
-            zs3::perm_tables(c->matrix[(size_t)(k + r) * k + j], &c->tables[((size_t)r * k + j) * 8]);
-    // Dyadic structure: the Vandermonde points 0..k+m-1 make the parity block of the
-    // power-of-two shapes (4+2, 8+4, 16+4, ...) dyadic in m x m blocks,
-    // P[r][q*m + t] = D_q[r ^ t], so each block is a group-algebra product that
-    // needs 3 (m = 2) or 9 (m = 4) GF multiplies instead of m*m (gf_dev.hpp).
-    if ((m == 2 || m == 4) && k % m == 0) {
-        bool dy = true;
-        for (int r = 0; r < m && dy; ++r)
-            for (int j = 0; j < k && dy; ++j) {
-                const int q = j / m, t = j % m;
-                dy = c->matrix[(size_t)(k + r) * k + j] == c->matrix[(size_t)k * k + q * m + (r ^ t)];
-            }
-        if (dy) {
-            c->dyb = m;
-            c->dyadic_off = c->tables.size();
-            const int per = m;  // local-ring coefficients per block (gf_dev.hpp encode_dyadic)
-            c->tables.resize(c->tables.size() + (size_t)(k / m) * per * 8, 0);
-            for (int q = 0; q < k / m; ++q) {
-                const uint8_t* D = &c->matrix[(size_t)k * k + q * m];
-                uint8_t co[4];
-                if (m == 2) {
-                    co[0] = D[0] ^ D[1]; co[1] = D[1];
-                } else {
-                    const uint8_t a = D[0], b = D[1], cc = D[2], d = D[3];
-                    co[0] = a ^ b ^ cc ^ d; co[1] = b ^ d; co[2] = cc ^ d; co[3] = d;
-                }
-                for (int i = 0; i < per; ++i)
-                    zs3::perm_tables(co[i], &c->tables[c->dyadic_off + ((size_t)q * per + i) * 8]);
-            }
-        }
-    }
+    const int rc = zs3::build_codec_tables(k, m, *c);
+    if (rc) return rc;
     *out = c.release();
     return ZS3_OK;
 }
@@ -726,26 +589,27 @@ int zs3_reconstruct_batch_masks(const zs3_codec* cc, uint8_t* d_shards, int64_t 
     if (shard_len == 0) return first ? first : (n_blocks ? ZS3_ERR_SHARD_NO_DATA : ZS3_OK);
     hipStream_t s = (hipStream_t)stream;
     int last = zs3k::PATH_NONE;
+    int32_t* d_ids = nullptr;
+    int rc = upload_group_ids(groups, true, s, &d_ids);
+    if (rc) return rc;
     for (auto& g : groups) {
         if (g.blocks.empty() || g.plan->noop) continue;
         zs3k::RecArgs a{};
-        int rc = plan_device(c, g.plan.get(), &a.tables, &a.coef, &a.rows);
-        if (rc) return rc;
-        int32_t* d_ids = nullptr;
-        rc = upload_ids(g.blocks.data(), g.blocks.size(), s, &d_ids);
-        if (rc) return rc;
+        rc = plan_device(c, g.plan.get(), &a.tables, &a.coef, &a.rows);
+        if (rc) break;
         a.shards = d_shards;
         a.block_stride = block_stride;
         a.S = shard_len;
         a.n_blocks = (int64_t)g.blocks.size();
         a.k = c->k;
         a.e = g.plan->e;
-        a.ids = d_ids;
+        a.ids = d_ids + g.ids_off;
         a.variant = call_variant();
         rc = map_hip(zs3k::launch_reconstruct(a, s, &last));
-        (void)hipFreeAsync(d_ids, s);
-        if (rc) return rc;
+        if (rc) break;
     }
+    if (d_ids) (void)hipFreeAsync(d_ids, s);
+    if (rc) return rc;
     t_last_path = last;
     return first;
 }
@@ -766,14 +630,14 @@ int zs3_verify_reconstruct_batch_masks(const zs3_codec* cc, uint8_t* d_shards, i
     int rc = map_hip(hipMemsetAsync(d_bad, 0, (size_t)n_blocks * R * 4, s));
     if (rc) return rc;
     int last = zs3k::PATH_NONE;
+    int32_t* d_ids = nullptr;
+    rc = upload_group_ids(groups, false, s, &d_ids);
+    if (rc) return rc;
     for (auto& g : groups) {
         if (g.blocks.empty()) continue;
         zs3k::VrArgs a{};
         rc = plan_device(c, g.plan.get(), &a.tables, &a.coef, &a.rows);
-        if (rc) return rc;
-        int32_t* d_ids = nullptr;
-        rc = upload_ids(g.blocks.data(), g.blocks.size(), s, &d_ids);
-        if (rc) return rc;
+        if (rc) break;
         a.shards = d_shards;
         a.block_stride = block_stride;
         a.S = shard_len;
@@ -785,13 +649,14 @@ int zs3_verify_reconstruct_batch_masks(const zs3_codec* cc, uint8_t* d_shards, i
         a.bad = d_bad;
         a.sums_out = a.e > 0 ? d_sums_out : nullptr;
         a.h_rows = g.plan->rows.data();
-        a.ids = d_ids;
+        a.ids = d_ids + g.ids_off;
         key_words(nullptr, a.key);
         a.variant = call_variant();
         rc = map_hip(zs3k::launch_verify_reconstruct(a, s, &last));
-        (void)hipFreeAsync(d_ids, s);
-        if (rc) return rc;
+        if (rc) break;
     }
+    if (d_ids) (void)hipFreeAsync(d_ids, s);
+    if (rc) return rc;
     t_last_path = last;
     return first;
 }
@@ -1144,6 +1009,11 @@ int64_t zs3_stream_encode_multi(const zs3_codec* cc, const int* devices, int n_d
         int64_t lo, hi;
         zs3_split_range(nfull, n_devices, r, &lo, &hi);
         th.emplace_back([&, r, lo, hi] {
+            // select the device first: an empty range still encodes the tail on devices[r]
+            if (hipSetDevice(devices[r]) != hipSuccess) {
+                rcs[(size_t)r] = ZS3_ERR_DEVICE;
+                return;
+            }
             rcs[(size_t)r] = stream_range(c, devices[r], src, lo, hi, h_parity, h_sums, batch_blocks, src_pinned,
                                           out_pinned, cpu_threads);
             if (r == n_devices - 1 && tail && rcs[(size_t)r] == ZS3_OK) {
@@ -1177,33 +1047,11 @@ int64_t zs3_stream_encode(const zs3_codec* c, const uint8_t* src, int64_t total_
 
 int zs3_selftest(void) {
     // erasureSelfTest, cmd/erasure-coding.go:158-216 (want table from :169)
-    static const struct {
-        uint8_t k, m;
-        uint64_t want;
-    } kat[] = {
-        {2, 2, 0x23fb21be2496f5d3ULL}, {2, 3, 0xa5cd5600ba0d8e7cULL}, {3, 1, 0x60ab052148b010b4ULL},
-        {3, 2, 0xe64927daef76435aULL}, {3, 3, 0x672f6f242b227b21ULL}, {3, 4, 0x571e41ba23a6dc6ULL},
-        {4, 1, 0x524eaa814d5d86e2ULL}, {4, 2, 0x62b9552945504fefULL}, {4, 3, 0xcbf9065ee053e518ULL},
-        {4, 4, 0x9a07581dcd03da8ULL},  {4, 5, 0xbf2d27b55370113fULL}, {5, 1, 0xf71031a01d70dafULL},
-        {5, 2, 0x8e5845859939d0f4ULL}, {5, 3, 0x7ad9161acbb4c325ULL}, {5, 4, 0xc446b88830b4f800ULL},
-        {5, 5, 0xabf1573cc6f76165ULL}, {5, 6, 0x7b5598a85045bfb8ULL}, {6, 1, 0xe2fc1e677cc7d872ULL},
-        {6, 2, 0x7ed133de5ca6a58eULL}, {6, 3, 0x39ef92d0a74cc3c0ULL}, {6, 4, 0xcfc90052bc25d20ULL},
-        {6, 5, 0x71c96f6baeef9c58ULL}, {6, 6, 0x4b79056484883e4cULL}, {6, 7, 0xb1a0e2427ac2dc1aULL},
-        {7, 1, 0x937ba2b7af467a22ULL}, {7, 2, 0x5fd13a734d27d37aULL}, {7, 3, 0x3be2722d9b66912fULL},
-        {7, 4, 0x14c628e59011be3dULL}, {7, 5, 0xcc3b39ad4c083b9fULL}, {7, 6, 0x45af361b7de7a4ffULL},
-        {7, 7, 0x456cc320cec8a6e6ULL}, {7, 8, 0x1867a9f4db315b5cULL}, {8, 1, 0xbc5756b9a9ade030ULL},
-        {8, 2, 0xdfd7d9d0b3e36503ULL}, {8, 3, 0x72bb72c2cdbcf99dULL}, {8, 4, 0x3ba5e9b41bf07f0ULL},
-        {8, 5, 0xd7dabc15800f9d41ULL}, {8, 6, 0xb482a6169fd270fULL},  {8, 7, 0x50748e0099d657e8ULL},
-        {9, 1, 0xc77ae0144fcaeb6eULL}, {9, 2, 0x8a86c7dbebf27b68ULL}, {9, 3, 0xa64e3be6d6fe7e92ULL},
-        {9, 4, 0x239b71c41745d207ULL}, {9, 5, 0x2d0803094c5a86ceULL}, {9, 6, 0xa3c2539b3af84874ULL},
-        {10, 1, 0x7d30d91b89fcec21ULL}, {10, 2, 0xfa5af9aa9f1857a3ULL}, {10, 3, 0x84bc4bda8af81f90ULL},
-        {10, 4, 0x6c1cba8631de994aULL}, {10, 5, 0x4383e58a086cc1acULL}, {11, 1, 0x4ed2929a2df690bULL},
-        {11, 2, 0xecd6f1b1399775c0ULL}, {11, 3, 0xc78cfbfc0dc64d01ULL}, {11, 4, 0xb2643390973702d6ULL},
-        {12, 1, 0x3b2a88686122d082ULL}, {12, 2, 0xfd2f30a48a8e2e9ULL}, {12, 3, 0xd5ce58368ae90b13ULL},
-        {13, 1, 0x9c88e2a9d1b8fff8ULL}, {13, 2, 0xcb8460aa4cf6613ULL}, {14, 1, 0x78a28bbaec57996eULL},
-    };
+    int nkat = 0;
+    const zs3::SelfTestKat* kat = zs3::selftest_kats(&nkat);
     int ok = 1;
-    for (const auto& t : kat) {
+    for (int ik = 0; ik < nkat; ++ik) {
+        const zs3::SelfTestKat& t = kat[ik];
         zs3_codec* c = nullptr;
         if (zs3_codec_new(t.k, t.m, 1 << 20, &c)) return ZS3_ERR_FILE_CORRUPT;
         const int R = t.k + t.m;
@@ -1219,7 +1067,7 @@ int zs3_selftest(void) {
             stream.push_back((uint8_t)i);
             stream.insert(stream.end(), buf.begin() + (size_t)i * S, buf.begin() + (size_t)(i + 1) * S);
         }
-        if (xxh64(stream.data(), stream.size()) != t.want) ok = 0;
+        if (zs3::xxh64(stream.data(), stream.size()) != t.want) ok = 0;
         // delete first shard, DecodeDataBlocks (:201-209)
         std::vector<uint8_t> first(buf.begin(), buf.begin() + S);
         std::vector<uint8_t> pres(R, 1);

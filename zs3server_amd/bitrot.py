@@ -16,20 +16,44 @@ ERR_FILE_CORRUPT = -7
 ERR_UNEXPECTED = -8
 
 
+class DiskError(Exception):
+    """A StorageAPI error value (cmd/storage-errors.go): errFaultyDisk, errDiskNotFound,
+    errFileNotFound, ...; `name` carries the Go identifier."""
+
+    def __init__(self, name: str):
+        self.name = name
+        super().__init__(name)
+
+
 class StreamingBitrotWriter:
-    """newStreamingBitrotWriterBuffer (bitrot-streaming.go:84) — in-memory sink."""
+    """newStreamingBitrotWriterBuffer (bitrot-streaming.go:84) — in-memory sink.
+    close_with_err() mirrors streamingBitrotWriter.closeWithErr (the CreateFile pipe
+    closed with an error: every later Write fails with it)."""
 
     def __init__(self, shard_size: int, sink=None):
         self.shard_size = shard_size
         self.iow = sink if sink is not None else io.BytesIO()
+        self.err = None
 
     def Write(self, p: bytes) -> int:
         # bitrot-streaming.go:43-65
         if len(p) == 0:
             return 0
-        self.iow.write(hh256(bytes(p), MAGIC_HH256_KEY))
+        return self.WriteWithSum(p, hh256(bytes(p), MAGIC_HH256_KEY))
+
+    def WriteWithSum(self, p, sum32: bytes) -> int:
+        """Write with the sum the fused device encode already computed (the cgo shim's
+        precomputed-sum path): same [sum][chunk] bytes as Write."""
+        if len(p) == 0:
+            return 0
+        if self.err is not None:
+            raise DiskError(self.err)
+        self.iow.write(bytes(sum32))
         self.iow.write(bytes(p))
         return len(p)
+
+    def close_with_err(self, err: str) -> None:
+        self.err = err
 
     def Close(self) -> None:
         pass
@@ -50,6 +74,15 @@ class StreamingBitrotReader:
 
     def ReadAt(self, n: int, offset: int) -> bytes:
         # bitrot-streaming.go:142-189
+        want, buf = self.read_raw(n, offset)
+        if hh256(buf, MAGIC_HH256_KEY) != want:
+            raise ZS3Error(ERR_FILE_CORRUPT, "ReadAt: content hash does not match")
+        return buf
+
+    def read_raw(self, n: int, offset: int):
+        """ReadAt's stream handling (offset checks, [sum][chunk] framing, short reads)
+        without the hash: returns (stored sum, chunk) so a caller can verify many
+        chunks in one device launch (ParallelReader)."""
         if offset % self.shard_size != 0:
             raise ZS3Error(ERR_UNEXPECTED, "ReadAt: unaligned offset")
         if self.rc is None:
@@ -62,10 +95,19 @@ class StreamingBitrotReader:
         buf = self.rc.read(n)
         if len(want) != HASH_SIZE or len(buf) != n:
             raise ZS3Error(ERR_UNEXPECTED, "ReadAt: short read (io.ErrUnexpectedEOF)")
-        if hh256(buf, MAGIC_HH256_KEY) != want:
-            raise ZS3Error(ERR_FILE_CORRUPT, "ReadAt: content hash does not match")
         self.curr_offset += n
-        return buf
+        return want, buf
+
+
+class BadDiskReader:
+    """A bitrot reader over badDisk (erasure-decode_test.go:31, erasure-encode_test.go:30):
+    ReadFileStream fails with errFaultyDisk."""
+
+    def ReadAt(self, n: int, offset: int) -> bytes:
+        raise DiskError("errFaultyDisk")
+
+    def read_raw(self, n: int, offset: int):
+        raise DiskError("errFaultyDisk")
 
 
 def bitrot_verify(stream: bytes, want_size: int, part_size: int, shard_size: int) -> None:

@@ -463,8 +463,15 @@ constexpr int ws_cwe() {
 // the parity stores + barrier.  EP = 2 (early data write): the data columns go to LDS
 // before the encode instead of after it, so the LDS drains the tile's data rows while
 // the VALU encodes and only the parity rows are written between encode and barrier.
+// PFD (L2 prefetch distance, pair-form hash role): while hashing tile s-1 the hash waves
+// touch every 128-byte line of the data rows of tile s+PFD with one untracked
+// global_load_dword each (result discarded), so the HBM fetch of a tile starts PFD-1
+// steps before the encode waves load it and their own loads hit L2: the HBM stream
+// keeps ~PFD tiles of reads in flight per CU instead of the one tile the encode waves'
+// registers hold.  The hash waves never wait on these loads (they have no other vector
+// loads in the loop); the sink register stays allocated until the final vmcnt(0).
 template <int K, int M, int G, int T, int PF, bool BUF = false, bool HQ = false, bool WT = false, int PM = 0,
-          int CWX = 0, bool RING = false, int NTM = 0, bool STB = false, int EP = 0>
+          int CWX = 0, bool RING = false, int NTM = 0, bool STB = false, int EP = 0, int PFD = 0>
 __global__ void __launch_bounds__((ws_nh<K, M, G, T, HQ>() + G * (T / ws_cwe<K, CWX>()))) __attribute__((amdgpu_waves_per_eu(3)))
 k_ehx_ws(EncArgs a) {
     constexpr int R = K + M;
@@ -608,8 +615,29 @@ k_ehx_ws(EncArgs a) {
             stamp();
             return;
         }
+        // PFD: this thread's prefetch lines (line li = tid + q*NH of the tile's data rows)
+        constexpr int LPR = T / 128, NLN = G * K * LPR, NPL = PFD ? (NLN + NH - 1) / NH : 1;
+        const uint8_t* pfa[NPL];
+        uint32_t sink = 0;
+        if constexpr (PFD > 0) {
+            static_assert(T % 128 == 0, "prefetch whole 128-byte lines");
+#pragma unroll
+            for (int q = 0; q < NPL; ++q) {
+                const int li = tid + q * NH < NLN ? tid + q * NH : NLN - 1;
+                const int r = li / LPR, g = r / K, j = r % K;
+                const int64_t b = (blk0 + g) < a.n_blocks ? (blk0 + g) : (a.n_blocks - 1);
+                pfa[q] = a.data + b * a.data_stride + (int64_t)j * S + (li % LPR) * 128;
+            }
+        }
         bar();  // step 0: tile 0 being encoded
         for (int64_t s = 1; s <= nfull; ++s) {
+            if constexpr (PFD > 0) {
+                if (s + PFD < nfull) {
+#pragma unroll
+                    for (int q = 0; q < NPL; ++q)
+                        asm volatile("global_load_dword %0, %1, off" : "+v"(sink) : "v"(pfa[q] + (s + PFD) * T));
+                }
+            }
             const uint4* p = reinterpret_cast<const uint4*>(tile[(s - 1) & 1] + row_off) + hh;
             uint4 w[NPK];
 #pragma unroll
@@ -637,6 +665,7 @@ k_ehx_ws(EncArgs a) {
             if (tail & 31) hh2_remainder(st, row + (tail & ~31), (uint32_t)(tail & 31), hh);
         }
         for (int64_t s = nfull + 1; s < total; ++s) bar();
+        if constexpr (PFD > 0) asm volatile("s_waitcnt vmcnt(0)" : "+v"(sink)::"memory");
         uint64_t d0, d1;
         hh2_finalize256(st, d0, d1);
         if (blk0 + chain / R < a.n_blocks) {
@@ -847,7 +876,7 @@ k_ehx_ws(EncArgs a) {
 }
 
 template <int K, int M, int G, int T, int PF, bool BUF = false, bool HQ = false, int LDSMIN = 0, bool WT = false,
-          int PM = 0, int CWX = 0, bool RING = false, int NTM = 0, bool STB = false, int EP = 0>
+          int PM = 0, int CWX = 0, bool RING = false, int NTM = 0, bool STB = false, int EP = 0, int PFD = 0>
 static bool launch_ws_t(const EncArgs& a, hipStream_t s) {
     constexpr int R = K + M;
     constexpr int NT = ws_nh<K, M, G, T, HQ>() + G * (T / ws_cwe<K, CWX>());
@@ -860,7 +889,7 @@ static bool launch_ws_t(const EncArgs& a, hipStream_t s) {
         if (BUF && ((G - 1) * a.data_stride + K * a.S > 0x7FFFFFFF ||
                     (G - 1) * a.parity_stride + M * a.S > 0x7FFFFFFF || a.data_stride < 0 || a.parity_stride < 0))
             return false;
-        auto kern = k_ehx_ws<K, M, G, T, PF, BUF, HQ, WT, PM, CWX, RING, NTM, STB, EP>;
+        auto kern = k_ehx_ws<K, M, G, T, PF, BUF, HQ, WT, PM, CWX, RING, NTM, STB, EP, PFD>;
         if (ensure_dyn_lds((const void*)kern, dyn) != hipSuccess) return false;
         const int64_t grid = (a.n_blocks + G - 1) / G;
         hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), dyn, s, a);
@@ -997,6 +1026,14 @@ static bool launch_ehx_km(int v, const EncArgs& a, hipStream_t s) {
         case 161: if constexpr (few) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 2>(a, s); else return false;
         case 163: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 3>(a, s); else return false;
         case 164: if constexpr (few) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 3>(a, s); else return false;
+        // L2 prefetch of the data rows PFD tiles ahead by the hash waves (product 151 + PFD)
+        case 170: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 0, 2>(a, s); else return false;
+        case 171: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 0, 3>(a, s); else return false;
+        case 172: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 0, 4>(a, s); else return false;
+        case 173: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 0, 6>(a, s); else return false;
+        case 174: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 2, false, 0, 3>(a, s); else return false;
+        case 175: if constexpr (K == 16 && M == 4) return launch_ws_t<K, M, 8, 384, 1, true, false, 0, false, 0, 0, false, 3, false, 2, 3>(a, s); else return false;
+        case 176: if constexpr (few) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 0, 3>(a, s); else return false;
         case 168: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 8>(a, s); else return false;
         case 169: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 9>(a, s); else return false;
         case 162: if constexpr (K == 16 && M == 4) return launch_ws_t<K, M, 8, 384, 1, true, false, 0, false, 0, 0, false, 3, false, 2>(a, s); else return false;

@@ -25,6 +25,157 @@ class ErasureReadQuorum(Exception):
     """errErasureReadQuorum (cmd/erasure-errors.go): fewer than k readable shards."""
 
 
+class ErasureWriteQuorum(Exception):
+    """errErasureWriteQuorum (cmd/erasure-errors.go): fewer than writeQuorum writers ok."""
+
+
+# erasure-decode.go: the two read errors Decode / Heal pass upstream (heal triggers)
+ERR_FILE_NOT_FOUND = "errFileNotFound"
+ERR_FILE_CORRUPT_NAME = "errFileCorrupt"
+
+
+class ParallelWriter:
+    """parallelWriter (cmd/erasure-encode.go:29-73): one Write per shard writer, a
+    failed writer is dropped (its slot in the caller's list set to None, as the Go
+    slice is shared), quorum reduced over the per-writer errors.  The fused device
+    encode hands each writer its precomputed HighwayHash sum (WriteWithSum)."""
+
+    def __init__(self, writers: list, write_quorum: int):
+        self.writers = writers  # shared with the caller, like the Go slice
+        self.write_quorum = write_quorum
+        self.errs = [None] * len(writers)
+
+    def Write(self, blocks: list, sums=None) -> None:
+        from .bitrot import DiskError
+        for i, w in enumerate(self.writers):
+            if w is None:
+                self.errs[i] = "errDiskNotFound"
+                continue
+            if self.errs[i] is not None:
+                continue
+            try:
+                if sums is not None and hasattr(w, "WriteWithSum"):
+                    n = w.WriteWithSum(blocks[i], sums[i])
+                else:
+                    n = w.Write(blocks[i])
+                if n != len(blocks[i]):
+                    self.errs[i] = "io.ErrShortWrite"
+                    self.writers[i] = None
+            except DiskError as e:
+                self.errs[i] = e.name
+                self.writers[i] = None
+        # HealFile uses writeQuorum 1 (erasure-encode.go:63-69)
+        if sum(e is None for e in self.errs) >= self.write_quorum:
+            return
+        raise ErasureWriteQuorum(f"{sum(e is None for e in self.errs)} writers ok < quorum {self.write_quorum}")
+
+
+class ParallelReader:
+    """parallelReader (cmd/erasure-decode.go:31-203).  Reads shard chunks reader by
+    reader until k chunks verified: each round reads the next candidates' [sum][chunk]
+    without hashing, then verifies all of them in ONE device launch
+    (zs3_hh256_verify_batch, per-chunk errFileCorrupt flags); a failed or corrupt reader
+    is dropped from both reader lists (shared with the caller, as in Go) and the next
+    one is tried.  Same shards decode as the goroutine version: the data are unique."""
+
+    def __init__(self, readers: list, e: "Erasure", offset: int, total_length: int):
+        self.readers = readers
+        self.org_readers = readers
+        self.data_blocks = e.dataBlocks
+        self.offset = (offset // e.blockSize) * e.ShardSize()
+        self.shard_size = e.ShardSize()
+        self.shard_file_size = e.ShardFileSize(total_length)
+        self.reader_to_buf = list(range(len(readers)))
+
+    def prefer_readers(self, prefer: list) -> None:
+        # erasure-decode.go:65-90
+        if len(prefer) != len(self.org_readers):
+            return
+        self.readers = list(self.org_readers)
+        nxt = 0
+        for i, ok in enumerate(prefer):
+            if not ok or self.readers[i] is None:
+                continue
+            if i == nxt:
+                nxt += 1
+                continue
+            self.readers[nxt], self.readers[i] = self.readers[i], self.readers[nxt]
+            self.reader_to_buf[nxt] = i
+            self.reader_to_buf[i] = nxt
+            nxt += 1
+
+    def Read(self):
+        """Returns (bufs, err): bufs = k+m chunks (None = not read), err =
+        errFileNotFound / errFileCorrupt when a reader failed that way but k chunks were
+        still read; raises ErasureReadQuorum when fewer than k chunks could be read."""
+        from .bitrot import DiskError
+        n = len(self.readers)
+        new_buf = [None] * n
+        if self.offset + self.shard_size > self.shard_file_size:
+            self.shard_size = self.shard_file_size - self.offset
+        if self.shard_size == 0:
+            return [np.zeros(0, np.uint8)] * n, None
+        bitrot_heal = missing_heal = False
+        ri = 0
+        while sum(b is not None for b in new_buf) < self.data_blocks and ri < n:
+            need = self.data_blocks - sum(b is not None for b in new_buf)
+            cand = []  # (reader index, buf index, sum, chunk)
+            while len(cand) < need and ri < n:
+                i = ri
+                ri += 1
+                rr = self.readers[i]
+                if rr is None:
+                    continue
+                bi = self.reader_to_buf[i]
+                try:
+                    want, chunk = rr.read_raw(self.shard_size, self.offset)
+                    cand.append((i, bi, want, chunk))
+                except (DiskError, ZS3Error) as err:
+                    name = getattr(err, "name", "")
+                    if name == ERR_FILE_NOT_FOUND:
+                        missing_heal = True
+                    self.org_readers[bi] = None
+                    self.readers[i] = None
+            if not cand:
+                continue
+            bad = _verify_chunks([c[3] for c in cand], [c[2] for c in cand])
+            for (i, bi, _, chunk), b in zip(cand, bad):
+                if b:
+                    bitrot_heal = True
+                    self.org_readers[bi] = None
+                    self.readers[i] = None
+                else:
+                    new_buf[bi] = np.frombuffer(bytes(chunk), dtype=np.uint8)
+        if sum(b is not None for b in new_buf) >= self.data_blocks:
+            self.offset += self.shard_size
+            if missing_heal:
+                return new_buf, ERR_FILE_NOT_FOUND
+            if bitrot_heal:
+                return new_buf, ERR_FILE_CORRUPT_NAME
+            return new_buf, None
+        raise ErasureReadQuorum(f"{sum(b is not None for b in new_buf)} shards read < {self.data_blocks}")
+
+
+def _verify_chunks(chunks: list, wants: list) -> list:
+    """HighwayHash-256 verify of equal-length chunks in one device launch: per-chunk
+    errFileCorrupt flags (bitrot-streaming.go:182-185)."""
+    import torch
+
+    from . import MAGIC_HH256_KEY, hh256_verify_batch
+    L = len(chunks[0])
+    n = len(chunks)
+    stride = max(16, -(-L // 16) * 16)
+    host = np.zeros(n * stride, np.uint8)
+    for i, c in enumerate(chunks):
+        host[i * stride: i * stride + L] = np.frombuffer(bytes(c), np.uint8)
+    want = np.frombuffer(b"".join(bytes(w) for w in wants), np.uint8).copy()
+    d = torch.from_numpy(host).to("cuda")
+    w = torch.from_numpy(want).to("cuda")
+    bad = torch.zeros(n, dtype=torch.int32, device="cuda")
+    hh256_verify_batch(d, stride, L, n, w, bad, key=MAGIC_HH256_KEY)
+    return [bool(x) for x in bad.cpu().numpy()]
+
+
 class Erasure:
     """cmd/erasure-coding.go:35-39."""
 
@@ -61,6 +212,11 @@ class Erasure:
         arr = np.frombuffer(buf, dtype=np.uint8) if not isinstance(buf, np.ndarray) else buf
         if length == 0:
             return [np.zeros(0, dtype=np.uint8) for _ in range(k + m)], None
+        S = -(-length // k)
+        if len(arr) < (k + m) * S:  # reedsolomon.Split allocates the padding shards
+            big = np.zeros((k + m) * S, dtype=np.uint8)
+            big[:length] = arr[:length]
+            arr = big
         S, sums = self._codec.encode_data(arr, length, sums=True)
         return [arr[i * S:(i + 1) * S] for i in range(k + m)], sums
 
@@ -136,6 +292,89 @@ class Erasure:
                 row = one.cpu().numpy()
         return corrupt
 
+    # erasure-encode.go:75-113
+    def Encode(self, src, writers: list, buf, quorum: int) -> int:
+        """Erasure.Encode: read `src` (a file-like) in blockSize pieces into the bpool
+        buffer `buf` (capacity >= 2*blockSize), encode + hash each block on the device
+        (EncodeDataWithSums) and hand it to parallelWriter.  Returns the byte count;
+        raises ErasureWriteQuorum like the reference."""
+        arr = np.frombuffer(buf, dtype=np.uint8) if not isinstance(buf, np.ndarray) else buf
+        w = ParallelWriter(writers, quorum)
+        total = 0
+        bs = self.blockSize
+        while True:
+            chunk = src.read(bs)
+            n = len(chunk)
+            eof = n < bs
+            if n == 0 and total != 0:
+                break
+            arr[:n] = np.frombuffer(chunk, np.uint8)
+            # n == 0 and total == 0: empty data and parity files
+            blocks, sums = self.EncodeDataWithSums(arr, n)
+            w.Write(blocks, None if sums is None else [sums[i].tobytes() for i in range(len(blocks))])
+            total += n
+            if eof:
+                break
+        return total
+
+    # erasure-decode.go:206-282
+    def Decode(self, writer, readers: list, offset: int, length: int, total_length: int, prefer=None):
+        """Erasure.Decode: returns (written, derr) where derr is errFileNotFound /
+        errFileCorrupt when a reader failed that way but the read still succeeded;
+        raises ZS3Error(errInvalidArgument) / ErasureReadQuorum like the reference."""
+        if offset < 0 or length < 0:
+            raise ZS3Error(ERR_INVALID_ARGUMENT, "Decode")
+        if offset + length > total_length:
+            raise ZS3Error(ERR_INVALID_ARGUMENT, "Decode")
+        if length == 0:
+            return 0, None
+        reader = ParallelReader(readers, self, offset, total_length)
+        if prefer is not None and len(prefer) == len(readers):
+            reader.prefer_readers(prefer)
+        bs = self.blockSize
+        start_block, end_block = offset // bs, (offset + length) // bs
+        written, derr = 0, None
+        for block in range(start_block, end_block + 1):
+            if start_block == end_block:
+                boff, blen = offset % bs, length
+            elif block == start_block:
+                boff = offset % bs
+                blen = bs - boff
+            elif block == end_block:
+                boff, blen = 0, (offset + length) % bs
+            else:
+                boff, blen = 0, bs
+            if blen == 0:
+                break
+            bufs, err = reader.Read()
+            if err in (ERR_FILE_NOT_FOUND, ERR_FILE_CORRUPT_NAME) and derr is None:
+                derr = err
+            self.DecodeDataBlocks(bufs)
+            written += write_data_blocks(bufs, self.dataBlocks, boff, blen, dst=writer)
+        if written != length:
+            raise ZS3Error(ERR_SHORT_DATA, "Decode: errLessData")
+        return written, derr
+
+    # erasure-decode.go:285-332
+    def Heal(self, writers: list, readers: list, total_length: int):
+        """Erasure.Heal: read + DecodeDataAndParityBlocks + parallelWriter with write
+        quorum 1 per block; the rebuilt chunks' sums come from one device launch per
+        block.  Returns derr (errFileNotFound / errFileCorrupt or None)."""
+        from . import MAGIC_HH256_KEY, hh256_batch
+        if len(writers) != self.parityBlocks + self.dataBlocks:
+            raise ZS3Error(ERR_INVALID_ARGUMENT, "Heal")
+        reader = ParallelReader(readers, self, 0, total_length)
+        end_block = total_length // self.blockSize + (1 if total_length % self.blockSize else 0)
+        derr = None
+        for _ in range(end_block):
+            bufs, err = reader.Read()
+            if err in (ERR_FILE_NOT_FOUND, ERR_FILE_CORRUPT_NAME) and derr is None:
+                derr = err
+            self.DecodeDataAndParityBlocks(bufs)
+            sums = _hash_chunks(bufs, MAGIC_HH256_KEY, hh256_batch)
+            ParallelWriter(writers, 1).Write(bufs, sums)
+        return derr
+
     def ShardSize(self) -> int:
         return self._codec.shard_size()
 
@@ -144,6 +383,24 @@ class Erasure:
 
     def ShardFileOffset(self, start_offset: int, length: int, total_length: int) -> int:
         return self._codec.shard_file_offset(start_offset, length, total_length)
+
+
+def _hash_chunks(bufs: list, key: bytes, hh256_batch) -> list:
+    """HighwayHash-256 of k+m equal-length chunks in one device launch."""
+    import torch
+    L = len(bufs[0])
+    if L == 0:
+        return None
+    n = len(bufs)
+    stride = max(16, -(-L // 16) * 16)
+    host = np.zeros(n * stride, np.uint8)
+    for i, c in enumerate(bufs):
+        host[i * stride: i * stride + L] = np.asarray(c, dtype=np.uint8)
+    d = torch.from_numpy(host).to("cuda")
+    out = torch.zeros(n * 32, dtype=torch.uint8, device="cuda")
+    hh256_batch(d, stride, L, n, out, key=key)
+    o = out.cpu().numpy().reshape(n, 32)
+    return [o[i].tobytes() for i in range(n)]
 
 
 def NewErasure(data_blocks: int, parity_blocks: int, block_size: int) -> Erasure:

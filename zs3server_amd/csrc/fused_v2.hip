@@ -470,8 +470,14 @@ constexpr int ws_cwe() {
 // keeps ~PFD tiles of reads in flight per CU instead of the one tile the encode waves'
 // registers hold.  The hash waves never wait on these loads (they have no other vector
 // loads in the loop); the sink register stays allocated until the final vmcnt(0).
+// UA (unaligned shard size): S need not be a multiple of 16 (RS(12+4) on 1 MiB blocks:
+// S = 87 382, every row 2-byte aligned; k*S - n = 8 bytes of Split padding).  Full tiles
+// use the same vector loads and stores at the rows' byte offsets (the GPU runs global
+// memory in unaligned mode); the ragged tail tile is never prefetched: each lane reads
+// its columns of it byte by byte, with the Split padding of the last data row (n..k*S)
+// and everything past the row read as zero, and stores only the parity bytes below S.
 template <int K, int M, int G, int T, int PF, bool BUF = false, bool HQ = false, bool WT = false, int PM = 0,
-          int CWX = 0, bool RING = false, int NTM = 0, bool STB = false, int EP = 0, int PFD = 0>
+          int CWX = 0, bool RING = false, int NTM = 0, bool STB = false, int EP = 0, int PFD = 0, bool UA = false>
 __global__ void __launch_bounds__((ws_nh<K, M, G, T, HQ>() + G * (T / ws_cwe<K, CWX>()))) __attribute__((amdgpu_waves_per_eu(3)))
 k_ehx_ws(EncArgs a) {
     constexpr int R = K + M;
@@ -499,7 +505,7 @@ k_ehx_ws(EncArgs a) {
     for (int i = tid; i < NTAB; i += NT) tabs[i] = a.dtables[i];
     if (RING && tid < 4) ring[tid] = 0;
     const int64_t nfull = S / T;
-    const int tail = (int)(S - nfull * T);  // multiple of 16 (launch requires S % 16 == 0)
+    const int tail = (int)(S - nfull * T);  // multiple of 16 unless UA
     // Step schedule shared by both roles: PF edge steps, the steady loop in units of PF
     // while i + 2*PF <= nfull, 2*PF edge steps, one step that only hashes.
     int64_t iend = PF;
@@ -737,11 +743,49 @@ k_ehx_ws(EncArgs a) {
         }
     };
     auto prefetch_any = [&](VT (&xs)[K], int64_t tn) {
-        const bool ok = tn < nfull || (tn == nfull && o < tail);
+        // UA: the tail tile is read byte by byte in its step (tail_cols), never prefetched
+        const bool ok = tn < nfull || (!UA && tn == nfull && o < tail);
         if constexpr (BUF)
             load_buf(xs, vo_d + (ok ? (uint32_t)(tn * T) : 0u), 0);  // per-lane part in voffset
         else
             load(xs, ok ? tn * T : 0);
+    };
+    // UA tail tile: bytes [o, o + CWE) of every data row, zero past the row's valid length
+    // (tail, or for the last data row the end of the block: Split padding reads as zero)
+    auto tail_cols = [&](VT (&xs)[K]) {
+        const uint8_t* t0p = src + nfull * T;
+        const int64_t last_valid = a.n - (int64_t)(K - 1) * S - nfull * T;
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            const int64_t valid = j == K - 1 ? (last_valid < tail ? last_valid : tail) : tail;
+            uint32_t w[NWd];
+#pragma unroll
+            for (int q = 0; q < NWd; ++q) {
+                uint32_t v = 0;
+#pragma unroll
+                for (int bb = 0; bb < 4; ++bb) {
+                    const int pos = o + 4 * q + bb;
+                    if (pos < valid) v |= (uint32_t)t0p[(int64_t)j * S + 4 * q + bb] << (8 * bb);
+                }
+                w[q] = v;
+            }
+            if constexpr (NWd == 1) {
+                xs[j] = w[0];
+            } else {
+#pragma unroll
+                for (int q = 0; q < NWd; ++q) xs[j][q] = w[q];
+            }
+        }
+    };
+    auto store_tail = [&](const Col<NWd> (&par)[M]) {
+        uint8_t* t0p = pdst + nfull * T;
+#pragma unroll
+        for (int r = 0; r < M; ++r)
+#pragma unroll
+            for (int q = 0; q < NWd; ++q)
+#pragma unroll
+                for (int bb = 0; bb < 4; ++bb)
+                    if (o + 4 * q + bb < tail) t0p[(int64_t)r * S + 4 * q + bb] = (uint8_t)(par[r].w[q] >> (8 * bb));
     };
     auto encode = [&](VT (&xr)[K], uint8_t* tl, Col<NWd> (&par)[M]) {
         Col<NWd> xs[K];
@@ -841,10 +885,18 @@ k_ehx_ws(EncArgs a) {
         if (full || part) slot_free(ti);
         vm_wait<0>(xs);
         Col<NWd> par[M];
+        if constexpr (UA) {
+            if (part) tail_cols(xs);
+        }
         if (full || part) encode(xs, tile[ti & 1], par);
         if (RING && (full || part)) ring_signal(&ring[ti & 1]);
         prefetch_any(xs, ti + PF);
-        if (full || (part && o < tail)) store_par(par, ti * T);
+        if constexpr (UA) {
+            if (full) store_par(par, ti * T);
+            else if (part && o < tail) store_tail(par);
+        } else {
+            if (full || (part && o < tail)) store_par(par, ti * T);
+        }
         if constexpr (!RING) bar();
     };
     bar();  // tables visible
@@ -876,7 +928,8 @@ k_ehx_ws(EncArgs a) {
 }
 
 template <int K, int M, int G, int T, int PF, bool BUF = false, bool HQ = false, int LDSMIN = 0, bool WT = false,
-          int PM = 0, int CWX = 0, bool RING = false, int NTM = 0, bool STB = false, int EP = 0, int PFD = 0>
+          int PM = 0, int CWX = 0, bool RING = false, int NTM = 0, bool STB = false, int EP = 0, int PFD = 0,
+          bool UA = false>
 static bool launch_ws_t(const EncArgs& a, hipStream_t s) {
     constexpr int R = K + M;
     constexpr int NT = ws_nh<K, M, G, T, HQ>() + G * (T / ws_cwe<K, CWX>());
@@ -885,11 +938,18 @@ static bool launch_ws_t(const EncArgs& a, hipStream_t s) {
     if constexpr (dyn + K * 32 > 163840 || NT > 1024) {
         return false;
     } else {
-        if (a.dyb != M || (a.S % 16) != 0) return false;
+        if (a.dyb != M) return false;
+        if constexpr (UA) {
+            // the Split padding (n .. k*S) must lie in the last data row's tail tile
+            const int64_t tail = a.S % T;
+            if ((int64_t)K * a.S - a.n > tail || a.n <= (int64_t)(K - 1) * a.S) return false;
+        } else {
+            if ((a.S % 16) != 0 || a.n != (int64_t)K * a.S) return false;
+        }
         if (BUF && ((G - 1) * a.data_stride + K * a.S > 0x7FFFFFFF ||
                     (G - 1) * a.parity_stride + M * a.S > 0x7FFFFFFF || a.data_stride < 0 || a.parity_stride < 0))
             return false;
-        auto kern = k_ehx_ws<K, M, G, T, PF, BUF, HQ, WT, PM, CWX, RING, NTM, STB, EP, PFD>;
+        auto kern = k_ehx_ws<K, M, G, T, PF, BUF, HQ, WT, PM, CWX, RING, NTM, STB, EP, PFD, UA>;
         if (ensure_dyn_lds((const void*)kern, dyn) != hipSuccess) return false;
         const int64_t grid = (a.n_blocks + G - 1) / G;
         hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), dyn, s, a);
@@ -966,6 +1026,21 @@ static int launch_ehx_default(const EncArgs& a, hipStream_t s) {
         if (n > 4 * 256)
             return launch_ws_t<K, M, 8, 384, 1, true, false, 0, false, 0, 0, false, 3, false, 2>(a, s) ? PATH_WS : PATH_NONE;
         return launch_ws_t<K, M, 4, 512, 1, true, true, 0, false, 0, 0, false, 3>(a, s) ? PATH_WS : PATH_NONE;
+    } else if constexpr (K == 12 && M == 4) {
+        // RS(12+4), the 16-drive default (cmd/format-erasure.go:870-881), at shard sizes
+        // that are multiples of 16; 1 MiB blocks (S = 87 382) take launch_ehx_ua.  Same
+        // shapes as RS(16+4): 8 stripes of 8-byte buffer-addressed columns, data rows
+        // written to LDS before the encode; 4 stripes with quad-form hash waves up to 1024.
+        if (n > 4 * 256)
+            return launch_ws_t<K, M, 8, 384, 1, true, false, 0, false, 0, 0, false, 3, false, 2>(a, s) ? PATH_WS : PATH_NONE;
+        return launch_ws_t<K, M, 4, 512, 1, true, true, 0, false, 0, 0, false, 3>(a, s) ? PATH_WS : PATH_NONE;
+    } else if constexpr (K == 4 && M == 4) {
+        // RS(4+4), the 8-drive default: the RS(8+4) shape (16 stripes, 16-byte columns,
+        // pair-form hash waves) for large batches, the RS(4+2) config-2 shape (4 stripes,
+        // quad-form hash waves, 4 tiles of prefetch) below.
+        if (n > 8 * 256)
+            return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3>(a, s) ? PATH_WS : PATH_NONE;
+        return launch_ws_t<K, M, 4, 512, 4, false, true, 83968, false, 0, 0, false, 3>(a, s) ? PATH_WS : PATH_NONE;
     } else if constexpr (K == 4 && M == 2) {
         if (n >= 1024 && n <= 8 * 256)
             return launch_ws_t<K, M, 4, 512, 4, false, true, 83968, false, 0, 0, false, 3>(a, s) ? PATH_WS : PATH_NONE;
@@ -1033,6 +1108,11 @@ static bool launch_ehx_km(int v, const EncArgs& a, hipStream_t s) {
         case 173: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 0, 6>(a, s); else return false;
         case 174: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 2, false, 0, 3>(a, s); else return false;
         case 175: if constexpr (K == 16 && M == 4) return launch_ws_t<K, M, 8, 384, 1, true, false, 0, false, 0, 0, false, 3, false, 2, 3>(a, s); else return false;
+        // config 2 (latency-bound chains): longer tiles = fewer per-step barriers and LDS
+        // read latencies on the chain's critical path
+        case 177: if constexpr (few) return launch_ws_t<K, M, 4, 1024, 4, false, true, 83968, false, 0, 0, false, 3>(a, s); else return false;
+        case 178: if constexpr (few) return launch_ws_t<K, M, 4, 1024, 2, false, true, 83968, false, 0, 0, false, 3>(a, s); else return false;
+        case 179: if constexpr (few) return launch_ws_t<K, M, 4, 2048, 2, false, true, 83968, false, 0, 0, false, 3>(a, s); else return false;
         case 176: if constexpr (few) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 0, 3>(a, s); else return false;
         case 168: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 8>(a, s); else return false;
         case 169: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 9>(a, s); else return false;
@@ -1401,11 +1481,40 @@ static bool launch_vr_ws_bt(const VrArgs& a, hipStream_t s) {
     }
 }
 
+#if ZS3_DIAG
+// RS(16+4) rebuild / heal with the survivor prefetch depth and tile length as
+// parameters (diagnostics 250-257, round 3): e = 1..4 rebuilt rows.
+template <int T, int PF, bool HOUT, int BT>
+static bool vr16(const VrArgs& a, hipStream_t s) {
+    switch (a.e) {
+        case 1: return launch_vr_ws_t<16, 1, HOUT, 8, T, PF, 4, false, true, BT>(a, s);
+        case 2: return launch_vr_ws_t<16, 2, HOUT, 8, T, PF, 4, false, true, BT>(a, s);
+        case 3: return launch_vr_ws_t<16, 3, HOUT, 8, T, PF, 4, false, true, BT>(a, s);
+        case 4: return launch_vr_ws_t<16, 4, HOUT, 8, T, PF, 4, false, true, BT>(a, s);
+        default: return false;
+    }
+}
+#endif
+
 // GET / heal defaults (variant 0) and diagnostics variants 210-215.
 // RS(8+4)-shaped GET: 16 stripes, 256-byte tiles, verify-only or rebuild 2; heal with
 // 8-byte columns (16-byte columns spill at the heal's 168-VGPR budget: 4.7 ms).
 bool launch_vr_ws(int v, const VrArgs& a, hipStream_t s) {
     if (!ZS3_DIAG && v != 0) return false;
+#if ZS3_DIAG
+    if (a.k == 16 && v >= 250 && v <= 257 && a.e >= 1) {
+        const bool h = a.sums_out != nullptr;
+        switch (v) {
+            case 250: return h ? vr16<128, 2, true, 4>(a, s) : vr16<256, 2, false, 0>(a, s);
+            case 251: return h ? vr16<128, 4, true, 4>(a, s) : vr16<128, 4, false, 0>(a, s);
+            case 252: return h ? vr16<256, 2, true, 4>(a, s) : vr16<256, 3, false, 0>(a, s);
+            case 253: return h ? vr16<256, 1, true, 4>(a, s) : vr16<512, 1, false, 0>(a, s);
+            case 254: return h ? vr16<128, 3, true, 4>(a, s) : vr16<128, 2, false, 0>(a, s);
+            case 255: return h ? vr16<256, 2, true, 0>(a, s) : vr16<256, 2, false, 4>(a, s);
+            default: return false;
+        }
+    }
+#endif
     if (a.k == 4 && (v == 0 || v == 214)) {
         // RS(4+2)-shaped GET / heal default: quad-form hash waves, 8 stripes, one wave
         // of each kind per SIMD (the 8 192 chains of a 2048-object batch are
@@ -1582,11 +1691,24 @@ bool launch_vr_ws(int v, const VrArgs& a, hipStream_t s) {
     }
 }
 
+int launch_ehx_ua(const EncArgs& a, hipStream_t s) {
+    if (a.k == 12 && a.m == 4) {
+        if (a.n_blocks > 4 * 256)
+            return launch_ws_t<12, 4, 8, 384, 1, true, false, 0, false, 0, 0, false, 3, false, 2, 0, true>(a, s)
+                       ? PATH_WS : PATH_NONE;
+        return launch_ws_t<12, 4, 4, 512, 1, true, true, 0, false, 0, 0, false, 3, false, 0, 0, true>(a, s)
+                   ? PATH_WS : PATH_NONE;
+    }
+    return PATH_NONE;
+}
+
 int launch_ehx(int v, const EncArgs& a, hipStream_t s) {
     if (v == 0) {
         if (a.k == 8 && a.m == 4) return launch_ehx_default<8, 4>(a, s);
         if (a.k == 4 && a.m == 2) return launch_ehx_default<4, 2>(a, s);
         if (a.k == 16 && a.m == 4) return launch_ehx_default<16, 4>(a, s);
+        if (a.k == 12 && a.m == 4) return launch_ehx_default<12, 4>(a, s);
+        if (a.k == 4 && a.m == 4) return launch_ehx_default<4, 4>(a, s);
         return PATH_NONE;
     }
 #if ZS3_DIAG

@@ -1366,6 +1366,15 @@ hipError_t launch_encode(const EncArgs& a, hipStream_t s, int* path) {
     }
     ZS3_FAST_KM(X)
 #undef X
+    // fused encode + sums at shard sizes that are not a multiple of 16 (RS(12+4) on
+    // 1 MiB blocks: S = 87 382)
+    if (a.sums && a.dyb && a.variant == 0) {
+        const int p = launch_ehx_ua(a, s);
+        if (p != PATH_NONE) {
+            if (path) *path = p;
+            return hipGetLastError();
+        }
+    }
     if (path) *path = PATH_GENERIC;
     const int R = a.k + a.m;
     int nt = round64(4 * R);

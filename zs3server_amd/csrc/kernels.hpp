@@ -144,6 +144,9 @@ bool has_fast_encode(int k, int m);
 // number; the product build knows only the defaults it dispatches to.  Returns the
 // path that ran, or PATH_NONE when the variant does not apply (caller falls back).
 int launch_ehx(int v, const EncArgs& a, hipStream_t s);
+// Fused encode + sums for shard sizes that are not a multiple of 16 (k_ehx_ws UA mode,
+// e.g. RS(12+4) on 1 MiB blocks); PATH_NONE when the shape has no such instance.
+int launch_ehx_ua(const EncArgs& a, hipStream_t s);
 // Warp-specialised GET / heal pass (fused_v2.hip); false if the shape has no instance.
 bool launch_vr_ws(int v, const VrArgs& a, hipStream_t s);
 

@@ -291,3 +291,72 @@ def test_rs124_ragged_blocks(oracle, blen):
         want = oracle.encode_data(k, m, oracle.fill(5, b, blen), mat)
         assert np.array_equal(host[b, k:], want[k:]), b
         assert np.array_equal(hs[b], oracle.hh256_rows(KEY, want)), b
+
+
+@pytest.mark.parametrize("k,m,nb", [(11, 5, 1024), (10, 6, 1024), (5, 4, 512), (7, 3, 300), (9, 7, 256), (13, 3, 64)])
+def test_any_geometry_encode(oracle, k, m, nb):
+    """Geometries of other set sizes and parity upgrades (cmd/erasure-object.go:724-775):
+    the any-geometry encode (8-byte columns at unaligned row offsets) + the batched hash
+    in stripe mode; 1 MiB blocks, every block vs cpu_ref, Split padding bytes poisoned."""
+    R = k + m
+    S = -(-MiB // k)
+    codec = z.Codec(k, m, MiB)
+    d = torch.zeros(nb * R * S, dtype=torch.uint8, device=DEV)
+    z.fill_batch(d, R * S, MiB, nb, seed=k * 10 + m, obj0=0)
+    if k * S > MiB:
+        d.view(nb, R * S)[:, MiB:k * S] = 0xEE
+    sums = torch.zeros(nb * R * 32, dtype=torch.uint8, device=DEV)
+    codec.encode_batch(d, R * S, MiB, nb, parity=d, parity_offset=k * S, parity_stride=R * S, sums=sums)
+    torch.cuda.synchronize()
+    mat = oracle.build_matrix(k, m)
+    host = d.cpu().numpy().reshape(nb, R * S)
+    par = np.empty(nb * m * S, np.uint8)
+    sref = np.empty(nb * R * 32, np.uint8)
+    cpuref.encode_hash(k, m, mat, np.ascontiguousarray(host), MiB, nb, R * S, par, m * S, sref, KEY,
+                       cpuref.threads_available())
+    assert np.array_equal(host[:, k * S:], par.reshape(nb, m * S))
+    assert np.array_equal(sums.cpu().numpy(), sref)
+
+
+@pytest.mark.parametrize("k,m,erased,heal", [(12, 4, [0, 5], False), (12, 4, [3, 13], True),
+                                             (12, 4, [0, 1, 2, 15], True), (11, 5, [1, 4, 12], True),
+                                             (10, 6, [0, 9], False), (5, 4, [4, 5, 6, 7], True)])
+def test_any_geometry_get_heal(oracle, k, m, erased, heal):
+    """GET / heal on the geometries without a warp-specialised instance (unaligned
+    shard sizes on 1 MiB blocks): survivors verified in one stripe-mode hash launch,
+    the any-geometry rebuild, rebuilt rows hashed in one launch; one rotted survivor
+    flagged exactly; 512 stripes of 64 distinct oracle stripes."""
+    R = k + m
+    nb = 512
+    base, bsum, reps = _tiled_stripes(oracle, k, m, MiB, nb, seed=31)
+    S = base.shape[2]
+    codec = z.Codec(k, m, MiB)
+    d = torch.from_numpy(base).to(DEV).repeat(reps, 1, 1).contiguous()
+    for e in erased:
+        d[:, e, :] = 0x5A
+    surv = [i for i in range(R) if i not in erased][:k]
+    bad_blk, bad_row = 77, surv[2]
+    d[bad_blk, bad_row, S - 1] ^= 4
+    exp = torch.from_numpy(bsum).to(DEV).repeat(reps, 1, 1).contiguous()
+    bad = torch.full((nb, R), 7, dtype=torch.int32, device=DEV)
+    out = torch.zeros((nb, R, 32), dtype=torch.uint8, device=DEV) if heal else None
+    codec.verify_reconstruct_batch(d, R * S, S, nb, [i not in erased for i in range(R)], not heal, exp, bad,
+                                   sums_out=out)
+    torch.cuda.synchronize()
+    want_bad = np.zeros((nb, R), np.int32)
+    want_bad[bad_blk, bad_row] = 1
+    assert np.array_equal(bad.cpu().numpy(), want_bad)
+    ok = torch.ones(nb, dtype=torch.bool, device=DEV)
+    ok[bad_blk] = False
+    ref = torch.from_numpy(base).to(DEV)
+    refs = torch.from_numpy(bsum).to(DEV)
+    dv = d.view(reps, 64, R, S)
+    okv = ok.view(reps, 64)
+    for i in erased:
+        if i < k or heal:
+            assert bool((dv[:, :, i, :] == ref[None, :, i, :]).all(dim=2)[okv].all()), f"rebuilt shard {i}"
+            if heal:
+                sv = out.view(reps, 64, R, 32)[:, :, i, :]
+                assert bool((sv == refs[None, :, i, :]).all(dim=2)[okv].all()), f"heal sum {i}"
+        else:
+            assert bool((dv[:, :, i, :] == 0x5A).all())

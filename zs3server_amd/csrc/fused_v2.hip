@@ -1108,6 +1108,13 @@ static bool launch_ehx_km(int v, const EncArgs& a, hipStream_t s) {
         case 173: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 0, 6>(a, s); else return false;
         case 174: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 2, false, 0, 3>(a, s); else return false;
         case 175: if constexpr (K == 16 && M == 4) return launch_ws_t<K, M, 8, 384, 1, true, false, 0, false, 0, 0, false, 3, false, 2, 3>(a, s); else return false;
+        // tile / wave-count shapes for RS(8+4) at the product's memory policy (r03)
+        case 180: if constexpr (deep) return launch_ws_t<K, M, 8, 768, 1, false, false, 0, false, 1, 0, false, 3>(a, s); else return false;
+        case 182: if constexpr (deep) return launch_ws_t<K, M, 8, 768, 1, false, false, 0, false, 1, 8, false, 3>(a, s); else return false;
+        case 183: if constexpr (deep) return launch_ws_t<K, M, 8, 512, 2, false, false, 0, false, 1, 0, false, 3>(a, s); else return false;
+        case 184: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, true, 1, 0, false, 3>(a, s); else return false;
+        case 185: if constexpr (deep) return launch_ws_t<K, M, 16, 256, 1, false, false, 0, false, 1, 0, false, 3>(a, s); else return false;
+        case 186: if constexpr (deep) return launch_ws_t<K, M, 8, 512, 1, false, false, 0, false, 1, 0, false, 3>(a, s); else return false;
         // config 2 (latency-bound chains): longer tiles = fewer per-step barriers and LDS
         // read latencies on the chain's critical path
         case 177: if constexpr (few) return launch_ws_t<K, M, 4, 1024, 4, false, true, 83968, false, 0, 0, false, 3>(a, s); else return false;
@@ -1506,7 +1513,7 @@ bool launch_vr_ws(int v, const VrArgs& a, hipStream_t s) {
         const bool h = a.sums_out != nullptr;
         switch (v) {
             case 250: return h ? vr16<128, 2, true, 4>(a, s) : vr16<256, 2, false, 0>(a, s);
-            case 251: return h ? vr16<128, 4, true, 4>(a, s) : vr16<128, 4, false, 0>(a, s);
+            case 251: return h ? vr16<128, 3, true, 0>(a, s) : vr16<128, 3, false, 4>(a, s);
             case 252: return h ? vr16<256, 2, true, 4>(a, s) : vr16<256, 3, false, 0>(a, s);
             case 253: return h ? vr16<256, 1, true, 4>(a, s) : vr16<512, 1, false, 0>(a, s);
             case 254: return h ? vr16<128, 3, true, 4>(a, s) : vr16<128, 2, false, 0>(a, s);

@@ -871,6 +871,153 @@ __global__ void __launch_bounds__(256) k_reconstruct_generic(RecArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Any-geometry kernels (k <= 64, m / e <= AMAX, any shard size, any alignment): the
+// server's other erasure geometries (set sizes 4-16 with parity upgrades,
+// cmd/erasure-object.go:724-775, e.g. RS(11+5), RS(10+6), RS(5+4)) and ragged last
+// blocks with Split padding.  One 8-byte column of one stripe per thread, 8-byte
+// vector loads and stores at the rows' byte offsets (unaligned global access), the
+// parity / rebuilt rows accumulated with the per-coefficient permute tables
+// (gf_dev.hpp), the partial last column and the Split padding read byte by byte.
+// The bitrot sums of these geometries come from the batched hash kernel in stripe mode.
+constexpr int AMAX = 8;
+
+typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ u2v ld8_any(const uint8_t* p, int64_t o, int64_t vlen) {
+    u2v v = {0u, 0u};
+    if (o + 8 <= vlen) {
+        __builtin_memcpy(&v, p + o, 8);
+    } else if (o < vlen) {
+        uint32_t w[2] = {0u, 0u};
+        for (int z = 0; z < 8; ++z)
+            if (o + z < vlen) w[z >> 2] |= (uint32_t)p[o + z] << (8 * (z & 3));
+        v.x = w[0];
+        v.y = w[1];
+    }
+    return v;
+}
+
+__device__ __forceinline__ void st8_any(uint8_t* p, int64_t o, int64_t len, uint32_t x, uint32_t y) {
+    if (o + 8 <= len) {
+        const u2v v = {x, y};
+        __builtin_memcpy(p + o, &v, 8);
+    } else {
+        for (int z = 0; z < 8; ++z)
+            if (o + z < len) p[o + z] = (uint8_t)((z < 4 ? x : y) >> (8 * (z & 3)));
+    }
+}
+
+// acc ^= c * x for two packed dwords (x split once per input row).
+__device__ __forceinline__ void gf_mac2(uint32_t& a0, uint32_t& a1, const Nib& n0, const Nib& n1, const CoefTab& t) {
+    const Prod3 p0 = gf_lookup(n0, t), p1 = gf_lookup(n1, t);
+    a0 = xor3(a0, p0.a, p0.b) ^ p0.c;
+    a1 = xor3(a1, p1.a, p1.b) ^ p1.c;
+}
+
+// Encode only (Erasure.EncodeData's arithmetic, erasure-coding.go:77-91), any k / m <= AMAX.
+__global__ void __launch_bounds__(256) k_encode_any(EncArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t etabs[];  // m*k*8 dwords
+    const int k = a.k, m = a.m;
+    for (int i = threadIdx.x; i < m * k * 8; i += 256) etabs[i] = a.tables[i];
+    __syncthreads();
+    const int64_t S = a.S;
+    const int64_t cols = (S + 7) >> 3;
+    for (int64_t b = blockIdx.y; b < a.n_blocks; b += gridDim.y) {
+        const uint8_t* blk = a.data + b * a.data_stride;
+        uint8_t* pb = a.parity + b * a.parity_stride;
+        for (int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x; c < cols; c += (int64_t)gridDim.x * 256) {
+            const int64_t o = c * 8;
+            uint32_t acc[AMAX][2];
+#pragma unroll
+            for (int r = 0; r < AMAX; ++r) acc[r][0] = acc[r][1] = 0;
+            for (int j = 0; j < k; ++j) {
+                int64_t vlen = a.n - (int64_t)j * S;  // Split padding of the last rows reads as zero
+                vlen = vlen < 0 ? 0 : (vlen < S ? vlen : S);
+                const u2v x = ld8_any(blk + (int64_t)j * S, o, vlen);
+                const Nib n0 = split_nibbles(x.x), n1 = split_nibbles(x.y);
+                const uint32_t* tb = etabs + opaque_zero() + j * 8;
+#pragma unroll
+                for (int r = 0; r < AMAX; ++r)
+                    if (r < m) gf_mac2(acc[r][0], acc[r][1], n0, n1, load_coef(tb, r * k));
+            }
+#pragma unroll
+            for (int r = 0; r < AMAX; ++r)
+                if (r < m) st8_any(pb + (int64_t)r * S, o, S, acc[r][0], acc[r][1]);
+        }
+    }
+}
+
+// Reconstruct (ReconstructData / Reconstruct, erasure-coding.go:96-119): e <= AMAX rows
+// from the k survivors rows[0..k) into rows[k..k+e), any k.
+__global__ void __launch_bounds__(256) k_reconstruct_any(RecArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t rtabs[];  // e*k*8 dwords, then rows
+    const int k = a.k, E = a.e;
+    int32_t* rows = reinterpret_cast<int32_t*>(rtabs + E * k * 8);
+    for (int i = threadIdx.x; i < E * k * 8; i += 256) rtabs[i] = a.tables[i];
+    for (int i = threadIdx.x; i < k + E; i += 256) rows[i] = a.rows[i];
+    __syncthreads();
+    const int64_t S = a.S;
+    const int64_t cols = (S + 7) >> 3;
+    for (int64_t b = blockIdx.y; b < a.n_blocks; b += gridDim.y) {
+        uint8_t* blk = a.shards + (a.ids ? (int64_t)a.ids[b] : b) * a.block_stride;
+        for (int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x; c < cols; c += (int64_t)gridDim.x * 256) {
+            const int64_t o = c * 8;
+            uint32_t acc[AMAX][2];
+#pragma unroll
+            for (int r = 0; r < AMAX; ++r) acc[r][0] = acc[r][1] = 0;
+            for (int t = 0; t < k; ++t) {
+                const u2v x = ld8_any(blk + (int64_t)rows[t] * S, o, S);
+                const Nib n0 = split_nibbles(x.x), n1 = split_nibbles(x.y);
+                const uint32_t* tb = rtabs + opaque_zero() + t * 8;
+#pragma unroll
+                for (int r = 0; r < AMAX; ++r)
+                    if (r < E) gf_mac2(acc[r][0], acc[r][1], n0, n1, load_coef(tb, r * k));
+            }
+#pragma unroll
+            for (int r = 0; r < AMAX; ++r)
+                if (r < E) st8_any(blk + (int64_t)rows[k + r] * S, o, S, acc[r][0], acc[r][1]);
+        }
+    }
+}
+
+// Bitrot sums of every shard of a batch in one launch (hash kernel, stripe mode).
+static hipError_t hash_stripes(const EncArgs& a, hipStream_t s) {
+    HashArgs h{};
+    const int R = a.k + a.m;
+    h.rps = R;
+    h.kd = a.k;
+    h.rtot = R;
+    h.msgs = a.data;
+    h.stride = a.data_stride;
+    h.par = a.parity;
+    h.par_stride = a.parity_stride;
+    h.len = a.S;
+    h.vlim = a.n;
+    h.n = a.n_blocks * R;
+    h.sums = a.sums;
+    for (int i = 0; i < R; ++i) h.rowmap[i] = (uint8_t)i;
+    for (int q = 0; q < 4; ++q) h.key[q] = a.key[q];
+    return launch_hash(h, s);
+}
+
+static bool encode_any_ok(const EncArgs& a) {
+    return a.k + a.m <= 64 && a.m <= AMAX && (size_t)a.m * a.k * 32 <= 65536;
+}
+
+static hipError_t launch_encode_any(const EncArgs& a, hipStream_t s) {
+    const size_t lds = (size_t)a.m * a.k * 32;
+    hipError_t e = ensure_dyn_lds((const void*)k_encode_any, lds);
+    if (e != hipSuccess) return e;
+    const int64_t cols = (a.S + 7) >> 3;
+    const int64_t gx = (cols + 255) / 256;
+    const unsigned gy = (unsigned)(a.n_blocks < 65535 ? a.n_blocks : 65535);
+    hipLaunchKernelGGL(k_encode_any, dim3((unsigned)gx, gy), dim3(256), lds, s, a);
+    e = hipGetLastError();
+    if (e != hipSuccess || !a.sums) return e;
+    return hash_stripes(a, s);
+}
+
+// ---------------------------------------------------------------------------
 // HighwayHash-256 of n messages (64 chains = 256 threads per workgroup), with
 // optional compare against expected digests (streamingBitrotReader.ReadAt,
 // cmd/bitrot-streaming.go:180-186, and bitrotVerify, cmd/bitrot.go:158-210: a
@@ -890,10 +1037,29 @@ struct MsgGeom {
     const uint8_t* exp;  // expected digest (or nullptr)
     int64_t len;
     int64_t slot;        // index into sums / bad
+    int64_t vlen;        // bytes at or past vlen read as zero (<= len)
 };
 
 __device__ __forceinline__ MsgGeom msg_geom(const HashArgs& a, int64_t i) {
     MsgGeom g;
+    if (a.rps > 0) {
+        // stripe mode: shard rowmap[q] of stripe bq
+        const int64_t bq = i / a.rps;
+        const int q = (int)(i - bq * a.rps);
+        const int64_t slot = a.ids ? (int64_t)a.ids[bq] : bq;
+        const int idx = a.rowmap[q];
+        g.p = idx < a.kd ? a.msgs + slot * a.stride + (int64_t)idx * a.len
+                         : a.par + slot * a.par_stride + (int64_t)(idx - a.kd) * a.len;
+        g.len = a.len;
+        g.slot = slot * a.rtot + idx;
+        g.exp = a.expect ? a.expect + g.slot * 32 : nullptr;
+        g.vlen = a.len;
+        if (a.vlim > 0 && idx < a.kd) {
+            const int64_t v = a.vlim - (int64_t)idx * a.len;
+            g.vlen = v < 0 ? 0 : (v < a.len ? v : a.len);
+        }
+        return g;
+    }
     g.slot = a.ids ? (int64_t)a.ids[i] : i;
     const int64_t ss = a.sum_stride ? a.sum_stride : 32;
     if (a.chunk > 0) {
@@ -908,6 +1074,7 @@ __device__ __forceinline__ MsgGeom msg_geom(const HashArgs& a, int64_t i) {
         g.len = a.lens ? a.lens[i] : a.len;
         g.exp = a.expect ? a.expect + g.slot * ss : nullptr;
     }
+    g.vlen = g.len;
     return g;
 }
 
@@ -923,7 +1090,7 @@ __global__ void __launch_bounds__(256) k_hash_batch(HashArgs a) {
     HHLane st = hh_init(lane, a.key[0], a.key[1], a.key[2], a.key[3]);
     // geometry of this thread's hash chain and of the HB_PPT rows it loads
     const bool live = m0 + chain < a.n;
-    const MsgGeom mine = live ? msg_geom(a, m0 + chain) : MsgGeom{nullptr, nullptr, 0, 0};
+    const MsgGeom mine = live ? msg_geom(a, m0 + chain) : MsgGeom{nullptr, nullptr, 0, 0, 0};
     if (lane == 0) s_len[chain] = mine.len;
     const uint8_t* rp[HB_PPT];
     int64_t rl[HB_PPT];
@@ -931,9 +1098,9 @@ __global__ void __launch_bounds__(256) k_hash_batch(HashArgs a) {
     for (int q = 0; q < HB_PPT; ++q) {
         const int r = (tid + q * 256) / (HB_T / 16);
         const bool ok = m0 + r < a.n;
-        const MsgGeom g = ok ? msg_geom(a, m0 + r) : MsgGeom{nullptr, nullptr, 0, 0};
+        const MsgGeom g = ok ? msg_geom(a, m0 + r) : MsgGeom{nullptr, nullptr, 0, 0, 0};
         rp[q] = g.p;
-        rl[q] = g.len;
+        rl[q] = g.vlen;  // loads stop at the valid bytes (zero past them); the chain hashes len
     }
     __syncthreads();
     int64_t maxlen = 0;
@@ -996,7 +1163,8 @@ __global__ void __launch_bounds__(256) k_hash_batch(HashArgs a) {
     }
     const uint64_t h = hh_finalize256(st, lane, sel);
     if (live) {
-        const int64_t ss = a.sum_stride ? a.sum_stride : 32, bs = a.bad_stride ? a.bad_stride : 1;
+        const int64_t ss = a.rps > 0 ? 32 : (a.sum_stride ? a.sum_stride : 32);
+        const int64_t bs = a.rps > 0 ? 1 : (a.bad_stride ? a.bad_stride : 1);
         const int64_t out_i = a.chunk > 0 ? m0 + chain : mine.slot;
         if (a.sums) *reinterpret_cast<uint64_t*>(a.sums + out_i * ss + 8 * lane) = h;
         if (mine.exp && a.bad) {
@@ -1376,6 +1544,9 @@ hipError_t launch_encode(const EncArgs& a, hipStream_t s, int* path) {
         }
     }
     if (path) *path = PATH_GENERIC;
+    // any other geometry: encode (8-byte columns) + the batched hash in stripe mode;
+    // diagnostics 97 keeps the byte kernel reachable
+    if (encode_any_ok(a) && !(ZS3_DIAG && a.variant == 97)) return launch_encode_any(a, s);
     const int R = a.k + a.m;
     int nt = round64(4 * R);
     if (nt < 256) nt = 256;
@@ -1450,6 +1621,15 @@ hipError_t launch_reconstruct(const RecArgs& a, hipStream_t s, int* path) {
         }
     }
     if (path) *path = PATH_GENERIC;
+    if (a.e <= AMAX && a.k <= 64 && !(ZS3_DIAG && a.variant == 97)) {
+        const size_t lds = (size_t)a.e * a.k * 32 + 4 * (size_t)(a.k + a.e);
+        hipError_t e = ensure_dyn_lds((const void*)k_reconstruct_any, lds);
+        if (e != hipSuccess) return e;
+        const int64_t gx = ((a.S + 7) / 8 + 255) / 256;
+        const unsigned gy = (unsigned)(a.n_blocks < 65535 ? a.n_blocks : 65535);
+        hipLaunchKernelGGL(k_reconstruct_any, dim3((unsigned)gx, gy), dim3(256), lds, s, a);
+        return hipGetLastError();
+    }
     const size_t lds = (size_t)((a.e * a.k + 3) & ~3) + 4 * (size_t)(a.k + a.e);
     hipError_t e = ensure_dyn_lds((const void*)k_reconstruct_generic, lds);
     if (e != hipSuccess) return e;
@@ -1606,6 +1786,51 @@ hipError_t launch_verify_reconstruct(const VrArgs& a, hipStream_t s, int* path) 
     } else if (hipMemcpyAsync(rows, a.rows, (size_t)(a.k + a.e) * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
                hipStreamSynchronize(s) != hipSuccess) {
         return hipGetLastError();
+    }
+    if (a.k <= 64 && a.e <= 64 && !(ZS3_DIAG && a.variant == 97)) {
+        // survivors verified in one launch (hash kernel, stripe mode), then the rebuild,
+        // then (heal) the rebuilt rows hashed in one launch
+        HashArgs h{};
+        h.rps = a.k;
+        h.kd = a.k + a.m;
+        h.rtot = a.k + a.m;
+        h.msgs = a.shards;
+        h.stride = a.block_stride;
+        h.len = a.S;
+        h.n = a.n_blocks * a.k;
+        h.expect = a.expect;
+        h.bad = a.bad;
+        h.ids = a.ids;
+        for (int j = 0; j < a.k; ++j) h.rowmap[j] = (uint8_t)rows[j];
+        for (int q = 0; q < 4; ++q) h.key[q] = a.key[q];
+        hipError_t e = launch_hash(h, s);
+        if (e != hipSuccess || a.e == 0) return e;
+        RecArgs r{};
+        r.shards = a.shards;
+        r.block_stride = a.block_stride;
+        r.S = a.S;
+        r.n_blocks = a.n_blocks;
+        r.tables = a.tables;
+        r.coef = a.coef;
+        r.rows = a.rows;
+        r.k = a.k;
+        r.e = a.e;
+        r.ids = a.ids;
+        e = launch_reconstruct(r, s, nullptr);
+        if (e != hipSuccess || !a.sums_out) return e;
+        HashArgs g{};
+        g.rps = a.e;
+        g.kd = a.k + a.m;
+        g.rtot = a.k + a.m;
+        g.msgs = a.shards;
+        g.stride = a.block_stride;
+        g.len = a.S;
+        g.n = a.n_blocks * a.e;
+        g.sums = a.sums_out;
+        g.ids = a.ids;
+        for (int j = 0; j < a.e; ++j) g.rowmap[j] = (uint8_t)rows[a.k + j];
+        for (int q = 0; q < 4; ++q) g.key[q] = a.key[q];
+        return launch_hash(g, s);
     }
     for (int j = 0; j < a.k; ++j) {
         HashArgs h{};

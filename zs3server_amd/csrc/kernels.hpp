@@ -90,6 +90,17 @@ struct HashArgs {
     int64_t nchunks;          // chunks per file
     int64_t last_len;         // length of each file's last chunk
     int variant;              // diagnostics build only (0 = tuned default)
+    // stripe mode (rps > 0): message i = shard rowmap[i % rps] of stripe i / rps (slot
+    // ids[stripe] if ids); shard idx < kd at msgs + slot*stride + idx*len, else at
+    // par + slot*par_stride + (idx-kd)*len; sums / expect / bad at slot*rtot + idx;
+    // bytes of data shard idx at or past vlim - idx*len read as zero (Split padding)
+    int rps;
+    int kd;
+    int rtot;
+    int64_t vlim;             // valid bytes of the stripe's data (EncodeData's len); 0 = all
+    const uint8_t* par;
+    int64_t par_stride;
+    uint8_t rowmap[64];
 };
 
 // GET / heal pass: verify the k survivor shards the decode reads

@@ -158,7 +158,9 @@ def transfer(state, insns, report, name):
             continue
         touched = regs(args)
         is_vmem = op.startswith(VMEM)
-        is_asm_load = is_vmem and is_asm and "load" in op
+        # an LDS-DMA load (global_load_lds_*, buffer_load ... lds) has no VGPR destination:
+        # its first operand is the address; it only ages the other loads
+        is_asm_load = is_vmem and is_asm and "load" in op and "_lds" not in op and not args.rstrip().endswith(" lds")
         if not is_asm_load:
             hit = [r for r in st if r & touched]
             if hit and report:

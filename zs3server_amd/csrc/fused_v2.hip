@@ -1042,8 +1042,11 @@ static int launch_ehx_default(const EncArgs& a, hipStream_t s) {
             return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3>(a, s) ? PATH_WS : PATH_NONE;
         return launch_ws_t<K, M, 4, 512, 4, false, true, 83968, false, 0, 0, false, 3>(a, s) ? PATH_WS : PATH_NONE;
     } else if constexpr (K == 4 && M == 2) {
+        // config 2 (1024 objects, 6 144 chains: the chain latency sets the pace): 2 KiB
+        // tiles, so each chain runs 64 packets between barriers (0.397 -> 0.364 ms over
+        // 512-byte tiles, profiles/r03/ab_config2_tiles.jsonl)
         if (n >= 1024 && n <= 8 * 256)
-            return launch_ws_t<K, M, 4, 512, 4, false, true, 83968, false, 0, 0, false, 3>(a, s) ? PATH_WS : PATH_NONE;
+            return launch_ws_t<K, M, 4, 2048, 2, false, true, 83968, false, 0, 0, false, 3>(a, s) ? PATH_WS : PATH_NONE;
         if (n <= 8 * 256)
             return launch_ws_t<K, M, 4, 512, 4, false, true, 83968, false, 0, 0, false, 2>(a, s) ? PATH_WS : PATH_NONE;
         return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3>(a, s) ? PATH_WS : PATH_NONE;
@@ -1490,14 +1493,15 @@ static bool launch_vr_ws_bt(const VrArgs& a, hipStream_t s) {
 
 #if ZS3_DIAG
 // RS(16+4) rebuild / heal with the survivor prefetch depth and tile length as
-// parameters (diagnostics 250-257, round 3): e = 1..4 rebuilt rows.
-template <int T, int PF, bool HOUT, int BT>
+// parameters (diagnostics 250-259, round 3; PF = 2 with 8-byte columns spills
+// in-flight load registers, scripts/check_async_loads.py, so no such instance): e = 1..4 rebuilt rows.
+template <int T, int PF, bool HOUT, int BT, int CW = 4>
 static bool vr16(const VrArgs& a, hipStream_t s) {
     switch (a.e) {
-        case 1: return launch_vr_ws_t<16, 1, HOUT, 8, T, PF, 4, false, true, BT>(a, s);
-        case 2: return launch_vr_ws_t<16, 2, HOUT, 8, T, PF, 4, false, true, BT>(a, s);
-        case 3: return launch_vr_ws_t<16, 3, HOUT, 8, T, PF, 4, false, true, BT>(a, s);
-        case 4: return launch_vr_ws_t<16, 4, HOUT, 8, T, PF, 4, false, true, BT>(a, s);
+        case 1: return launch_vr_ws_t<16, 1, HOUT, 8, T, PF, CW, false, true, BT>(a, s);
+        case 2: return launch_vr_ws_t<16, 2, HOUT, 8, T, PF, CW, false, true, BT>(a, s);
+        case 3: return launch_vr_ws_t<16, 3, HOUT, 8, T, PF, CW, false, true, BT>(a, s);
+        case 4: return launch_vr_ws_t<16, 4, HOUT, 8, T, PF, CW, false, true, BT>(a, s);
         default: return false;
     }
 }
@@ -1509,7 +1513,7 @@ static bool vr16(const VrArgs& a, hipStream_t s) {
 bool launch_vr_ws(int v, const VrArgs& a, hipStream_t s) {
     if (!ZS3_DIAG && v != 0) return false;
 #if ZS3_DIAG
-    if (a.k == 16 && v >= 250 && v <= 257 && a.e >= 1) {
+    if (a.k == 16 && v >= 250 && v <= 259 && a.e >= 1) {
         const bool h = a.sums_out != nullptr;
         switch (v) {
             case 250: return h ? vr16<128, 2, true, 4>(a, s) : vr16<256, 2, false, 0>(a, s);
@@ -1518,6 +1522,9 @@ bool launch_vr_ws(int v, const VrArgs& a, hipStream_t s) {
             case 253: return h ? vr16<256, 1, true, 4>(a, s) : vr16<512, 1, false, 0>(a, s);
             case 254: return h ? vr16<128, 3, true, 4>(a, s) : vr16<128, 2, false, 0>(a, s);
             case 255: return h ? vr16<256, 2, true, 0>(a, s) : vr16<256, 2, false, 4>(a, s);
+            case 256: return h ? vr16<256, 1, true, 4, 8>(a, s) : vr16<512, 1, false, 4, 8>(a, s);
+            case 257: return h ? vr16<512, 1, true, 4, 8>(a, s) : vr16<256, 2, false, 4, 8>(a, s);
+            case 259: return h ? vr16<384, 1, true, 4, 8>(a, s) : vr16<384, 1, false, 4, 8>(a, s);
             default: return false;
         }
     }
@@ -1719,6 +1726,7 @@ int launch_ehx(int v, const EncArgs& a, hipStream_t s) {
         return PATH_NONE;
     }
 #if ZS3_DIAG
+    if (v == 190) return launch_ehx_dma(v, a, s);
     bool ok = false;
     if (a.k == 8 && a.m == 4) ok = launch_ehx_km<8, 4>(v, a, s);
     if (a.k == 4 && a.m == 2) ok = launch_ehx_km<4, 2>(v, a, s);

@@ -158,6 +158,8 @@ int launch_ehx(int v, const EncArgs& a, hipStream_t s);
 // Fused encode + sums for shard sizes that are not a multiple of 16 (k_ehx_ws UA mode,
 // e.g. RS(12+4) on 1 MiB blocks); PATH_NONE when the shape has no such instance.
 int launch_ehx_ua(const EncArgs& a, hipStream_t s);
+// LDS-DMA fused encode (fused_dma.hip); PATH_NONE when the shape / layout does not fit.
+int launch_ehx_dma(int v, const EncArgs& a, hipStream_t s);
 // Warp-specialised GET / heal pass (fused_v2.hip); false if the shape has no instance.
 bool launch_vr_ws(int v, const VrArgs& a, hipStream_t s);
 

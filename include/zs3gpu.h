@@ -268,7 +268,10 @@ void zs3_split_range(int64_t total, int world, int rank, int64_t* lo, int64_t* h
  * little work for one device round trip.  A queue gathers the blocks that concurrent
  * callers (OS threads: every goroutine inside cgo holds one) submit into device
  * batches on pinned staging slots, each slot with its own stream:
- *   - a block is copied into the queue's pinned staging by its submitting thread;
+ *   - a block is copied into the queue's pinned staging by its submitting thread, or,
+ *     when the caller's buffer lies inside a zs3_host_alloc allocation (the pinned
+ *     bpool) and holds a full-size block, DMA'd from it directly (zero-copy: no host
+ *     memcpy either way; parity / rebuilt rows are DMA'd straight back into it);
  *   - a batch is launched when it is full, when fewer than slots-1 batches of its lane
  *     are in flight (batch while busy), when its oldest block has waited max_wait_us,
  *     or on flush;
@@ -282,7 +285,9 @@ typedef struct zs3_queue zs3_queue;
 typedef struct zs3_req zs3_req;
 typedef struct {
     int device;       /* HIP device ordinal; -1 = the calling thread's current device */
-    int max_batch;    /* blocks per device batch (0 = 128) */
+    int max_batch;    /* blocks per device batch (0 = 128).  Memory per lane in use:
+                         slots x max_batch x (k+m) x S of pinned host AND of device
+                         memory (+ sums); RS(8+4) 1 MiB, 4 slots, 128: 768 MiB each */
     int max_wait_us;  /* longest a block waits for its batch to fill (0 = 200) */
     int slots;        /* pinned staging slots (+ streams) per lane (0 = 4; at least 2) */
 } zs3_queue_opts;
@@ -318,6 +323,7 @@ int zs3_queue_submit_decode(zs3_queue* q, uint8_t* h_shards, int64_t shard_len, 
 int64_t zs3_req_wait(zs3_req* req);
 int zs3_queue_flush(zs3_queue* q);   /* launch the open batches now */
 int zs3_queue_stats(const zs3_queue* q, int64_t* batches, int64_t* blocks);
+int64_t zs3_queue_zero_copy_blocks(const zs3_queue* q);  /* blocks DMA'd from / to pinned callers */
 
 /* Synchronous conveniences (submit + wait): what the cgo shim calls per block. */
 int64_t zs3_queue_encode_data(zs3_queue* q, uint8_t* h_buf, int64_t len, int64_t cap, uint8_t* h_sums);

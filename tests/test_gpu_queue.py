@@ -214,3 +214,67 @@ def test_queue_batches_concurrent_blocks(oracle):
     batches, blocks = q.stats()
     assert blocks == 128 and batches < blocks
     q.close()
+
+
+@pytest.mark.parametrize("k,m,bs", [(8, 4, 1 << 20), (5, 3, 100000)])
+def test_queue_zero_copy_pinned_callers(oracle, k, m, bs):
+    """Callers whose block buffers come from zs3_host_alloc (the pinned bpool) are
+    served zero-copy (the DMA engine reads the data rows from, and writes the parity
+    rows / rebuilt rows into, the caller's buffer), side by side in the same batches
+    with pageable callers and with pinned callers' short last blocks (staged); every
+    result vs the oracle, and the queue reports the zero-copy blocks."""
+    codec = z.Codec(k, m, bs)
+    q = z.Queue(codec, max_batch=16, max_wait_us=500)
+    R = k + m
+    S = -(-bs // k)
+    mat = oracle.build_matrix(k, m)
+    nthr, per = 8, 4
+    pins = [z.HostBuffer(R * S + 64) for _ in range(nthr)]
+    pins_dec = [z.HostBuffer(R * S) for _ in range(nthr)]
+
+    def worker(t):
+        pinned = t % 2 == 0
+        for i in range(per):
+            short = i == per - 1 and t % 4 == 0
+            ln = bs // 3 + 7 if short else bs
+            data = oracle.fill(700 + t, i, ln)
+            Sb = -(-ln // k)
+            buf = pins[t].array[:R * Sb + 64] if pinned else np.zeros(R * Sb + 64, np.uint8)
+            buf[:] = 0xEE
+            buf[:ln] = data
+            got_S, sums = q.encode_data(buf, ln)
+            want = oracle.encode_data(k, m, data, mat)
+            assert got_S == Sb
+            assert np.array_equal(buf[:R * Sb].reshape(R, Sb), want), (t, i)
+            assert np.array_equal(sums, oracle.hh256_rows(KEY, want)), (t, i)
+            # GET / heal of a full stripe from the pinned (or pageable) caller buffer
+            sh, ssum = _stripe(oracle, k, m, bs, 800 + t, i)
+            work = pins_dec[t].array.reshape(R, S) if pinned else np.zeros((R, S), np.uint8)
+            work[:] = sh
+            present = np.ones(R, bool)
+            present[[(i + t) % k, k + (t % m)]] = False
+            work[~present] = 0x5A
+            heal = i % 2 == 1
+            out = np.zeros((R, 32), np.uint8) if heal else None
+            bad = np.full(R, 9, np.int32)
+            assert q.decode(work, present, not heal, expect=ssum, bad=bad, sums_out=out) == 0, (t, i)
+            assert not bad.any()
+            for r in range(R):
+                if present[r] or r < k or heal:
+                    assert np.array_equal(work[r], sh[r]), (t, i, r)
+                else:
+                    assert (work[r] == 0x5A).all(), "DecodeDataBlocks leaves missing parity alone"
+            if heal:
+                for r in np.nonzero(~present)[0]:
+                    assert np.array_equal(out[r], ssum[r]), (t, i, r)
+
+    run_threads(nthr, worker)
+    batches, blocks = q.stats()
+    assert blocks == nthr * per * 2
+    zc = q.zero_copy_blocks()
+    # pinned threads: every full encode block and every decode block
+    n_short = sum(1 for t in range(0, nthr, 2) if t % 4 == 0)
+    assert zc == (nthr // 2) * per * 2 - n_short, zc
+    q.close()
+    for p in pins + pins_dec:
+        p.free()

@@ -4,7 +4,9 @@
 // synchronously (submit + wait per block, as EncodeData returns before the next block
 // is read).  Prints one JSON line per T: aggregate GiB/s of object bytes, per-block
 // latency p50 / p99, blocks per device batch.
-//   tools/queue_bench [T,T,...] [per] [k] [m] [max_batch] [slots]
+//   tools/queue_bench [T,T,...] [per] [k] [m] [max_batch] [slots] [pinned]
+// pinned = 1: every caller's block buffer comes from zs3_host_alloc (the pinned bpool),
+// so the queue DMAs it zero-copy; 0 (default): pageable buffers, staged by memcpy.
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -40,7 +42,18 @@ int main(int argc, char** argv) {
     zs3_queue* q = nullptr;
     if (zs3_queue_new(c, &o, &q) != ZS3_OK) return 3;
     const int tmax = *std::max_element(Ts.begin(), Ts.end());
-    std::vector<std::vector<uint8_t>> bufs(tmax, std::vector<uint8_t>((size_t)(R * S)));
+    const bool pinned = argc > 7 && std::atoi(argv[7]) != 0;
+    std::vector<std::vector<uint8_t>> pageable(pinned ? 0 : tmax, std::vector<uint8_t>((size_t)(R * S)));
+    std::vector<uint8_t*> bufs(tmax);
+    for (int t = 0; t < tmax; ++t) {
+        if (pinned) {
+            void* p = nullptr;
+            if (zs3_host_alloc(&p, (size_t)(R * S)) != ZS3_OK) return 4;
+            bufs[t] = (uint8_t*)p;
+        } else {
+            bufs[t] = pageable[t].data();
+        }
+    }
     std::vector<std::vector<uint8_t>> sums(tmax, std::vector<uint8_t>((size_t)(R * 32)));
     for (int t = 0; t < tmax; ++t)
         for (int64_t i = 0; i < B; ++i) bufs[t][(size_t)i] = (uint8_t)(i * 131 + t * 7 + (i >> 9));
@@ -56,7 +69,7 @@ int main(int argc, char** argv) {
                 th.emplace_back([&, t] {
                     for (int i = 0; i < per; ++i) {
                         const auto a = Clock::now();
-                        if (zs3_queue_encode_data(q, bufs[t].data(), B, R * S, sums[t].data()) != S) errs++;
+                        if (zs3_queue_encode_data(q, bufs[t], B, R * S, sums[t].data()) != S) errs++;
                         lat[t].push_back(std::chrono::duration<double, std::micro>(Clock::now() - a).count());
                     }
                 });
@@ -67,15 +80,17 @@ int main(int argc, char** argv) {
             for (auto& v : lat) all.insert(all.end(), v.begin(), v.end());
             std::sort(all.begin(), all.end());
             if (rep == 1)
-                std::printf("{\"path\": \"queue_encode_native\", \"k\": %d, \"m\": %d, \"threads\": %d, \"blocks\": %d, "
+                std::printf("{\"path\": \"queue_encode_native\", \"pinned\": %s, \"k\": %d, \"m\": %d, \"threads\": %d, \"blocks\": %d, "
                             "\"GiBps\": %.2f, \"block_latency_us_p50\": %.1f, \"block_latency_us_p99\": %.1f, "
                             "\"blocks_per_batch\": %.1f, \"errors\": %d}\n",
-                            k, m, T, T * per, (double)T * per * B / dt / (1 << 30), all[all.size() / 2],
+                            pinned ? "true" : "false", k, m, T, T * per, (double)T * per * B / dt / (1 << 30), all[all.size() / 2],
                             all[(size_t)(all.size() * 0.99)], (double)(n1 - n0) / std::max<int64_t>(1, b1 - b0),
                             errs.load());
             std::fflush(stdout);
         }
     zs3_queue_free(q);
+    if (pinned)
+        for (auto* p : bufs) zs3_host_free(p);
     zs3_codec_free(c);
     return 0;
 }

@@ -53,7 +53,7 @@ EXPORTS = [
     "zs3_last_path", "zs3_reconstruct_batch_masks", "zs3_verify_reconstruct_batch_masks",
     "zs3_hh256_batch_ragged", "zs3_bitrot_verify_file_batch", "zs3_codec_params",
     "zs3_queue_new", "zs3_queue_free", "zs3_queue_submit_encode", "zs3_queue_submit_decode", "zs3_req_wait",
-    "zs3_queue_flush", "zs3_queue_stats", "zs3_queue_encode_data", "zs3_queue_decode_data_blocks",
+    "zs3_queue_flush", "zs3_queue_stats", "zs3_queue_zero_copy_blocks", "zs3_queue_encode_data", "zs3_queue_decode_data_blocks",
     "zs3_stream_encode_multi", "zs3_split_range",
 ]
 # include/zs3gpu_diag.h: exported by the diagnostics build only
@@ -164,6 +164,8 @@ def _load(path):
     L.zs3_req_wait.restype = i64
     L.zs3_queue_flush.argtypes = [vp]
     L.zs3_queue_stats.argtypes = [vp, C.POINTER(i64), C.POINTER(i64)]
+    L.zs3_queue_zero_copy_blocks.argtypes = [vp]
+    L.zs3_queue_zero_copy_blocks.restype = i64
     L.zs3_queue_encode_data.argtypes = [vp, vp, i64, i64, vp]
     L.zs3_queue_encode_data.restype = i64
     L.zs3_queue_decode_data_blocks.argtypes = [vp, vp, i64, vp, C.c_int, vp, vp]
@@ -400,6 +402,10 @@ class Queue:
         b, n = C.c_int64(0), C.c_int64(0)
         _check(self._L.zs3_queue_stats(self._h, C.byref(b), C.byref(n)))
         return b.value, n.value
+
+    def zero_copy_blocks(self) -> int:
+        """Blocks whose bytes were DMA'd straight from / to a pinned caller buffer."""
+        return int(self._L.zs3_queue_zero_copy_blocks(self._h))
 
 
 class HostBuffer:

@@ -52,6 +52,8 @@
 
 #include "../../include/zs3gpu.h"
 
+bool zs3i_pinned(const void* p, size_t n);  // zs3gpu.hip: inside a live zs3_host_alloc range
+
 namespace {
 
 enum Lane { ENC = 0, GET = 1, HEAL = 2, NLANE = 3 };
@@ -78,6 +80,8 @@ struct zs3_req {
     int32_t* h_bad = nullptr;
     uint8_t* h_sums_out = nullptr;
     int status = ZS3_OK;   // the block's status at launch (its pattern's reedsolomon error)
+    bool zc = false;       // zero-copy: the caller's buffer is pinned (zs3_host_alloc), so the
+                           // DMA engine moves its bytes to / from the device slot directly
     bool done = false;     // results copied out (completer)
     int64_t result = 0;    // zs3_req_wait's return value
 };
@@ -119,7 +123,8 @@ struct zs3_queue {
     std::condition_variable cv_done;    // a slot finished
     std::condition_variable cv_comp;    // completer: a slot was launched
     std::vector<Slot> slots[NLANE];
-    bool alloc_failed[NLANE] = {false, false, false};
+    enum { LANE_NONE, LANE_INIT, LANE_READY };
+    int lane_state[NLANE] = {LANE_NONE, LANE_NONE, LANE_NONE};
     Slot* open[NLANE] = {nullptr, nullptr, nullptr};
     int inflight[NLANE] = {0, 0, 0};
     std::deque<Slot*> launched;
@@ -127,7 +132,7 @@ struct zs3_queue {
     bool stop = false;       // dispatcher: drain the open slots and exit
     bool comp_stop = false;  // completer: exit once every launched slot is done
     std::thread disp, comp;
-    std::atomic<int64_t> n_batches{0}, n_blocks{0};
+    std::atomic<int64_t> n_batches{0}, n_blocks{0}, n_zc{0};
 
     // region offsets inside a slot (bytes).  ENCODE: [cap][k*S] data rows, then
     // [cap][m*S] parity rows (each direction one contiguous DMA copy of the bytes that
@@ -145,23 +150,31 @@ namespace {
 
 int map_hip(hipError_t e) { return e == hipSuccess ? ZS3_OK : (e == hipErrorOutOfMemory ? ZS3_ERR_NOMEM : ZS3_ERR_DEVICE); }
 
-// Allocate a lane's slots on first use (caller holds q->mu; runs on a submitter).
-int ensure_lane(zs3_queue* q, int lane) {
-    if (!q->slots[lane].empty()) return ZS3_OK;
-    if (q->alloc_failed[lane]) return ZS3_ERR_NOMEM;
+// Allocate a lane's slots on first use (runs on a submitter; lk is held on entry and
+// on return, but the allocation itself runs unlocked so the dispatcher and completer
+// keep serving the other lanes; other submitters of this lane wait for it).  A failed
+// allocation leaves the lane unallocated, so a later submit retries.
+int ensure_lane(zs3_queue* q, std::unique_lock<std::mutex>& lk, int lane) {
+    for (;;) {
+        if (q->lane_state[lane] == zs3_queue::LANE_READY) return ZS3_OK;
+        if (q->lane_state[lane] == zs3_queue::LANE_NONE) break;
+        q->cv_space.wait(lk);
+    }
+    q->lane_state[lane] = zs3_queue::LANE_INIT;
+    const size_t bytes = q->slot_bytes(lane);
+    const int nslots = q->nslots, cap = q->cap, device = q->device;
+    lk.unlock();
     int prev = 0;
     (void)hipGetDevice(&prev);
-    if (hipSetDevice(q->device) != hipSuccess) return ZS3_ERR_DEVICE;
-    std::vector<Slot> v((size_t)q->nslots);
-    int rc = ZS3_OK;
-    const size_t bytes = q->slot_bytes(lane);
+    std::vector<Slot> v((size_t)nslots);
+    int rc = map_hip(hipSetDevice(device));
     for (auto& s : v) {
         s.lane = lane;
         if (rc == ZS3_OK) rc = map_hip(hipHostMalloc((void**)&s.h, bytes, hipHostMallocDefault));
         if (rc == ZS3_OK) rc = map_hip(hipMalloc((void**)&s.d, bytes));
         if (rc == ZS3_OK) rc = map_hip(hipEventCreateWithFlags(&s.done_ev, hipEventDisableTiming));
         if (rc == ZS3_OK) rc = map_hip(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
-        s.claimed.reset(new std::atomic<uint8_t>[(size_t)q->cap]);
+        s.claimed.reset(new std::atomic<uint8_t>[(size_t)cap]);
     }
     if (rc != ZS3_OK) {
         for (auto& s : v) {
@@ -170,17 +183,33 @@ int ensure_lane(zs3_queue* q, int lane) {
             if (s.done_ev) (void)hipEventDestroy(s.done_ev);
             if (s.stream) (void)hipStreamDestroy(s.stream);
         }
-        q->alloc_failed[lane] = true;
-    } else {
-        q->slots[lane] = std::move(v);
     }
     (void)hipSetDevice(prev);
+    lk.lock();
+    if (rc == ZS3_OK) q->slots[lane] = std::move(v);
+    q->lane_state[lane] = rc == ZS3_OK ? zs3_queue::LANE_READY : zs3_queue::LANE_NONE;
+    q->cv_space.notify_all();
     return rc;
+}
+
+// Calls f(a, b) for every maximal run [a, b) of positions < n with skip[pos] == 0.
+template <class F>
+void for_runs(const std::vector<uint8_t>& skip, int n, F f) {
+    for (int i = 0; i < n;) {
+        if (skip[(size_t)i]) {
+            ++i;
+            continue;
+        }
+        int j = i;
+        while (j < n && !skip[(size_t)j]) ++j;
+        f(i, j);
+        i = j;
+    }
 }
 
 // Reserve a position for one block in the lane's open slot (caller holds lk).
 int reserve(zs3_queue* q, std::unique_lock<std::mutex>& lk, zs3_req* r, bool full) {
-    int rc = ensure_lane(q, r->lane);
+    int rc = ensure_lane(q, lk, r->lane);
     if (rc) return rc;
     for (;;) {
         if (q->stop) return ZS3_ERR_INVALID_ARG;
@@ -232,9 +261,23 @@ void launch_slot(zs3_queue* q, Slot* s) {
         // full-size blocks: data rows in, one fused launch, parity rows + sums out
         const size_t KS = (size_t)k * S, MS = (size_t)m * S, po = q->off_par();
         if (nf > 0) {
-            chk(map_hip(hipMemcpyAsync(s->d, s->h, (size_t)nf * KS, hipMemcpyHostToDevice, st)));
+            // staged blocks: one DMA per run of staged positions each way; zero-copy
+            // blocks were copied in by their submitter and get their parity rows
+            // straight back into the caller's buffer
+            std::vector<uint8_t> zc((size_t)nf, 0);
+            for (zs3_req* r : s->reqs)
+                if (r->pos < nf && r->zc) zc[(size_t)r->pos] = 1;
+            for_runs(zc, nf, [&](int a, int b) {
+                chk(map_hip(hipMemcpyAsync(s->d + a * KS, s->h + a * KS, (size_t)(b - a) * KS, hipMemcpyHostToDevice, st)));
+            });
             chk(zs3_encode_batch(q->c, s->d, (int64_t)KS, q->B, nf, s->d + po, (int64_t)MS, dsum, st));
-            chk(map_hip(hipMemcpyAsync(s->h + po, s->d + po, (size_t)nf * MS, hipMemcpyDeviceToHost, st)));
+            for_runs(zc, nf, [&](int a, int b) {
+                chk(map_hip(hipMemcpyAsync(s->h + po + a * MS, s->d + po + a * MS, (size_t)(b - a) * MS,
+                                           hipMemcpyDeviceToHost, st)));
+            });
+            for (zs3_req* r : s->reqs)
+                if (r->pos < nf && r->zc)
+                    chk(map_hip(hipMemcpyAsync(r->h_buf + KS, s->d + po + r->pos * MS, MS, hipMemcpyDeviceToHost, st)));
             chk(map_hip(hipMemcpyAsync(hsum, dsum, (size_t)nf * R * 32, hipMemcpyDeviceToHost, st)));
         }
         for (zs3_req* r : s->reqs) {
@@ -255,7 +298,13 @@ void launch_slot(zs3_queue* q, Slot* s) {
         std::vector<uint8_t> pres;
         std::vector<int32_t> status;
         if (nf > 0) {
-            chk(map_hip(hipMemcpyAsync(s->d, s->h, (size_t)nf * E, hipMemcpyHostToDevice, st)));
+            std::vector<uint8_t> zc((size_t)nf, 0);
+            for (zs3_req* r : s->reqs)
+                if (r->pos < nf && r->zc) zc[(size_t)r->pos] = 1;
+            for_runs(zc, nf, [&](int a, int b) {
+                chk(map_hip(hipMemcpyAsync(s->d + (size_t)a * E, s->h + (size_t)a * E, (size_t)(b - a) * E,
+                                           hipMemcpyHostToDevice, st)));
+            });
             chk(map_hip(hipMemcpyAsync(dsum, hsum, (size_t)nf * R * 32, hipMemcpyHostToDevice, st)));
             pres.assign((size_t)nf * R, 0);
             status.assign((size_t)nf, ZS3_OK);
@@ -284,13 +333,15 @@ void launch_slot(zs3_queue* q, Slot* s) {
             chk(map_hip(hipMemcpyAsync(hbad + bo, (uint8_t*)dbad + bo, (size_t)R * 4, hipMemcpyDeviceToHost, st)));
             if (dout) chk(map_hip(hipMemcpyAsync(hout + so, dout + so, (size_t)R * 32, hipMemcpyDeviceToHost, st)));
         }
-        // rebuilt rows back to the pinned slot (only those, per block)
+        // rebuilt rows back to the pinned slot (only those, per block), or straight into
+        // a zero-copy caller's shard rows
         for (zs3_req* r : s->reqs) {
             if (r->status != ZS3_OK) continue;
             const size_t o = (size_t)r->pos * E;
+            uint8_t* hdst = r->zc ? r->h_shards : s->h + o;
             for (int i = 0; i < R; ++i)
                 if (!r->present[i] && (i < k || !data_only))
-                    chk(map_hip(hipMemcpyAsync(s->h + o + (size_t)i * r->S, s->d + o + (size_t)i * r->S, (size_t)r->S,
+                    chk(map_hip(hipMemcpyAsync(hdst + (size_t)i * r->S, s->d + o + (size_t)i * r->S, (size_t)r->S,
                                                hipMemcpyDeviceToHost, st)));
         }
     }
@@ -355,15 +406,16 @@ void finish_req(zs3_queue* q, Slot* s, zs3_req* r) {
     const int k = q->k, R = q->R;
     if (rc == ZS3_OK) {
         if (r->lane == ENC) {
-            std::memcpy(r->h_buf + (size_t)k * r->S, s->h + q->off_par() + (size_t)r->pos * q->m * q->S,
-                        (size_t)(q->m * r->S));
+            if (!r->zc)
+                std::memcpy(r->h_buf + (size_t)k * r->S, s->h + q->off_par() + (size_t)r->pos * q->m * q->S,
+                            (size_t)(q->m * r->S));
             if (k * r->S > r->len)
                 std::memset(r->h_buf + r->len, 0, (size_t)(k * r->S - r->len));  // Split zero-fill in place
             if (r->h_sums) std::memcpy(r->h_sums, s->h + q->off_sums() + (size_t)r->pos * R * 32, (size_t)R * 32);
             rc = r->S;
         } else {
             const int data_only = r->lane == GET;
-            for (int i = 0; i < R; ++i)
+            for (int i = 0; i < R && !r->zc; ++i)
                 if (!r->present[i] && (i < k || !data_only))
                     std::memcpy(r->h_shards + (size_t)i * r->S, s->h + o + (size_t)i * r->S, (size_t)r->S);
             const int32_t* bad = (const int32_t*)(s->h + q->off_bad()) + (size_t)r->pos * R;
@@ -515,10 +567,19 @@ int zs3_queue_submit_encode(zs3_queue* q, uint8_t* h_buf, int64_t len, int64_t c
         }
         s = r->slot;
     }
-    // Split (reedsolomon): data rows are the input bytes, zero-padded to k*S
-    uint8_t* dst = s->h + (size_t)r->pos * q->k * q->S;
-    std::memcpy(dst, h_buf, (size_t)len);
-    if (q->k * Sb > len) std::memset(dst + len, 0, (size_t)(q->k * Sb - len));
+    // Split (reedsolomon): data rows are the input bytes, zero-padded to k*S (the
+    // kernel reads the pad of a full block as zero).  A full block in pinned memory is
+    // DMA'd from the caller's buffer on the slot's stream, ahead of the batch's launch.
+    const size_t KS = (size_t)q->k * q->S;
+    if (len == q->B && zs3i_pinned(h_buf, (size_t)q->R * q->S))
+        r->zc = hipMemcpyAsync(s->d + (size_t)r->pos * KS, h_buf, (size_t)len, hipMemcpyHostToDevice, s->stream) ==
+                hipSuccess;
+    if (r->zc) q->n_zc.fetch_add(1);
+    if (!r->zc) {
+        uint8_t* dst = s->h + (size_t)r->pos * KS;
+        std::memcpy(dst, h_buf, (size_t)len);
+        if (q->k * Sb > len) std::memset(dst + len, 0, (size_t)(q->k * Sb - len));
+    }
     copy_in_done(q, s);
     *req = r;
     return ZS3_OK;
@@ -550,8 +611,21 @@ int zs3_queue_submit_decode(zs3_queue* q, uint8_t* h_shards, int64_t shard_len, 
         }
         s = r->slot;
     }
+    // survivors: DMA'd straight from a pinned caller buffer (runs of present rows, same
+    // row layout as the slot), else copied into the pinned slot
+    if (shard_len == q->S && zs3i_pinned(h_shards, (size_t)q->E)) {
+        std::vector<uint8_t> absent((size_t)q->R);
+        for (int i = 0; i < q->R; ++i) absent[(size_t)i] = !r->present[i];
+        bool ok = true;
+        for_runs(absent, q->R, [&](int a, int b) {
+            ok &= hipMemcpyAsync(s->d + (size_t)r->pos * q->E + (size_t)a * q->S, h_shards + (size_t)a * q->S,
+                                 (size_t)(b - a) * q->S, hipMemcpyHostToDevice, s->stream) == hipSuccess;
+        });
+        r->zc = ok;
+        if (ok) q->n_zc.fetch_add(1);
+    }
     uint8_t* dst = s->h + (size_t)r->pos * q->E;
-    for (int i = 0; i < q->R; ++i)
+    for (int i = 0; i < q->R && !r->zc; ++i)
         if (r->present[i]) std::memcpy(dst + (size_t)i * shard_len, h_shards + (size_t)i * shard_len, (size_t)shard_len);
     uint8_t* exp = s->h + q->off_sums() + (size_t)r->pos * q->R * 32;
     if (h_expect)
@@ -598,6 +672,8 @@ int zs3_queue_stats(const zs3_queue* q, int64_t* batches, int64_t* blocks) {
     if (blocks) *blocks = q->n_blocks.load();
     return ZS3_OK;
 }
+
+int64_t zs3_queue_zero_copy_blocks(const zs3_queue* q) { return q ? q->n_zc.load() : ZS3_ERR_INVALID_ARG; }
 
 int64_t zs3_queue_encode_data(zs3_queue* q, uint8_t* h_buf, int64_t len, int64_t cap, uint8_t* h_sums) {
     zs3_req* r = nullptr;

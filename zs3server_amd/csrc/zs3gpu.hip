@@ -299,7 +299,23 @@ Staging* staging(size_t dbytes, size_t hbytes) {
 
 size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
+// Live zs3_host_alloc ranges (base -> bytes): the queue DMAs straight from / to a
+// caller buffer that lies in one of them (the pinned bpool, internal/bpool/bpool.go:29)
+std::mutex g_pin_mu;
+std::map<uintptr_t, size_t> g_pinned;
+
 }  // namespace
+
+// [p, p+n) inside one live zs3_host_alloc allocation (queue.hip's zero-copy test)
+__attribute__((visibility("hidden"))) bool zs3i_pinned(const void* p, size_t n) {
+    if (!p) return false;
+    const uintptr_t a = (uintptr_t)p;
+    std::lock_guard<std::mutex> g(g_pin_mu);
+    auto it = g_pinned.upper_bound(a);
+    if (it == g_pinned.begin()) return false;
+    --it;
+    return a >= it->first && a - it->first <= it->second && n <= it->second - (a - it->first);
+}
 
 extern "C" {
 
@@ -335,9 +351,20 @@ int zs3_dev_alloc(void** d_ptr, size_t bytes) {
 int zs3_dev_free(void* d_ptr) { return map_hip(hipFree(d_ptr)); }
 int zs3_host_alloc(void** h_ptr, size_t bytes) {
     if (!h_ptr) return ZS3_ERR_INVALID_ARG;
-    return map_hip(hipHostMalloc(h_ptr, bytes, hipHostMallocDefault));
+    const int rc = map_hip(hipHostMalloc(h_ptr, bytes, hipHostMallocDefault));
+    if (rc == ZS3_OK && *h_ptr) {
+        std::lock_guard<std::mutex> g(g_pin_mu);
+        g_pinned[(uintptr_t)*h_ptr] = bytes;
+    }
+    return rc;
 }
-int zs3_host_free(void* h_ptr) { return map_hip(hipHostFree(h_ptr)); }
+int zs3_host_free(void* h_ptr) {
+    {
+        std::lock_guard<std::mutex> g(g_pin_mu);
+        g_pinned.erase((uintptr_t)h_ptr);
+    }
+    return map_hip(hipHostFree(h_ptr));
+}
 int zs3_memcpy_h2d(void* d, const void* h, size_t bytes, void* stream) {
     return map_hip(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, (hipStream_t)stream));
 }

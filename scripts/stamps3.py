@@ -64,12 +64,14 @@ for v in [int(x) for x in os.environ.get("VARIANTS", "50").split(",")]:
     simdkey = Counter([(a, b, c, e, int(f)) for (a, b, c, e), f in zip(cukey, simd)])
     print("  waves per SIMD histogram:", sorted(Counter(simdkey.values()).items()))
     print("  (wave index in a 12-wave workgroup, SIMD) counts:", sorted(Counter(zip(wid.tolist(), simd.tolist())).items())[:24])
-    wait = (d[:, 4] >> 8).double()  # barrier-wait shader cycles (variants built with WT)
+    wait = ((d[:, 4] >> 8) & 0xFFFFFFF).double()  # barrier-wait shader cycles (variants built with WT)
+    vwait = (d[:, 4] >> 36).double()  # encode role: cycles waiting for its tile's loads (WT)
     for r in range(12):
         sel = wid == r
         if sel.any():
             print(f"  wave {r:2d}: life mean {float(life[sel].mean()):.1f} us, clock {float(clk[sel].mean()):.3f} GHz, "
-                  f"barrier wait {float((wait[sel] / cyc[sel]).mean()) * 100:.1f} % of cycles")
+                  f"barrier wait {float((wait[sel] / cyc[sel]).mean()) * 100:.1f} %, load wait "
+                  f"{float((vwait[sel] / cyc[sel]).mean()) * 100:.1f} % of cycles")
     for x in sorted(set(int(t) for t in xcc)):
         sel = xcc == x
         print(f"  xcc {x}: waves {int(sel.sum())} life mean {float(life[sel].mean()):.1f} end max {float(end[sel].max()):.1f}")

@@ -1,4 +1,4 @@
-"""ISA guard for fused_v2.hip (CPU, needs hipcc): the kernels issue global loads the
+"""ISA guard for the fused_v2 kernels (CPU, needs hipcc): the kernels issue global loads the
 compiler does not track (inline asm, exact s_waitcnt vmcnt(N) by hand), so no
 instruction may touch a load's destination VGPRs before a wait retires it.  Compiles
 the device code to assembly and runs scripts/check_async_loads.py's dataflow check on
@@ -29,12 +29,21 @@ def test_untracked_loads_never_touched_in_flight(tmp_path, diag):
     experimental ones."""
     import check_async_loads as cal
 
-    asm = tmp_path / "fused_v2.s"
-    subprocess.check_call([_hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "--cuda-device-only", "-S"]
-                          + (["-DZS3_DIAG=1"] if diag else []) +
-                          ["-o", str(asm), os.path.join(ROOT, "zs3server_amd", "csrc", "fused_v2.hip"),
-                           "-I", os.path.join(ROOT, "include")], stderr=subprocess.DEVNULL)
-    text = asm.read_text().split("\n")
+    # every translation unit that instantiates fused_v2.hpp's kernels, compiled in parallel
+    units = ["fused_v2.hip", "fused_v2_get.hip"] + (
+        ["fused_v2_km84.hip", "fused_v2_km42.hip", "fused_v2_km164.hip"] if diag else [])
+    procs = []
+    for u in units:
+        asm = tmp_path / (u + ".s")
+        procs.append((asm, subprocess.Popen(
+            [_hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "--cuda-device-only", "-S"]
+            + (["-DZS3_DIAG=1"] if diag else []) +
+            ["-o", str(asm), os.path.join(ROOT, "zs3server_amd", "csrc", u), "-I", os.path.join(ROOT, "include")],
+            stderr=subprocess.DEVNULL)))
+    text = []
+    for asm, p in procs:
+        assert p.wait() == 0, asm
+        text += asm.read_text().split("\n")
     funcs, cur = [], None
     for i, line in enumerate(text, 1):
         if line.startswith("_Z") and line.rstrip().endswith(":") or (line.startswith("_Z") and ":" in line and "@" in line):

@@ -1,0 +1,1362 @@
+// fused_v2.hpp — kernel templates of the second-generation fused kernels (k_ehx, k_ehx_ws,
+// k_vr_ws) and their template launchers, shared by the translation units that
+// instantiate them: fused_v2.hip (encode defaults), fused_v2_get.hip (GET / heal) and,
+// in the diagnostics build only, fused_v2_km{84,42,164}.hip (encode variants).
+//
+// fused_v2.hip — second-generation fused Split + Encode + HighwayHash-256 kernel.
+//
+// Replaces the arithmetic of Erasure.EncodeData (cmd/erasure-coding.go:77-91) plus
+// the k+m streamingBitrotWriter sums (cmd/bitrot-streaming.go:43-65) for the
+// dyadic RS shapes (m in {2,4}, m | k: RS(8+4), RS(4+2), RS(16+4), ...).
+//
+// Same work decomposition as k_encode_hash (kernels.hip): G whole stripes per
+// workgroup, one HighwayHash lane per thread (a quad per shard row), one CW-byte
+// column per thread for the encode, tiles of T bytes per shard row staged in LDS.
+// What changes is the memory pipeline, measured on MI355X (scripts/sweep_variants.py):
+//  * vmcnt is one in-order counter for loads AND stores, so the old order
+//    (store parity(i), then load tile i+1) made the wait for tile i+1's data also
+//    wait for tile i's store acknowledgements.  Here the loads of tile i+PF are
+//    issued BEFORE the parity stores of tile i, so the wait at step i+1 leaves the
+//    stores in flight.
+//  * every LDS read of a tile's hash words is issued before the first HighwayHash
+//    update (one lgkmcnt wait per tile instead of one per two packets).
+//  * NBUF = 2 LDS tiles: one barrier per step.
+//  * full tiles run a branch-free body; the ragged tail tile (S % T) is peeled.
+#pragma once
+#include "kernels.hpp"
+#include "gf_dev.hpp"
+#include "hh256_dev.hpp"
+
+#include <type_traits>
+
+using namespace zs3dev;
+
+namespace zs3k {
+
+namespace {
+
+__device__ __forceinline__ void lds_barrier2() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+template <int NWd>
+__device__ __forceinline__ Col<NWd> ld_col(const uint8_t* p) {
+    Col<NWd> v;
+    __builtin_memcpy(&v, p, 4 * NWd);
+    return v;
+}
+template <int NWd>
+__device__ __forceinline__ void st_col(uint8_t* p, const Col<NWd>& v) {
+    __builtin_memcpy(p, &v, 4 * NWd);
+}
+template <int NWd>
+__device__ __forceinline__ void st_col_nt(uint8_t* p, const Col<NWd>& v) {
+    if constexpr (NWd == 4) {
+        typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+        u4 t = {v.w[0], v.w[1], v.w[2], v.w[3]};
+        __builtin_nontemporal_store(t, reinterpret_cast<u4*>(p));
+    } else if constexpr (NWd == 2) {
+        typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+        u2 t = {v.w[0], v.w[1]};
+        __builtin_nontemporal_store(t, reinterpret_cast<u2*>(p));
+    } else {
+        __builtin_nontemporal_store(v.w[0], reinterpret_cast<uint32_t*>(p));
+    }
+}
+
+// Raw 4/8/16-byte register types for the in-flight columns.
+template <int NWd> struct VecOf;
+template <> struct VecOf<1> { typedef uint32_t type; };
+template <> struct VecOf<2> { typedef uint32_t type __attribute__((ext_vector_type(2))); };
+template <> struct VecOf<4> { typedef uint32_t type __attribute__((ext_vector_type(4))); };
+
+// Global load whose completion the compiler does not track: LLVM's waitcnt pass waits
+// vmcnt(0) before the first use of a load that has stores issued after it, which
+// serialises the parity stores with the next tile's data (and defeats any deeper
+// prefetch).  The hardware retires vector-memory ops in issue order, so the kernel
+// waits for exactly the loads it needs with vm_wait<N>().  The destination is the
+// long-lived prefetch variable itself (no temporary), so its register stays
+// allocated until the wait; scripts/check_async_loads.py verifies in the ISA that no
+// instruction reads a load's destination before the next s_waitcnt vmcnt.
+template <int NWd>
+__device__ __forceinline__ void ld_async(typename VecOf<NWd>::type& dst, const uint8_t* p) {
+    if constexpr (NWd == 4)
+        asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(dst) : "v"(p) : "memory");
+    else if constexpr (NWd == 2)
+        asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(dst) : "v"(p) : "memory");
+    else
+        asm volatile("global_load_dword %0, %1, off" : "=v"(dst) : "v"(p) : "memory");
+}
+
+// s_waitcnt vmcnt(N), then an empty asm that "redefines" each column, so no use of a
+// column can be scheduled above the wait.
+// Non-temporal form (streamed data read once: nt cache policy).
+template <int NWd>
+__device__ __forceinline__ void ld_async_nt(typename VecOf<NWd>::type& dst, const uint8_t* p) {
+    if constexpr (NWd == 4)
+        asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(dst) : "v"(p) : "memory");
+    else if constexpr (NWd == 2)
+        asm volatile("global_load_dwordx2 %0, %1, off nt" : "=v"(dst) : "v"(p) : "memory");
+    else
+        asm volatile("global_load_dword %0, %1, off nt" : "=v"(dst) : "v"(p) : "memory");
+}
+
+template <int N, int K, typename V>
+__device__ __forceinline__ void vm_wait(V (&xs)[K]) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+#pragma unroll
+    for (int j = 0; j < K; ++j) asm volatile("" : "+v"(xs[j]));
+}
+
+// LDS hand-off counters (k_ehx_ws RING).  Signal: this wave's LDS accesses have
+// completed (lgkmcnt(0)), then one lane adds 1.  Wait: poll until the count reaches
+// `target`, sleeping between polls; the spin is bounded so that a protocol error can
+// only produce wrong output, never a wave that does not finish.
+__device__ __forceinline__ void ring_signal(uint32_t* ctr) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (__lane_id() == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void ring_wait(const uint32_t* ctr, uint32_t target) {
+    for (int spin = 0; spin < (1 << 22); ++spin) {
+        const uint32_t v = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (__builtin_amdgcn_readfirstlane(v) >= target) break;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    asm volatile("" ::: "memory");
+}
+
+template <int NWd>
+__device__ __forceinline__ Col<NWd> to_col(const typename VecOf<NWd>::type& v) {
+    Col<NWd> c;
+    if constexpr (NWd == 1) {
+        c.w[0] = v;
+    } else {
+#pragma unroll
+        for (int w = 0; w < NWd; ++w) c.w[w] = v[w];
+    }
+    return c;
+}
+
+}  // namespace
+
+// K data rows, M parity rows (dyadic), G stripes per workgroup, CW-byte columns,
+// PF tiles of register prefetch, NBUF LDS tiles, NTS = non-temporal parity stores.
+// ABL (timing-only diagnostics): 1 = no hash, 2 = no GF arithmetic (parity = data
+// rows 0..M-1), 3 = neither.
+// PIPE: software-pipelined body, one basic block per step holding encode(tile i)
+// AND hash(tile i-1), so the scheduler fills the HighwayHash chain's dependent
+// latency with independent GF work (requires NBUF = 2).
+// PRIO: rotate s_setprio by (tile + workgroup) so co-resident workgroups of a CU
+// progress at equal rates (oldest-first issue otherwise lets the first workgroup of a
+// CU finish far ahead and leaves the CU under-occupied for the rest of the launch).
+template <int K, int M, int G, int CW, int PF, int NBUF, bool NTS, int ABL = 0, bool PIPE = false, bool PRIO = false>
+__global__ void __launch_bounds__(4 * G * (K + M)) __attribute__((amdgpu_waves_per_eu(3))) k_ehx(EncArgs a) {
+    constexpr int R = K + M;
+    constexpr int NT = 4 * G * R;
+    constexpr int NWd = CW / 4;
+    constexpr int CPB = NT / G;        // columns per stripe = threads per stripe
+    constexpr int T = CPB * CW;        // tile bytes per shard row
+    constexpr int TS = T + 32;         // +8 banks per row: conflict-free b64 row reads
+    constexpr int NPK = T / 32;
+    constexpr int NTAB = K * 8;
+    static_assert(M == 2 || M == 4, "dyadic shapes only");
+    // tile buffers in dynamic LDS (one workgroup may take up to 160 KiB)
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem_dyn[];
+    uint8_t(*tile)[G * R * TS] = reinterpret_cast<uint8_t(*)[G * R * TS]>(smem_dyn);
+    __shared__ __attribute__((aligned(16))) uint32_t tabs[NTAB];
+    auto set_prio = [&](int64_t ti) {
+        if constexpr (PRIO) {
+            const int q = (int)((ti + blockIdx.x) & 3);
+            if (q == 0) __builtin_amdgcn_s_setprio(0);
+            else if (q == 1) __builtin_amdgcn_s_setprio(1);
+            else if (q == 2) __builtin_amdgcn_s_setprio(2);
+            else __builtin_amdgcn_s_setprio(3);
+        }
+    };
+
+    const int tid = threadIdx.x;
+    const int64_t blk0 = (int64_t)blockIdx.x * G;
+    const int64_t S = a.S;
+    for (int i = tid; i < NTAB; i += NT) tabs[i] = a.dtables[i];
+
+    // hash role: lane `lane` of shard row `chain` (stripe chain / R)
+    const int chain = tid >> 2, lane = tid & 3;
+    const bool chain_live = blk0 + chain / R < a.n_blocks;
+    const uint32_t sel = zipper_sel(lane);
+    HHLane st = hh_init(lane, a.key[0], a.key[1], a.key[2], a.key[3]);
+
+    // encode role: column o of stripe g (dead stripes of the last workgroup alias
+    // the last live block and store byte-identical parity)
+    const int g = tid / CPB, o = (tid % CPB) * CW;
+    const int64_t b = (blk0 + g) < a.n_blocks ? (blk0 + g) : (a.n_blocks - 1);
+    const uint8_t* src = a.data + b * a.data_stride + o;
+    uint8_t* pdst = a.parity + b * a.parity_stride + o;
+    const int col_off = g * R * TS + o;
+    const int row_off = chain * TS + 8 * lane;
+
+    const int64_t nfull = S / T;
+    const int tail = (int)(S - nfull * T);
+
+    // Diagnostics (a.dbg set): per-wave start/end real time, shader clocks, HW_ID and
+    // XCC_ID, to see load balance across CUs/XCDs and the in-kernel clock.
+    uint64_t rt0 = 0, ct0 = 0;
+    if (a.dbg) {
+        rt0 = __builtin_amdgcn_s_memrealtime();
+        ct0 = __builtin_amdgcn_s_memtime();
+    }
+
+    typedef typename VecOf<NWd>::type VT;
+    VT x[PF][K];
+    auto load = [&](VT (&xs)[K], int64_t t0) {
+#pragma unroll
+        for (int j = 0; j < K; ++j) ld_async<NWd>(xs[j], src + (int64_t)j * S + t0);
+    };
+    auto load_tail = [&](VT (&xs)[K], int64_t t0) {
+        if (o < tail) {
+#pragma unroll
+            for (int j = 0; j < K; ++j) ld_async<NWd>(xs[j], src + (int64_t)j * S + t0);
+        } else {
+#pragma unroll
+            for (int j = 0; j < K; ++j) xs[j] = VT{};
+        }
+    };
+    // encode tile into LDS buffer `tl`, then issue the loads of tile `t_next`
+    // into the same registers, then store parity of tile t0.
+    auto encode = [&](VT (&xr)[K], uint8_t* tl, Col<NWd> (&par)[M]) {
+        Col<NWd> xs[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) xs[j] = to_col<NWd>(xr[j]);
+        if constexpr (ABL & 2) {
+#pragma unroll
+            for (int r = 0; r < M; ++r)
+#pragma unroll
+                for (int w = 0; w < NWd; ++w) par[r].w[w] = xs[r].w[w] ^ xs[r + M].w[w];
+        } else {
+            encode_dyadic<NWd, K, M, !PIPE>(xs, par, tabs);
+        }
+#pragma unroll
+        for (int j = 0; j < K; ++j) st_col<NWd>(tl + col_off + j * TS, xs[j]);
+#pragma unroll
+        for (int r = 0; r < M; ++r) st_col<NWd>(tl + col_off + (K + r) * TS, par[r]);
+    };
+    auto store_par = [&](const Col<NWd> (&par)[M], int64_t t0) {
+#pragma unroll
+        for (int r = 0; r < M; ++r) {
+            if (NTS)
+                st_col_nt<NWd>(pdst + (int64_t)r * S + t0, par[r]);
+            else
+                st_col<NWd>(pdst + (int64_t)r * S + t0, par[r]);
+        }
+    };
+    auto hash_full = [&](const uint8_t* tl) {
+        const uint64_t* p = reinterpret_cast<const uint64_t*>(tl + row_off);
+        uint64_t w[NPK];
+#pragma unroll
+        for (int i = 0; i < NPK; ++i) w[i] = p[4 * i];
+#pragma unroll
+        for (int i = 0; i < NPK; ++i) {
+            if constexpr (ABL & 1)
+                st.v0 ^= w[i];
+            else
+                hh_update(st, w[i], sel);
+        }
+    };
+    // Branch-free prefetch for the edge steps: a tile past the end (or a tail column
+    // past the tail) re-reads tile 0 of its own row, so x is defined on every path (no
+    // phi copies of in-flight registers) and the value is unused.
+    auto prefetch_any = [&](VT (&xs)[K], int64_t tn) {
+        const bool ok = tn < nfull || (tn == nfull && o < tail);
+        load(xs, ok ? tn * T : 0);
+    };
+    // Steady-state step on full tile ti held in xs (tile ti+PF known full): encode
+    // into LDS, issue the loads of tile ti+PF into the freed registers, then the
+    // parity stores, barrier, hash.
+    // Before encode(ti) the wave's pending vector-memory ops are, oldest first:
+    // loads(ti), stores(ti-PF), loads(ti+1), stores(ti-PF+1), ..., loads(ti+PF-1),
+    // stores(ti-1).  Steady state waits for loads(ti) only: vmcnt(M + (PF-1)*(K+M)).
+    // Edge steps (below) wait for everything.
+    auto step = [&](VT (&xs)[K], int64_t ti) {
+        set_prio(ti);
+        uint8_t* tl = tile[NBUF == 1 ? 0 : (ti & 1)];
+        Col<NWd> par[M];
+        vm_wait<M + (PF - 1) * (K + M)>(xs);
+        encode(xs, tl, par);
+        load(xs, (ti + PF) * T);
+        store_par(par, ti * T);
+        lds_barrier2();
+        hash_full(tl);
+        if (NBUF == 1) lds_barrier2();
+    };
+
+    if constexpr (PIPE) {
+        static_assert(NBUF == 2, "pipelined body double-buffers the LDS tile");
+        // Step ti: hash tile ti-1 (buffer (ti-1)&1, written before the last barrier)
+        // and encode tile ti into buffer ti&1 (last read by hash(ti-2), which every
+        // wave finished before the last barrier); one barrier per step.
+        auto hash_words = [&](const uint8_t* tl, uint64_t (&w)[NPK]) {
+            const uint64_t* p = reinterpret_cast<const uint64_t*>(tl + row_off);
+#pragma unroll
+            for (int i2 = 0; i2 < NPK; ++i2) w[i2] = p[4 * i2];
+        };
+        auto hash_apply = [&](const uint64_t (&w)[NPK]) {
+#pragma unroll
+            for (int i2 = 0; i2 < NPK; ++i2) {
+                if constexpr (ABL & 1)
+                    st.v0 ^= w[i2];
+                else
+                    hh_update(st, w[i2], sel);
+            }
+        };
+        // steady state: full tile ti (>= 1) encoded, tile ti+PF known full
+        auto steady = [&](VT (&xs)[K], int64_t ti) {
+            set_prio(ti);
+            uint64_t w[NPK];
+            hash_words(tile[(ti - 1) & 1], w);
+            vm_wait<M + (PF - 1) * (K + M)>(xs);
+            Col<NWd> par[M];
+            encode(xs, tile[ti & 1], par);
+            load(xs, (ti + PF) * T);
+            store_par(par, ti * T);
+            hash_apply(w);
+            lds_barrier2();
+        };
+        // any step ti >= 0: hash tile ti-1 if it is a full tile, encode tile ti if it
+        // exists (full or tail); always prefetch tile ti+PF and hit the barrier.
+        auto edge = [&](VT (&xs)[K], int64_t ti) {
+            uint64_t w[NPK];
+            const bool do_hash = ti >= 1 && ti <= nfull;
+            if (do_hash) hash_words(tile[(ti - 1) & 1], w);
+            vm_wait<0>(xs);
+            if (ti < nfull || (ti == nfull && tail)) {
+                Col<NWd> par[M];
+                encode(xs, tile[ti & 1], par);
+                if (ti < nfull || o < tail) store_par(par, ti * T);
+            }
+            prefetch_any(xs, ti + PF);
+            if (do_hash) hash_apply(w);
+            lds_barrier2();
+        };
+        lds_barrier2();  // tables visible
+#pragma unroll
+        for (int p = 0; p < PF; ++p) prefetch_any(x[p], p);
+#pragma unroll
+        for (int p = 0; p < PF; ++p) edge(x[p], p);
+        int64_t i = PF;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        for (; i + 2 * PF <= nfull; i += PF) {
+#pragma unroll
+            for (int p = 0; p < PF; ++p) steady(x[p], i + p);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int p = 0; p < 2 * PF; ++p) edge(x[p % PF], i + p);
+        if (tail) {
+            const uint8_t* row = tile[nfull & 1] + chain * TS;
+            hh_packets(st, row, tail >> 5, lane, sel);
+            if (tail & 31) hh_remainder(st, row + (tail & ~31), (uint32_t)(tail & 31), lane, sel);
+        }
+    } else {
+        // Any step ti >= 0 outside the steady state: encode tile ti if it exists (full
+        // or tail), always prefetch tile ti+PF (branch-free), barrier, hash what was
+        // encoded.  Every wave runs every edge step, so barriers stay matched.
+        auto edge = [&](VT (&xs)[K], int64_t ti) {
+            uint8_t* tl = tile[NBUF == 1 ? 0 : (ti & 1)];
+            const bool full = ti < nfull, part = ti == nfull && tail;
+            vm_wait<0>(xs);
+            Col<NWd> par[M];
+            if (full || part) encode(xs, tl, par);
+            prefetch_any(xs, ti + PF);
+            if (full || (part && o < tail)) store_par(par, ti * T);
+            lds_barrier2();
+            if (full) {
+                hash_full(tl);
+            } else if (part) {
+                const uint8_t* row = tl + chain * TS;
+                hh_packets(st, row, tail >> 5, lane, sel);
+                if (tail & 31) hh_remainder(st, row + (tail & ~31), (uint32_t)(tail & 31), lane, sel);
+            }
+            if (NBUF == 1) lds_barrier2();
+        };
+        lds_barrier2();  // tables visible
+    #pragma unroll
+        for (int p = 0; p < PF; ++p) prefetch_any(x[p], p);
+    #pragma unroll
+        for (int p = 0; p < PF; ++p) edge(x[p], p);
+        int64_t i = PF;
+        // Drain once before the steady state and once after it: the in-loop vmcnt counts
+        // then only have to hold for the loop's own issue order (and
+        // scripts/check_async_loads.py can prove it without path-sensitive reasoning).
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        for (; i + 2 * PF <= nfull; i += PF) {
+    #pragma unroll
+            for (int p = 0; p < PF; ++p) step(x[p], i + p);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    #pragma unroll
+        for (int p = 0; p < 2 * PF; ++p) edge(x[p % PF], i + p);
+
+    }
+
+    // Keep every prefetch register allocated until all loads have retired: a load
+    // whose value turns out unused must not have its destination handed to other code
+    // while it is still in flight.
+#pragma unroll
+    for (int p = 0; p < PF; ++p) vm_wait<0>(x[p]);
+
+    const uint64_t h = hh_finalize256(st, lane, sel);
+    if (chain_live) {
+        const int64_t bb = blk0 + chain / R;
+        const int s = chain % R;
+        *reinterpret_cast<uint64_t*>(a.sums + (bb * R + s) * 32 + 8 * lane) = h;
+    }
+    if (a.dbg && (tid & 63) == 0) {
+        const uint64_t rt1 = __builtin_amdgcn_s_memrealtime();
+        const uint64_t ct1 = __builtin_amdgcn_s_memtime();
+        uint64_t* d = a.dbg + ((int64_t)blockIdx.x * (NT / 64) + (tid >> 6)) * 5;
+        d[0] = rt0;
+        d[1] = rt1;
+        d[2] = ct1 - ct0;
+        d[3] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+        d[4] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+    }
+}
+
+// Warp-specialised form (one workgroup per CU, G stripes): the first NH = 2*G*R threads
+// only hash, one HighwayHash chain per thread PAIR (hh256_dev.hpp pair form: no DPP and
+// a shared zipper v_perm, 16 instead of 19 VALU per lane-packet); the other NE threads
+// only encode, one 16-byte column each (dwordx4 loads/stores, half the memory
+// instructions per byte of the 8-byte form).  Step s: encode waves encode tile s into
+// LDS buffer s&1 and store its parity; hash waves hash tile s-1 from buffer (s-1)&1;
+// one barrier.  Both roles run the same number of steps, so barriers stay matched.
+// With 6 + 6 waves on 4 SIMDs the busiest SIMD carries one hash and two encode waves:
+// ~6 % less issue than three mixed waves (asm_loops.py + scripts/ubench/opcost.hip).
+// BUF: the encode role addresses rows through buffer resources (workgroup base in
+// SGPRs, row/tile offset in an SGPR soffset, one constant per-lane voffset) instead
+// of 64-bit per-lane pointers: no VALU address arithmetic per load/store.
+// HQ: the hash waves use the quad form (one HH lane per thread, as k_ehx; 19 VALU per
+// lane-packet but the shortest dependent chain per packet) — for small batches, where a
+// hash wave has its SIMD to itself and the chain latency, not issue, bounds the launch
+// (RS(4+2) config 2: 6 144 chains); the hash thread count is padded to whole waves, the
+// pad quads hash a real row and discard the digest.
+template <int K, int M, int G, int T, bool HQ>
+constexpr int ws_nh() {
+    return HQ ? ((4 * G * (K + M) + 63) / 64) * 64 : 2 * G * (K + M);
+}
+// Encode column width: 16 bytes, 8 for K > 8 (16 rows of 16-byte columns do not fit
+// the 168-VGPR budget beside the encode's working set).
+template <int K, int CWX = 0>
+constexpr int ws_cwe() {
+    return CWX ? CWX : (K > 8 ? 8 : 16);
+}
+
+// WT (diagnostic): per-wave shader cycles spent waiting at barriers, into the dbg stamps.
+// PM (issue-priority experiments): 1 = encode waves s_setprio 1 over hash waves; 2 = as 1
+// plus the younger encode wave of each SIMD-sharing pair (waves w, w+4) at 2; 3 = hash
+// waves at 1.
+// CWX: encode column width override (0 = ws_cwe's default).
+// RING: the two roles hand tiles over through per-slot LDS counters instead of one
+// workgroup barrier per step (pair-form hash role only).  An encode wave waits only
+// until every hash wave has read the slot it is about to overwrite (tile s-2), a hash
+// wave only until every encode wave has written tile s; a hash wave releases the slot
+// as soon as its 12 reads have landed, before hashing them.  So the older encode wave
+// of a SIMD goes straight on to the next tile instead of idling at a barrier while its
+// younger partner finishes alone.
+// NTM (memory policy, bit mask): 1 = data loads non-temporal, 2 = parity stores non-temporal.
+// STB: encode role reads the coefficient tables with scalar loads (SGPRs) instead of LDS.
+// EP = 1 (early prefetch): the encode wave first copies its data columns into the LDS
+// tile, issues the next tile's loads into the freed registers, and then encodes from the
+// LDS copy (one block of M rows at a time): the loads get a whole step to land instead of
+// the parity stores + barrier.  EP = 2 (early data write): the data columns go to LDS
+// before the encode instead of after it, so the LDS drains the tile's data rows while
+// the VALU encodes and only the parity rows are written between encode and barrier.
+// PFD (L2 prefetch distance, pair-form hash role): while hashing tile s-1 the hash waves
+// touch every 128-byte line of the data rows of tile s+PFD with one untracked
+// global_load_dword each (result discarded), so the HBM fetch of a tile starts PFD-1
+// steps before the encode waves load it and their own loads hit L2: the HBM stream
+// keeps ~PFD tiles of reads in flight per CU instead of the one tile the encode waves'
+// registers hold.  The hash waves never wait on these loads (they have no other vector
+// loads in the loop); the sink register stays allocated until the final vmcnt(0).
+// UA (unaligned shard size): S need not be a multiple of 16 (RS(12+4) on 1 MiB blocks:
+// S = 87 382, every row 2-byte aligned; k*S - n = 8 bytes of Split padding).  Full tiles
+// use the same vector loads and stores at the rows' byte offsets (the GPU runs global
+// memory in unaligned mode); the ragged tail tile is never prefetched: each lane reads
+// its columns of it byte by byte, with the Split padding of the last data row (n..k*S)
+// and everything past the row read as zero, and stores only the parity bytes below S.
+template <int K, int M, int G, int T, int PF, bool BUF = false, bool HQ = false, bool WT = false, int PM = 0,
+          int CWX = 0, bool RING = false, int NTM = 0, bool STB = false, int EP = 0, int PFD = 0, bool UA = false>
+__global__ void __launch_bounds__((ws_nh<K, M, G, T, HQ>() + G * (T / ws_cwe<K, CWX>()))) __attribute__((amdgpu_waves_per_eu(3)))
+k_ehx_ws(EncArgs a) {
+    constexpr int R = K + M;
+    constexpr int NH = ws_nh<K, M, G, T, HQ>();  // hash threads
+    constexpr int CWE = ws_cwe<K, CWX>();
+    constexpr int CPS = T / CWE;    // encode columns per stripe row
+    constexpr int NE = G * CPS;     // encode threads
+    constexpr int NT = NH + NE;
+    constexpr int TS = HQ ? T + 32 : T + 16;  // conflict-free b64 (quad) / b128 (pair) row reads
+    constexpr int NPK = T / 32;
+    constexpr int NTAB = K * 8;
+    static_assert(M == 2 || M == 4, "dyadic shapes only");
+    static_assert(NH % 64 == 0 && NE % 64 == 0 && T % 32 == 0, "whole wavefronts per role");
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem_dyn[];
+    uint8_t(*tile)[G * R * TS] = reinterpret_cast<uint8_t(*)[G * R * TS]>(smem_dyn);
+    __shared__ __attribute__((aligned(16))) uint32_t tabs[NTAB];
+    // RING: [0..1] encode-wave completions per slot, [2..3] hash-wave releases per slot
+    __shared__ uint32_t ring[4];
+    static_assert(!RING || !HQ, "ring hand-off: pair-form hash role");
+    constexpr uint32_t NEW = (uint32_t)(NT - NH) / 64, NHW = (uint32_t)NH / 64;
+
+    const int tid = threadIdx.x;
+    const int64_t blk0 = (int64_t)blockIdx.x * G;
+    const int64_t S = a.S;
+    for (int i = tid; i < NTAB; i += NT) tabs[i] = a.dtables[i];
+    if (RING && tid < 4) ring[tid] = 0;
+    const int64_t nfull = S / T;
+    const int tail = (int)(S - nfull * T);  // multiple of 16 unless UA
+    // Step schedule shared by both roles: PF edge steps, the steady loop in units of PF
+    // while i + 2*PF <= nfull, 2*PF edge steps, one step that only hashes.
+    int64_t iend = PF;
+    if (nfull >= 3 * PF) iend = PF + ((nfull - 3 * PF) / PF + 1) * PF;
+    const int64_t total = iend + 2 * PF + 1;
+
+    // Diagnostics (a.dbg set): per-wave real time, shader clocks, HW_ID, XCC_ID, as in
+    // k_ehx (waves 0..NH/64-1 of a workgroup hash, the rest encode).
+    uint64_t rt0 = 0, ct0 = 0;
+    if (a.dbg) {
+        rt0 = __builtin_amdgcn_s_memrealtime();
+        ct0 = __builtin_amdgcn_s_memtime();
+    }
+    uint64_t wsum = 0, vwsum = 0;  // WT: shader cycles in barriers / in the encode's load wait
+    auto bar = [&]() {
+        if constexpr (WT) {
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            lds_barrier2();
+            wsum += __builtin_amdgcn_s_memtime() - t;
+        } else {
+            lds_barrier2();
+        }
+    };
+    auto stamp = [&]() {
+        if (a.dbg && (tid & 63) == 0) {
+            const uint64_t rt1 = __builtin_amdgcn_s_memrealtime();
+            const uint64_t ct1 = __builtin_amdgcn_s_memtime();
+            uint64_t* d = a.dbg + ((int64_t)blockIdx.x * (NT / 64) + (tid >> 6)) * 5;
+            d[0] = rt0;
+            d[1] = rt1;
+            d[2] = ct1 - ct0;
+            d[3] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+            // XCC_ID | barrier-wait cycles (bits 8-35) | load-wait cycles (bits 36-63)
+            d[4] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) | ((wsum & 0xFFFFFFF) << 8) | (vwsum << 36);
+        }
+    };
+
+    if (HQ && __builtin_amdgcn_readfirstlane(tid) < NH) {
+        // ---- hash role, quad form: lane `lane` of chain `chain`
+        const int chain = tid >> 2, lane = tid & 3;
+        const bool live = chain < G * R && blk0 + chain / R < a.n_blocks;
+        const int crow = chain < G * R ? chain : chain - G * R;
+        const int row_off = crow * TS + 8 * lane;
+        const uint32_t sel = zipper_sel(lane);
+        HHLane st = hh_init(lane, a.key[0], a.key[1], a.key[2], a.key[3]);
+        bar();  // tables (matches the encode role)
+        bar();  // step 0: tile 0 being encoded
+        for (int64_t s = 1; s <= nfull; ++s) {
+            const uint64_t* p = reinterpret_cast<const uint64_t*>(tile[(s - 1) & 1] + row_off);
+            uint64_t w[NPK];
+#pragma unroll
+            for (int i = 0; i < NPK; ++i) w[i] = p[4 * i];
+#pragma unroll
+            for (int i = 0; i < NPK; ++i) hh_update(st, w[i], sel);
+            bar();
+        }
+        if (tail) {
+            const uint8_t* row = tile[nfull & 1] + crow * TS;
+            hh_packets(st, row, tail >> 5, lane, sel);
+            if (tail & 31) hh_remainder(st, row + (tail & ~31), (uint32_t)(tail & 31), lane, sel);
+        }
+        for (int64_t s = nfull + 1; s < total; ++s) bar();
+        const uint64_t h = hh_finalize256(st, lane, sel);
+        if (live) {
+            const int64_t bb = blk0 + chain / R;
+            *reinterpret_cast<uint64_t*>(a.sums + (bb * R + chain % R) * 32 + 8 * lane) = h;
+        }
+        stamp();
+        return;
+    }
+    if constexpr (PM == 3) {
+        if (__builtin_amdgcn_readfirstlane(tid) < NH) __builtin_amdgcn_s_setprio(1);
+    } else if constexpr (PM == 1 || PM == 2) {
+        if (__builtin_amdgcn_readfirstlane(tid) >= NH) {
+            if (PM == 2 && __builtin_amdgcn_readfirstlane(tid) >= NH + 256)
+                __builtin_amdgcn_s_setprio(2);
+            else
+                __builtin_amdgcn_s_setprio(1);
+        }
+    }
+    if (!HQ && __builtin_amdgcn_readfirstlane(tid) < NH) {
+        // ---- hash role: lanes (2hh, 2hh+1) of chain `chain` = shard row s of stripe g
+        const int chain = tid >> 1, hh = tid & 1;
+        const int row_off = chain * TS;
+        HHPair st = hh2_init(hh, a.key[0], a.key[1], a.key[2], a.key[3]);
+        bar();  // tables (matches the encode role)
+        if constexpr (RING) {
+            for (int64_t s = 0; s <= nfull; ++s) {
+                if (s == nfull && !tail) break;
+                ring_wait(&ring[s & 1], NEW * (uint32_t)((s >> 1) + 1));  // tile s written
+                if (s == nfull) {
+                    const uint8_t* row = tile[nfull & 1] + row_off;
+                    hh2_packets(st, row, tail >> 5, hh);
+                    if (tail & 31) hh2_remainder(st, row + (tail & ~31), (uint32_t)(tail & 31), hh);
+                    break;
+                }
+                const uint4* p = reinterpret_cast<const uint4*>(tile[s & 1] + row_off) + hh;
+                uint4 w[NPK];
+#pragma unroll
+                for (int i = 0; i < NPK; ++i) w[i] = p[2 * i];
+                ring_signal(&ring[2 + (s & 1)]);  // reads landed: the slot may be refilled
+#pragma unroll
+                for (int i = 0; i < NPK; ++i)
+                    hh2_update(st, ((uint64_t)w[i].y << 32) | w[i].x, ((uint64_t)w[i].w << 32) | w[i].z);
+            }
+            uint64_t d0, d1;
+            hh2_finalize256(st, d0, d1);
+            if (blk0 + chain / R < a.n_blocks) {
+                const int64_t bb = blk0 + chain / R;
+                uint64_t* out = reinterpret_cast<uint64_t*>(a.sums + (bb * R + chain % R) * 32 + 16 * hh);
+                out[0] = d0;
+                out[1] = d1;
+            }
+            stamp();
+            return;
+        }
+        // PFD: this thread's prefetch lines (line li = tid + q*NH of the tile's data rows)
+        constexpr int LPR = T / 128, NLN = G * K * LPR, NPL = PFD ? (NLN + NH - 1) / NH : 1;
+        const uint8_t* pfa[NPL];
+        uint32_t sink = 0;
+        if constexpr (PFD > 0) {
+            static_assert(T % 128 == 0, "prefetch whole 128-byte lines");
+#pragma unroll
+            for (int q = 0; q < NPL; ++q) {
+                const int li = tid + q * NH < NLN ? tid + q * NH : NLN - 1;
+                const int r = li / LPR, g = r / K, j = r % K;
+                const int64_t b = (blk0 + g) < a.n_blocks ? (blk0 + g) : (a.n_blocks - 1);
+                pfa[q] = a.data + b * a.data_stride + (int64_t)j * S + (li % LPR) * 128;
+            }
+        }
+        bar();  // step 0: tile 0 being encoded
+        for (int64_t s = 1; s <= nfull; ++s) {
+            if constexpr (PFD > 0) {
+                if (s + PFD < nfull) {
+#pragma unroll
+                    for (int q = 0; q < NPL; ++q)
+                        asm volatile("global_load_dword %0, %1, off" : "+v"(sink) : "v"(pfa[q] + (s + PFD) * T));
+                }
+            }
+            const uint4* p = reinterpret_cast<const uint4*>(tile[(s - 1) & 1] + row_off) + hh;
+            uint4 w[NPK];
+#pragma unroll
+            for (int i = 0; i < NPK; ++i) w[i] = p[2 * i];
+            if constexpr (PM == 4) __builtin_amdgcn_s_setprio(3);
+#pragma unroll
+            for (int i = 0; i < NPK; ++i) {
+                if constexpr (PM == 4) {
+                    // progress-equalising priority: 3, 2, 1, 0 over the quarters of the tile
+                    if (i > 0 && (4 * i) % NPK == 0) {
+                        __builtin_amdgcn_sched_barrier(0);
+                        if (4 * i / NPK == 1) __builtin_amdgcn_s_setprio(2);
+                        if (4 * i / NPK == 2) __builtin_amdgcn_s_setprio(1);
+                        if (4 * i / NPK == 3) __builtin_amdgcn_s_setprio(0);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                }
+                hh2_update(st, ((uint64_t)w[i].y << 32) | w[i].x, ((uint64_t)w[i].w << 32) | w[i].z);
+            }
+            bar();
+        }
+        if (tail) {
+            const uint8_t* row = tile[nfull & 1] + row_off;
+            hh2_packets(st, row, tail >> 5, hh);
+            if (tail & 31) hh2_remainder(st, row + (tail & ~31), (uint32_t)(tail & 31), hh);
+        }
+        for (int64_t s = nfull + 1; s < total; ++s) bar();
+        if constexpr (PFD > 0) asm volatile("s_waitcnt vmcnt(0)" : "+v"(sink)::"memory");
+        uint64_t d0, d1;
+        hh2_finalize256(st, d0, d1);
+        if (blk0 + chain / R < a.n_blocks) {
+            const int64_t bb = blk0 + chain / R;
+            uint64_t* out = reinterpret_cast<uint64_t*>(a.sums + (bb * R + chain % R) * 32 + 16 * hh);
+            out[0] = d0;
+            out[1] = d1;
+        }
+        stamp();
+        return;
+    }
+
+    // ---- encode role: 16-byte column o of stripe g (dead stripes of the last
+    // workgroup alias the last live block and store byte-identical parity)
+    constexpr int NWd = CWE / 4;
+    typedef typename VecOf<NWd>::type VT;
+    const int e = tid - NH;
+    const int g = e / CPS, o = (e % CPS) * CWE;
+    const int64_t b = (blk0 + g) < a.n_blocks ? (blk0 + g) : (a.n_blocks - 1);
+    const uint8_t* src = a.data + b * a.data_stride + o;
+    uint8_t* pdst = a.parity + b * a.parity_stride + o;
+    const int col_off = g * R * TS + o;
+    // buffer form (launch checks that every offset fits in 31 bits)
+    const __amdgpu_buffer_rsrc_t rs_d =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(a.data + blk0 * a.data_stride), 0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs_p =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(a.parity + blk0 * a.parity_stride), 0, 0x7FFFFFFF, 0x00020000);
+    const uint32_t vo_d = (uint32_t)((b - blk0) * a.data_stride + o);
+    const uint32_t vo_p = (uint32_t)((b - blk0) * a.parity_stride + o);
+
+    VT x[PF][K];
+    CoefTab ptab[EP == 3 ? K : 1];  // EP = 3: coefficient tables held in registers
+    // rows j of tile offset t0u (wave-uniform) at per-lane byte offset vo within the row
+    auto load_buf = [&](VT (&xs)[K], uint32_t vo, int64_t t0u) {
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)(j * S + t0u));
+            if constexpr (NWd == 4 && (NTM & 1))
+                asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen nt"
+                             : "=v"(xs[j])
+                             : "v"(vo), "s"(rs_d), "s"(so)
+                             : "memory");
+            else if constexpr (NWd == 4)
+                asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen"
+                             : "=v"(xs[j])
+                             : "v"(vo), "s"(rs_d), "s"(so)
+                             : "memory");
+            else if constexpr (NTM & 1)
+                asm volatile("buffer_load_dwordx2 %0, %1, %2, %3 offen nt"
+                             : "=v"(xs[j])
+                             : "v"(vo), "s"(rs_d), "s"(so)
+                             : "memory");
+            else
+                asm volatile("buffer_load_dwordx2 %0, %1, %2, %3 offen"
+                             : "=v"(xs[j])
+                             : "v"(vo), "s"(rs_d), "s"(so)
+                             : "memory");
+        }
+    };
+    auto load = [&](VT (&xs)[K], int64_t t0) {
+        if constexpr (BUF) {
+            load_buf(xs, vo_d, t0);
+        } else if constexpr ((NTM & 1) != 0) {
+#pragma unroll
+            for (int j = 0; j < K; ++j) ld_async_nt<NWd>(xs[j], src + (int64_t)j * S + t0);
+        } else {
+#pragma unroll
+            for (int j = 0; j < K; ++j) ld_async<NWd>(xs[j], src + (int64_t)j * S + t0);
+        }
+    };
+    auto prefetch_any = [&](VT (&xs)[K], int64_t tn) {
+        // UA: the tail tile is read byte by byte in its step (tail_cols), never prefetched
+        const bool ok = tn < nfull || (!UA && tn == nfull && o < tail);
+        if constexpr (BUF)
+            load_buf(xs, vo_d + (ok ? (uint32_t)(tn * T) : 0u), 0);  // per-lane part in voffset
+        else
+            load(xs, ok ? tn * T : 0);
+    };
+    // UA tail tile: bytes [o, o + CWE) of every data row, zero past the row's valid length
+    // (tail, or for the last data row the end of the block: Split padding reads as zero)
+    auto tail_cols = [&](VT (&xs)[K]) {
+        const uint8_t* t0p = src + nfull * T;
+        const int64_t last_valid = a.n - (int64_t)(K - 1) * S - nfull * T;
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            const int64_t valid = j == K - 1 ? (last_valid < tail ? last_valid : tail) : tail;
+            uint32_t w[NWd];
+#pragma unroll
+            for (int q = 0; q < NWd; ++q) {
+                uint32_t v = 0;
+#pragma unroll
+                for (int bb = 0; bb < 4; ++bb) {
+                    const int pos = o + 4 * q + bb;
+                    if (pos < valid) v |= (uint32_t)t0p[(int64_t)j * S + 4 * q + bb] << (8 * bb);
+                }
+                w[q] = v;
+            }
+            if constexpr (NWd == 1) {
+                xs[j] = w[0];
+            } else {
+#pragma unroll
+                for (int q = 0; q < NWd; ++q) xs[j][q] = w[q];
+            }
+        }
+    };
+    auto store_tail = [&](const Col<NWd> (&par)[M]) {
+        uint8_t* t0p = pdst + nfull * T;
+#pragma unroll
+        for (int r = 0; r < M; ++r)
+#pragma unroll
+            for (int q = 0; q < NWd; ++q)
+#pragma unroll
+                for (int bb = 0; bb < 4; ++bb)
+                    if (o + 4 * q + bb < tail) t0p[(int64_t)r * S + 4 * q + bb] = (uint8_t)(par[r].w[q] >> (8 * bb));
+    };
+    auto encode = [&](VT (&xr)[K], uint8_t* tl, Col<NWd> (&par)[M]) {
+        Col<NWd> xs[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) xs[j] = to_col<NWd>(xr[j]);
+        if constexpr (EP == 9) {
+            // timing ablation (diagnostics only; output differs): no GF arithmetic
+#pragma unroll
+            for (int r = 0; r < M; ++r)
+#pragma unroll
+                for (int w = 0; w < NWd; ++w) par[r].w[w] = xs[r].w[w] ^ xs[r + M].w[w];
+        } else if constexpr (EP == 8) {
+            // timing ablation: only the first half of the data rows enter the parity
+            Col<NWd> xh[K];
+#pragma unroll
+            for (int j = 0; j < K; ++j) xh[j] = xs[j % (K / 2)];
+            encode_dyadic<NWd, K / 2, M, true, false, STB>(*reinterpret_cast<const Col<NWd>(*)[K / 2]>(xh), par, tabs,
+                                                            const_tables(a.dtables));
+        } else if constexpr (EP == 3) {
+            // tables held in registers: the data rows go to LDS first and drain under the encode
+#pragma unroll
+            for (int j = 0; j < K; ++j) st_col<NWd>(tl + col_off + j * TS, xs[j]);
+            encode_dyadic_f<NWd, K, M, true, false, false, true>(
+                [&](int j) { return xs[j]; }, par, tabs, nullptr, NoHook{}, ptab);
+        } else if constexpr (EP == 2) {
+            // data rows written right after the first block's table reads
+            encode_dyadic_f<NWd, K, M, true, false, STB>(
+                [&](int j) { return xs[j]; }, par, tabs, const_tables(a.dtables), [&]() {
+#pragma unroll
+                    for (int j = 0; j < K; ++j) st_col<NWd>(tl + col_off + j * TS, xs[j]);
+                });
+        } else if constexpr (PM == 4) {
+            __builtin_amdgcn_s_setprio(3);
+            encode_dyadic<NWd, K, M, true, true>(xs, par, tabs);
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_setprio(K / M >= 3 ? 0 : 1);
+        } else {
+            encode_dyadic<NWd, K, M, true, false, STB>(xs, par, tabs, const_tables(a.dtables));
+        }
+        if constexpr (EP != 2 && EP != 3) {
+#pragma unroll
+            for (int j = 0; j < K; ++j) st_col<NWd>(tl + col_off + j * TS, xs[j]);
+        }
+#pragma unroll
+        for (int r = 0; r < M; ++r) st_col<NWd>(tl + col_off + (K + r) * TS, par[r]);
+    };
+    auto store_par = [&](const Col<NWd> (&par)[M], int64_t t0) {
+#pragma unroll
+        for (int r = 0; r < M; ++r) {
+            if constexpr (BUF) {
+                const int so = (int)__builtin_amdgcn_readfirstlane((uint32_t)(r * S + t0));
+                constexpr int aux = (NTM & 2) ? 2 : 0;  // cache policy: 2 = nt (gfx940 family)
+                if constexpr (NWd == 4) {
+                    const VT v = {par[r].w[0], par[r].w[1], par[r].w[2], par[r].w[3]};
+                    __builtin_amdgcn_raw_buffer_store_b128(v, rs_p, (int)vo_p, so, aux);
+                } else {
+                    const VT v = {par[r].w[0], par[r].w[1]};
+                    __builtin_amdgcn_raw_buffer_store_b64(v, rs_p, (int)vo_p, so, aux);
+                }
+            } else if constexpr ((NTM & 2) != 0) {
+                st_col_nt<NWd>(pdst + (int64_t)r * S + t0, par[r]);
+            } else {
+                st_col<NWd>(pdst + (int64_t)r * S + t0, par[r]);
+            }
+        }
+    };
+    // RING: slot of tile ti free = every hash wave has read tile ti-2 out of it
+    auto slot_free = [&](int64_t ti) {
+        if (RING && ti >= 2) ring_wait(&ring[2 + (ti & 1)], NHW * (uint32_t)(ti >> 1));
+    };
+    // steady step (see k_ehx): wait for loads(ti) only
+    auto step = [&](VT (&xs)[K], int64_t ti) {
+        Col<NWd> par[M];
+        slot_free(ti);
+        if constexpr (WT) {
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            vm_wait<M + (PF - 1) * (K + M)>(xs);
+            vwsum += __builtin_amdgcn_s_memtime() - t;
+        } else {
+            vm_wait<M + (PF - 1) * (K + M)>(xs);
+        }
+        if constexpr (EP == 1) {
+            static_assert(PF == 1 && !RING && PM != 4, "early prefetch: PF = 1, barrier hand-off");
+            uint8_t* tl = tile[ti & 1];
+#pragma unroll
+            for (int j = 0; j < K; ++j) st_col<NWd>(tl + col_off + j * TS, to_col<NWd>(xs[j]));
+            load(xs, (ti + PF) * T);
+            // read back this wave's own columns (LDS keeps one wave's accesses in order)
+            encode_dyadic_f<NWd, K, M, true, false, STB>(
+                [&](int j) { return ld_col<NWd>(tl + col_off + j * TS); }, par, tabs, const_tables(a.dtables));
+#pragma unroll
+            for (int r = 0; r < M; ++r) st_col<NWd>(tl + col_off + (K + r) * TS, par[r]);
+        } else {
+            encode(xs, tile[ti & 1], par);
+            if constexpr (RING) ring_signal(&ring[ti & 1]);
+            load(xs, (ti + PF) * T);
+        }
+        store_par(par, ti * T);
+        if constexpr (!RING) bar();
+    };
+    auto edge = [&](VT (&xs)[K], int64_t ti) {
+        const bool full = ti < nfull, part = ti == nfull && tail;
+        if (full || part) slot_free(ti);
+        vm_wait<0>(xs);
+        Col<NWd> par[M];
+        if constexpr (UA) {
+            if (part) tail_cols(xs);
+        }
+        if (full || part) encode(xs, tile[ti & 1], par);
+        if (RING && (full || part)) ring_signal(&ring[ti & 1]);
+        prefetch_any(xs, ti + PF);
+        if constexpr (UA) {
+            if (full) store_par(par, ti * T);
+            else if (part && o < tail) store_tail(par);
+        } else {
+            if (full || (part && o < tail)) store_par(par, ti * T);
+        }
+        if constexpr (!RING) bar();
+    };
+    bar();  // tables visible
+    if constexpr (EP == 3) {
+#pragma unroll
+        for (int i = 0; i < K; ++i) ptab[i] = load_coef(tabs, i);
+        // consume them here, so the LDS-counter wait for the table reads sits before the
+        // loop rather than at the first use inside every step
+#pragma unroll
+        for (int i = 0; i < K; ++i) asm volatile("" ::"v"(ptab[i].ab.x), "v"(ptab[i].ab.y), "v"(ptab[i].ab.z), "v"(ptab[i].ab.w), "v"(ptab[i].c));
+    }
+#pragma unroll
+    for (int p = 0; p < PF; ++p) prefetch_any(x[p], p);
+#pragma unroll
+    for (int p = 0; p < PF; ++p) edge(x[p], p);
+    int64_t i = PF;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (; i + 2 * PF <= nfull; i += PF) {
+#pragma unroll
+        for (int p = 0; p < PF; ++p) step(x[p], i + p);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int p = 0; p < 2 * PF; ++p) edge(x[p % PF], i + p);
+    if constexpr (!RING) bar();  // the hash-only step
+#pragma unroll
+    for (int p = 0; p < PF; ++p) vm_wait<0>(x[p]);
+    stamp();
+}
+
+template <int K, int M, int G, int T, int PF, bool BUF = false, bool HQ = false, int LDSMIN = 0, bool WT = false,
+          int PM = 0, int CWX = 0, bool RING = false, int NTM = 0, bool STB = false, int EP = 0, int PFD = 0,
+          bool UA = false>
+static bool launch_ws_t(const EncArgs& a, hipStream_t s) {
+    constexpr int R = K + M;
+    constexpr int NT = ws_nh<K, M, G, T, HQ>() + G * (T / ws_cwe<K, CWX>());
+    constexpr size_t tiles = (size_t)2 * G * R * (HQ ? T + 32 : T + 16);
+    constexpr size_t dyn = tiles > (size_t)LDSMIN ? tiles : (size_t)LDSMIN;
+    if constexpr (dyn + K * 32 > 163840 || NT > 1024) {
+        return false;
+    } else {
+        if (a.dyb != M) return false;
+        if constexpr (UA) {
+            // the Split padding (n .. k*S) must lie in the last data row's tail tile
+            const int64_t tail = a.S % T;
+            if ((int64_t)K * a.S - a.n > tail || a.n <= (int64_t)(K - 1) * a.S) return false;
+        } else {
+            if ((a.S % 16) != 0 || a.n != (int64_t)K * a.S) return false;
+        }
+        if (BUF && ((G - 1) * a.data_stride + K * a.S > 0x7FFFFFFF ||
+                    (G - 1) * a.parity_stride + M * a.S > 0x7FFFFFFF || a.data_stride < 0 || a.parity_stride < 0))
+            return false;
+        auto kern = k_ehx_ws<K, M, G, T, PF, BUF, HQ, WT, PM, CWX, RING, NTM, STB, EP, PFD, UA>;
+        if (ensure_dyn_lds((const void*)kern, dyn) != hipSuccess) return false;
+        const int64_t grid = (a.n_blocks + G - 1) / G;
+        hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), dyn, s, a);
+        return true;
+    }
+}
+
+// GM multiplies the minimal stripe count per workgroup (GM = 4 on RS(8+4): 16 stripes,
+// 12 waves, one workgroup per CU, all of a CU's waves in one barrier domain).
+// LDSMIN pads the dynamic LDS so that at most 163840 / LDSMIN workgroups share a CU.
+template <int K, int M, int CW, int PF, int NBUF, bool NTS = false, int ABL = 0, bool PIPE = false,
+          int GM = 1, bool PRIO = false, int LDSMIN = 0>
+static bool launch_ehx_t(const EncArgs& a, hipStream_t s) {
+    constexpr int R = K + M;
+    // G: smallest number of stripes making 4*G*R a multiple of 64 (whole wavefronts)
+    constexpr int G0 = (R % 16 == 0) ? 1 : (R % 8 == 0) ? 2 : (R % 4 == 0) ? 4 : (R % 2 == 0) ? 8 : 16;
+    constexpr int G = G0 * GM;
+    constexpr int NT = 4 * G * R;
+    constexpr int T = (NT / G) * CW;
+    constexpr size_t tiles = (size_t)NBUF * G * R * (T + 32);
+    constexpr size_t dyn = tiles > (size_t)LDSMIN ? tiles : (size_t)LDSMIN;
+    if constexpr (dyn + K * 32 > 163840 || NT > 1024) {
+        return false;
+    } else {
+        if (a.dyb != M) return false;
+        auto kern = k_ehx<K, M, G, CW, PF, NBUF, NTS, ABL, PIPE, PRIO>;
+        if (ensure_dyn_lds((const void*)kern, dyn) != hipSuccess) return false;
+        const int64_t grid = (a.n_blocks + G - 1) / G;
+        hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), dyn, s, a);
+        return true;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// GET / heal pass, warp-specialised (replaces the arithmetic of
+// streamingBitrotReader.ReadAt's verify, bitrot-streaming.go:171-186, and
+// Erasure.DecodeDataBlocks, erasure-coding.go:96-109, for one batch of stripes).
+// Same contract as k_verify_reconstruct (kernels.hip) for exactly EX missing rows:
+// the k survivor rows are hashed and compared with their stored sums, the EX missing
+// rows rebuilt from the same loads (one HBM read per survivor), HOUT also hashes the
+// rebuilt rows.  Layout as k_ehx_ws: one workgroup per CU (LDS padded), G stripes;
+// the first 2*G*RH threads hash (pair form, RH = hashed rows per stripe), the other
+// G*T/16 rebuild (16-byte columns, untracked loads PF tiles ahead, exact vmcnt waits).
+template <int G, int RH, bool HQ>
+constexpr int vr_nh() {
+    // whole wavefronts; the pad chains hash a real row and discard the digest
+    return HQ ? ((4 * G * RH + 63) / 64) * 64 : ((2 * G * RH + 63) / 64) * 64;
+}
+
+// HQ: quad-form hash waves (one HH lane per thread; pad quads hash a real row and
+// discard the digest) for chain-latency-bound shapes (few chains per CU, e.g. RS(4+2)).
+// ST: the rebuild role reads its coefficient tables with scalar loads (SGPRs) instead of
+// from LDS (gf_dev.hpp load_coef_s): rebuilding e rows from k survivors needs e*k
+// tables per column, which from LDS is ~10x the column's own bytes for RS(16+4), e = 4.
+// BT (with ST): the scalar tables are read in batches of 4 coefficients, double-buffered
+// in SGPRs: batch i+1's s_loads are issued right after the wait for batch i and land
+// while batch i's 4 products are computed.  (Scalar loads return out of order, so every
+// wait is lgkmcnt(0); one table per wait serialises the rebuild on scalar-cache latency.)
+// NTL: non-temporal survivor loads and rebuilt-row stores.
+template <int K, int EX, bool HOUT, int G, int T, int PF, int CW = 16, bool HQ = false, bool ST = false,
+          int BT = 0, bool NTL = false>
+__global__ void __launch_bounds__((vr_nh<G, K + (HOUT ? EX : 0), HQ>() + G * (T / CW))) __attribute__((amdgpu_waves_per_eu(2)))
+k_vr_ws(VrArgs a) {
+    constexpr int RH = K + (HOUT ? EX : 0);
+    constexpr int NH = vr_nh<G, RH, HQ>();
+    constexpr int CPS = T / CW;
+    constexpr int NE = G * CPS;
+    constexpr int NT = NH + NE;
+    constexpr int TS = HQ ? T + 32 : T + 16;
+    constexpr int NPK = T / 32;
+    constexpr int NTAB = (EX > 0 ? EX : 1) * K * 8;
+    static_assert(NH % 64 == 0 && NE % 64 == 0 && T % 32 == 0, "whole wavefronts per role");
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem_dyn[];
+    uint8_t(*tile)[G * RH * TS] = reinterpret_cast<uint8_t(*)[G * RH * TS]>(smem_dyn);
+    __shared__ __attribute__((aligned(16))) uint32_t tabs[NTAB];
+    __shared__ int32_t srows[K + EX];
+
+    const int tid = threadIdx.x;
+    const int64_t blk0 = (int64_t)blockIdx.x * G;
+    const int64_t S = a.S;
+    const int R = a.k + a.m;
+    if (EX > 0)
+        for (int i = tid; i < EX * K * 8; i += NT) tabs[i] = a.tables[i];
+    for (int i = tid; i < K + EX; i += NT) srows[i] = a.rows[i];
+    const int64_t nfull = S / T;
+    const int tail = (int)(S - nfull * T);
+    int64_t iend = PF;
+    if (nfull >= 3 * PF) iend = PF + ((nfull - 3 * PF) / PF + 1) * PF;
+    const int64_t total = iend + 2 * PF + 1;
+
+    if (HQ && __builtin_amdgcn_readfirstlane(tid) < NH) {
+        // ---- hash role (quad form): lane `lane` of hashed row cj of stripe g
+        const int chain = tid >> 2, lane = tid & 3;
+        const int crow = chain < G * RH ? chain : chain - G * RH;
+        const int g = crow / RH, cj = crow % RH;
+        const int row_off = crow * TS + 8 * lane;
+        const uint32_t sel = zipper_sel(lane);
+        HHLane st = hh_init(lane, a.key[0], a.key[1], a.key[2], a.key[3]);
+        lds_barrier2();  // tables / rows (matches the rebuild role)
+        lds_barrier2();  // step 0
+        for (int64_t s = 1; s <= nfull; ++s) {
+            const uint64_t* p = reinterpret_cast<const uint64_t*>(tile[(s - 1) & 1] + row_off);
+            uint64_t w[NPK];
+#pragma unroll
+            for (int i = 0; i < NPK; ++i) w[i] = p[4 * i];
+#pragma unroll
+            for (int i = 0; i < NPK; ++i) hh_update(st, w[i], sel);
+            lds_barrier2();
+        }
+        if (tail) {
+            const uint8_t* row = tile[nfull & 1] + crow * TS;
+            hh_packets(st, row, tail >> 5, lane, sel);
+            if (tail & 31) hh_remainder(st, row + (tail & ~31), (uint32_t)(tail & 31), lane, sel);
+        }
+        for (int64_t s = nfull + 1; s < total; ++s) lds_barrier2();
+        const uint64_t h = hh_finalize256(st, lane, sel);
+        const bool live = chain < G * RH && blk0 + g < a.n_blocks;
+        const int64_t b = live && a.ids ? (int64_t)a.ids[blk0 + g] : blk0 + g;
+        const int srow = srows[cj];
+        if (cj < K) {
+            bool mis = false;
+            if (live) {
+                uint64_t want;
+                __builtin_memcpy(&want, a.expect + (b * R + srow) * 32 + 8 * lane, 8);
+                mis = want != h;
+            }
+            const unsigned long long m = __ballot(mis);
+            const bool bad = ((m >> (tid & 60)) & 0xFull) != 0;
+            if (live && lane == 0) a.bad[b * R + srow] = bad ? 1 : 0;
+        } else if (HOUT && live && a.sums_out) {
+            *reinterpret_cast<uint64_t*>(a.sums_out + (b * R + srow) * 32 + 8 * lane) = h;
+        }
+        return;
+    }
+    if (!HQ && __builtin_amdgcn_readfirstlane(tid) < NH) {
+        // ---- hash role (pair form): hashed row cj of stripe g (pad pairs past G*RH
+        // hash row chain - G*RH again and discard the digest)
+        const int chain0 = tid >> 1, hh = tid & 1;
+        const bool pad = chain0 >= G * RH;
+        const int chain = pad ? chain0 - G * RH : chain0;
+        const int g = chain / RH, cj = chain % RH;
+        const int row_off = chain * TS;
+        HHPair st = hh2_init(hh, a.key[0], a.key[1], a.key[2], a.key[3]);
+        lds_barrier2();  // tables / rows (matches the rebuild role)
+        lds_barrier2();  // step 0
+        for (int64_t s = 1; s <= nfull; ++s) {
+            const uint4* p = reinterpret_cast<const uint4*>(tile[(s - 1) & 1] + row_off) + hh;
+            uint4 w[NPK];
+#pragma unroll
+            for (int i = 0; i < NPK; ++i) w[i] = p[2 * i];
+#pragma unroll
+            for (int i = 0; i < NPK; ++i)
+                hh2_update(st, ((uint64_t)w[i].y << 32) | w[i].x, ((uint64_t)w[i].w << 32) | w[i].z);
+            lds_barrier2();
+        }
+        if (tail) {
+            const uint8_t* row = tile[nfull & 1] + row_off;
+            hh2_packets(st, row, tail >> 5, hh);
+            if (tail & 31) hh2_remainder(st, row + (tail & ~31), (uint32_t)(tail & 31), hh);
+        }
+        for (int64_t s = nfull + 1; s < total; ++s) lds_barrier2();
+        uint64_t d0, d1;
+        hh2_finalize256(st, d0, d1);
+        const bool live = !pad && blk0 + g < a.n_blocks;
+        const int64_t b = live && a.ids ? (int64_t)a.ids[blk0 + g] : blk0 + g;
+        const int srow = srows[cj];
+        if (cj < K) {
+            // errFileCorrupt per (stripe, survivor): either half of the digest differs
+            bool mis = false;
+            if (live) {
+                uint64_t e0, e1;
+                __builtin_memcpy(&e0, a.expect + (b * R + srow) * 32 + 16 * hh, 8);
+                __builtin_memcpy(&e1, a.expect + (b * R + srow) * 32 + 16 * hh + 8, 8);
+                mis = e0 != d0 || e1 != d1;
+            }
+            const unsigned long long m = __ballot(mis);
+            const bool bad = ((m >> (tid & 62)) & 3ull) != 0;
+            if (live && hh == 0) a.bad[b * R + srow] = bad ? 1 : 0;
+        } else if (HOUT && live && a.sums_out) {
+            uint64_t* out = reinterpret_cast<uint64_t*>(a.sums_out + (b * R + srow) * 32 + 16 * hh);
+            out[0] = d0;
+            out[1] = d1;
+        }
+        return;
+    }
+
+    // ---- rebuild role: CW-byte column o of stripe g
+    constexpr int NWd = CW / 4;
+    typedef typename VecOf<NWd>::type VT;
+    const int e = tid - NH;
+    const int g = e / CPS, o = (e % CPS) * CW;
+    const int64_t bl = (blk0 + g) < a.n_blocks ? (blk0 + g) : (a.n_blocks - 1);
+    const int64_t b = a.ids ? (int64_t)a.ids[bl] : bl;
+    uint8_t* blk = a.shards + b * a.block_stride + o;
+    const int col_off = g * RH * TS + o;
+    lds_barrier2();  // tables / rows visible
+    // row offsets in 32 bits (the launch requires (k + m) * S < 2^31): half the SGPRs
+    uint32_t roff[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) roff[j] = (uint32_t)__builtin_amdgcn_readfirstlane(srows[j]) * (uint32_t)S;
+    uint32_t ooff[EX > 0 ? EX : 1];
+#pragma unroll
+    for (int r = 0; r < EX; ++r) ooff[r] = (uint32_t)__builtin_amdgcn_readfirstlane(srows[K + r]) * (uint32_t)S;
+
+    VT x[PF][K];
+    auto load = [&](VT (&xs)[K], int64_t t0) {
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            if constexpr (NTL)
+                ld_async_nt<NWd>(xs[j], blk + roff[j] + t0);
+            else
+                ld_async<NWd>(xs[j], blk + roff[j] + t0);
+        }
+    };
+    auto prefetch_any = [&](VT (&xs)[K], int64_t tn) {
+        const bool ok = tn < nfull || (tn == nfull && o < tail);
+        load(xs, ok ? tn * T : 0);
+    };
+    // survivors to LDS, rebuilt rows into y (and LDS when hashed)
+    auto rebuild = [&](VT (&xr)[K], uint8_t* tl, Col<NWd> (&y)[EX > 0 ? EX : 1]) {
+        Col<NWd> xs[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) xs[j] = to_col<NWd>(xr[j]);
+        if constexpr (EX > 0) {
+            const uint32_t* tb = tabs + opaque_zero();
+            // opaque offset: the tables are reloaded per tile (scalar cache hits), not
+            // hoisted out of the tile loop into e*k*5 SGPRs
+            const ctab_ptr tg = const_tables(a.tables) + opaque_zero();
+            constexpr int NB = BT > 0 ? BT : 4;  // BT: coefficients per scalar batch
+            CoefTab tbat[2][NB];
+            auto load_batch = [&](CoefTab (&d)[NB], int c0) {
+#pragma unroll
+                for (int i = 0; i < NB; ++i) d[i] = load_coef_s(tg, c0 + i);
+            };
+            // BT: consume batch d (the wait for its scalar loads sits here), then issue the
+            // next batch's loads, then compute; the scheduling barriers keep that order
+            auto wait_batch = [&](const CoefTab (&d)[NB]) {
+#pragma unroll
+                for (int i = 0; i < NB; ++i)
+                    asm volatile("" ::"s"(d[i].ab.x), "s"(d[i].ab.y), "s"(d[i].ab.z), "s"(d[i].ab.w), "s"(d[i].c));
+                __builtin_amdgcn_sched_barrier(0);
+            };
+            if constexpr (ST && BT) {
+                static_assert(K % NB == 0, "whole batches per rebuilt row");
+                load_batch(tbat[0], 0);
+            }
+#pragma unroll
+            for (int r = 0; r < EX; ++r) {
+                GfAcc acc[NWd];
+#pragma unroll
+                for (int w = 0; w < NWd; ++w) acc_init(acc[w]);
+#pragma unroll
+                for (int j = 0; j < K; ++j) {
+                    if constexpr (ST && BT) {
+                        const int c = r * K + j, bi = c / NB, cur = bi & 1;
+                        if (c % NB == 0) {
+                            wait_batch(tbat[cur]);
+                            if (c + NB < EX * K) load_batch(tbat[cur ^ 1], c + NB);
+                            __builtin_amdgcn_sched_barrier(0);
+                        }
+                        const CoefTab t = tbat[cur][c % NB];
+#pragma unroll
+                        for (int w = 0; w < NWd; ++w) acc_add(acc[w], gf_lookup_s(split_nibbles(xs[j].w[w]), t));
+                    } else if constexpr (ST) {
+                        const CoefTab t = load_coef_s(tg, r * K + j);
+#pragma unroll
+                        for (int w = 0; w < NWd; ++w) acc_add(acc[w], gf_lookup_s(split_nibbles(xs[j].w[w]), t));
+                    } else {
+                        const CoefTab t = load_coef(tb, r * K + j);
+#pragma unroll
+                        for (int w = 0; w < NWd; ++w) acc_add(acc[w], gf_lookup(split_nibbles(xs[j].w[w]), t));
+                    }
+                }
+#pragma unroll
+                for (int w = 0; w < NWd; ++w) y[r].w[w] = acc_done(acc[w]);
+                // one rebuilt row at a time: its K coefficient tables, not all E*K, live
+                if constexpr (!(ST && BT)) __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < K; ++j) st_col<NWd>(tl + col_off + j * TS, xs[j]);
+        if constexpr (HOUT) {
+#pragma unroll
+            for (int r = 0; r < EX; ++r) st_col<NWd>(tl + col_off + (K + r) * TS, y[r]);
+        }
+    };
+    auto store_rows = [&](const Col<NWd> (&y)[EX > 0 ? EX : 1], int64_t t0) {
+#pragma unroll
+        for (int r = 0; r < EX; ++r) {
+            if constexpr (NTL)
+                st_col_nt<NWd>(blk + ooff[r] + t0, y[r]);
+            else
+                st_col<NWd>(blk + ooff[r] + t0, y[r]);
+        }
+    };
+    auto step = [&](VT (&xs)[K], int64_t ti) {
+        Col<NWd> y[EX > 0 ? EX : 1];
+        vm_wait<EX + (PF - 1) * (K + EX)>(xs);
+        rebuild(xs, tile[ti & 1], y);
+        load(xs, (ti + PF) * T);
+        store_rows(y, ti * T);
+        lds_barrier2();
+    };
+    auto edge = [&](VT (&xs)[K], int64_t ti) {
+        const bool full = ti < nfull, part = ti == nfull && tail;
+        vm_wait<0>(xs);
+        Col<NWd> y[EX > 0 ? EX : 1];
+        if (full || part) rebuild(xs, tile[ti & 1], y);
+        prefetch_any(xs, ti + PF);
+        if (full || (part && o < tail)) store_rows(y, ti * T);
+        lds_barrier2();
+    };
+#pragma unroll
+    for (int p = 0; p < PF; ++p) prefetch_any(x[p], p);
+    // edge(0) is step 0: its barrier pairs with the hash role's second barrier
+#pragma unroll
+    for (int p = 0; p < PF; ++p) edge(x[p], p);
+    int64_t i = PF;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (; i + 2 * PF <= nfull; i += PF) {
+#pragma unroll
+        for (int p = 0; p < PF; ++p) step(x[p], i + p);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int p = 0; p < 2 * PF; ++p) edge(x[p % PF], i + p);
+    lds_barrier2();  // the hash-only step
+#pragma unroll
+    for (int p = 0; p < PF; ++p) vm_wait<0>(x[p]);
+}
+
+template <int K, int EX, bool HOUT, int G, int T, int PF, int CW, bool HQ, bool ST, int BT, bool NTL = false>
+static bool launch_vr_ws_bt(const VrArgs& a, hipStream_t s);
+
+template <int K, int EX, bool HOUT, int G, int T, int PF, int CW = 16, bool HQ = false, bool ST = false,
+          int BT = 0>
+static bool launch_vr_ws_t(const VrArgs& a, hipStream_t s) {
+    // diagnostics 240: the same launch with the scalar-table batching flipped (off <-> 4
+    // coefficients per batch); 241: batches of 2
+    if constexpr (ZS3_DIAG && ST) {
+        if (a.variant == 240) return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, (BT ? 0 : 4), true>(a, s);
+        if (a.variant == 241) return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, 2, true>(a, s);
+    }
+    // Survivor loads and rebuilt-row stores are non-temporal (each byte is touched once):
+    // RS(8+4) verify 0.706 -> 0.627 ms, RS(16+4) verify 0.386 -> 0.351, rebuild 1-4 and
+    // heals 1-5 % faster (profiles/r02/ab_get_nt.jsonl).  Diagnostics 246: plain loads.
+    if constexpr (ZS3_DIAG) {
+        if (a.variant == 246) return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, BT, false>(a, s);
+    }
+    return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, BT, true>(a, s);
+}
+
+template <int K, int EX, bool HOUT, int G, int T, int PF, int CW, bool HQ, bool ST, int BT, bool NTL>
+static bool launch_vr_ws_bt(const VrArgs& a, hipStream_t s) {
+    constexpr int RH = K + (HOUT ? EX : 0);
+    constexpr int NT = vr_nh<G, RH, HQ>() + G * (T / CW);
+    constexpr size_t tiles = (size_t)2 * G * RH * (HQ ? T + 32 : T + 16);
+    constexpr size_t dyn = tiles > 83968 ? tiles : 83968;  // one workgroup per CU
+    if constexpr (dyn + (size_t)(EX > 0 ? EX : 1) * K * 32 + 4 * (K + EX) > 163840 || NT > 1024 ||
+                  vr_nh<G, RH, HQ>() % 64 != 0 || (G * (T / CW)) % 64 != 0) {
+        return false;
+    } else {
+        if (a.e != EX || (a.S % 16) != 0 || a.k != K || (HOUT != (a.sums_out != nullptr) && EX > 0)) return false;
+        if ((int64_t)(a.k + a.m) * a.S >= ((int64_t)1 << 31)) return false;  // 32-bit row offsets
+        auto kern = k_vr_ws<K, EX, HOUT, G, T, PF, CW, HQ, ST, BT, NTL>;
+        if (ensure_dyn_lds((const void*)kern, dyn) != hipSuccess) return false;
+        const int64_t grid = (a.n_blocks + G - 1) / G;
+        hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), dyn, s, a);
+        return true;
+    }
+}
+
+#if ZS3_DIAG
+// RS(16+4) rebuild / heal with the survivor prefetch depth and tile length as
+// parameters (diagnostics 250-259, round 3; PF = 2 with 8-byte columns spills
+// in-flight load registers, scripts/check_async_loads.py, so no such instance): e = 1..4 rebuilt rows.
+template <int T, int PF, bool HOUT, int BT, int CW = 4>
+static bool vr16(const VrArgs& a, hipStream_t s) {
+    switch (a.e) {
+        case 1: return launch_vr_ws_t<16, 1, HOUT, 8, T, PF, CW, false, true, BT>(a, s);
+        case 2: return launch_vr_ws_t<16, 2, HOUT, 8, T, PF, CW, false, true, BT>(a, s);
+        case 3: return launch_vr_ws_t<16, 3, HOUT, 8, T, PF, CW, false, true, BT>(a, s);
+        case 4: return launch_vr_ws_t<16, 4, HOUT, 8, T, PF, CW, false, true, BT>(a, s);
+        default: return false;
+    }
+}
+#endif
+
+#if ZS3_DIAG
+// Encode variants of the diagnostics build, one translation unit per shape
+// (fused_v2_km84.hip, fused_v2_km42.hip, fused_v2_km164.hip)
+bool launch_ehx_km_8_4(int v, const EncArgs& a, hipStream_t s);
+bool launch_ehx_km_4_2(int v, const EncArgs& a, hipStream_t s);
+bool launch_ehx_km_16_4(int v, const EncArgs& a, hipStream_t s);
+#endif
+
+}  // namespace zs3k

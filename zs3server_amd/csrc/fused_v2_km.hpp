@@ -1,0 +1,107 @@
+// fused_v2_km.hpp — encode variants of the diagnostics build (A/B and ablation
+// instances of k_ehx / k_ehx_ws, measured in profiles/r0*/ and tests/test_gpu_variants.py),
+// instantiated once per shape by fused_v2_km{84,42,164}.hip.
+#pragma once
+#include "fused_v2.hpp"
+
+namespace zs3k {
+
+#if ZS3_DIAG
+template <int K, int M>
+static bool launch_ehx_km(int v, const EncArgs& a, hipStream_t s) {
+    constexpr bool deep = K == 8 && M == 4;
+    constexpr bool few = K == 4 && M == 2;  // BASELINE config 2: 1024 objects, latency-bound
+    switch (v) {
+        case 90: if constexpr (few) return launch_ehx_t<K, M, 8, 4, 2, false, 0, false, 1, false, 83968>(a, s); else return false;
+        case 91: if constexpr (few) return launch_ehx_t<K, M, 8, 4, 2, false, 0, true, 1, false, 83968>(a, s); else return false;
+        case 92: if constexpr (few) return launch_ehx_t<K, M, 8, 2, 2, false, 0, false, 1, false, 83968>(a, s); else return false;
+        case 93: if constexpr (few) return launch_ehx_t<K, M, 8, 4, 2>(a, s); else return false;
+        case 94: if constexpr (few) return launch_ehx_t<K, M, 8, 8, 2, false, 0, false, 1, false, 83968>(a, s); else return false;
+        case 50: return launch_ehx_t<K, M, 8, 1, 2>(a, s);
+        case 51: return launch_ehx_t<K, M, 8, 1, 1>(a, s);
+        case 52: if constexpr (deep) return launch_ehx_t<K, M, 8, 2, 2>(a, s); else return false;
+        case 53: if constexpr (deep) return launch_ehx_t<K, M, 8, 2, 1>(a, s); else return false;
+        case 55: return launch_ehx_t<K, M, 8, 1, 2, true>(a, s);
+        case 70: return launch_ehx_t<K, M, 8, 1, 2, false, 0, true>(a, s);
+        case 71: if constexpr (deep) return launch_ehx_t<K, M, 8, 2, 2, false, 0, true>(a, s); else return false;
+        case 80: if constexpr (deep) return launch_ehx_t<K, M, 8, 1, 2, false, 0, false, 4>(a, s); else return false;
+        case 81: if constexpr (deep) return launch_ehx_t<K, M, 8, 1, 1, false, 0, false, 4, false, 83968>(a, s); else return false;
+        case 82: return launch_ehx_t<K, M, 8, 1, 2, false, 0, false, 1, true>(a, s);
+        case 83: if constexpr (deep) return launch_ehx_t<K, M, 8, 2, 2, false, 0, false, 4>(a, s); else return false;
+        case 84: if constexpr (deep) return launch_ehx_t<K, M, 8, 1, 2, false, 0, false, 2>(a, s); else return false;
+        case 85: if constexpr (deep) return launch_ehx_t<K, M, 8, 1, 2, false, 0, true, 4>(a, s); else return false;
+        case 86: if constexpr (deep) return launch_ehx_t<K, M, 8, 1, 2, false, 1, false, 4>(a, s); else return false;
+        case 87: if constexpr (deep) return launch_ehx_t<K, M, 8, 1, 2, false, 2, false, 4>(a, s); else return false;
+        case 88: if constexpr (deep) return launch_ehx_t<K, M, 8, 1, 2, false, 3, false, 4>(a, s); else return false;
+        case 100: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1>(a, s); else return false;
+        case 103: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 2, true>(a, s); else return false;
+        case 102: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, true>(a, s); else return false;
+        case 109: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, true, false, 0, false, 1>(a, s); else return false;
+        case 108: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 4>(a, s); else return false;
+        case 105: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1>(a, s); else return false;
+        case 106: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 2>(a, s); else return false;
+        case 107: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 3>(a, s); else return false;
+        case 104: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, true>(a, s); else return false;
+        case 150: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 1>(a, s); else return false;
+        case 151: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3>(a, s); else return false;
+        case 155: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, true>(a, s); else return false;
+        case 153: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 2>(a, s); else return false;
+        case 154: if constexpr (deep) return launch_ws_t<K, M, 8, 384, 1, false, false, 0, false, 1, 0, false, 2>(a, s); else return false;
+        case 117: if constexpr (few) return launch_ws_t<K, M, 4, 512, 4, false, true, 83968, false, 0, 0, false, 3>(a, s); else return false;
+        case 133: if constexpr (deep) return launch_ws_t<K, M, 8, 384, 1, false, false, 0, false, 1, 0, false, 3>(a, s); else return false;
+        case 125: if constexpr (K == 16 && M == 4) return launch_ws_t<K, M, 4, 512, 1, true, true, 0, false, 0, 0, false, 3>(a, s); else return false;
+        case 156: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 1>(a, s); else return false;
+        case 157: if constexpr (few) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 1>(a, s); else return false;
+        case 160: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 2>(a, s); else return false;
+        case 161: if constexpr (few) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 2>(a, s); else return false;
+        case 163: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 3>(a, s); else return false;
+        case 164: if constexpr (few) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 3>(a, s); else return false;
+        // L2 prefetch of the data rows PFD tiles ahead by the hash waves (product 151 + PFD)
+        case 170: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 0, 2>(a, s); else return false;
+        case 171: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 0, 3>(a, s); else return false;
+        case 172: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 0, 4>(a, s); else return false;
+        case 173: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 0, 6>(a, s); else return false;
+        case 174: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 2, false, 0, 3>(a, s); else return false;
+        case 175: if constexpr (K == 16 && M == 4) return launch_ws_t<K, M, 8, 384, 1, true, false, 0, false, 0, 0, false, 3, false, 2, 3>(a, s); else return false;
+        // tile / wave-count shapes for RS(8+4) at the product's memory policy (r03)
+        case 180: if constexpr (deep) return launch_ws_t<K, M, 8, 768, 1, false, false, 0, false, 1, 0, false, 3>(a, s); else return false;
+        case 182: if constexpr (deep) return launch_ws_t<K, M, 8, 768, 1, false, false, 0, false, 1, 8, false, 3>(a, s); else return false;
+        case 183: if constexpr (deep) return launch_ws_t<K, M, 8, 512, 2, false, false, 0, false, 1, 0, false, 3>(a, s); else return false;
+        case 184: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, true, 1, 0, false, 3>(a, s); else return false;
+        case 185: if constexpr (deep) return launch_ws_t<K, M, 16, 256, 1, false, false, 0, false, 1, 0, false, 3>(a, s); else return false;
+        case 186: if constexpr (deep) return launch_ws_t<K, M, 8, 512, 1, false, false, 0, false, 1, 0, false, 3>(a, s); else return false;
+        // config 2 (latency-bound chains): longer tiles = fewer per-step barriers and LDS
+        // read latencies on the chain's critical path
+        case 177: if constexpr (few) return launch_ws_t<K, M, 4, 1024, 4, false, true, 83968, false, 0, 0, false, 3>(a, s); else return false;
+        case 178: if constexpr (few) return launch_ws_t<K, M, 4, 1024, 2, false, true, 83968, false, 0, 0, false, 3>(a, s); else return false;
+        case 179: if constexpr (few) return launch_ws_t<K, M, 4, 2048, 2, false, true, 83968, false, 0, 0, false, 3>(a, s); else return false;
+        case 176: if constexpr (few) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 0, 3>(a, s); else return false;
+        case 168: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 8>(a, s); else return false;
+        case 169: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 9>(a, s); else return false;
+        case 162: if constexpr (K == 16 && M == 4) return launch_ws_t<K, M, 8, 384, 1, true, false, 0, false, 0, 0, false, 3, false, 2>(a, s); else return false;
+        case 152: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 2, false, false, 0, false, 1>(a, s); else return false;
+        case 140: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, true>(a, s); else return false;
+        case 141: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 0, 0, true>(a, s); else return false;
+        case 130: if constexpr (deep) return launch_ws_t<K, M, 8, 384, 1, false, false, 0, false, 1>(a, s); else return false;
+        case 131: if constexpr (deep) return launch_ws_t<K, M, 4, 512, 2, false, true>(a, s); else return false;
+        case 132: if constexpr (deep) return launch_ws_t<K, M, 2, 512, 2, false, true>(a, s); else return false;
+        case 120: if constexpr (K == 16 && M == 4) return launch_ws_t<K, M, 8, 384, 1, true>(a, s); else return false;
+        case 122: if constexpr (K == 16 && M == 4) return launch_ws_t<K, M, 8, 384, 1, true, false, 0, false, 0, 0, false, 3>(a, s); else return false;
+        case 123: if constexpr (K == 16 && M == 4) return launch_ws_t<K, M, 8, 384, 1, true, false, 0, false, 0, 0, false, 2>(a, s); else return false;
+        case 124: if constexpr (K == 16 && M == 4) return launch_ws_t<K, M, 4, 512, 1, true, true, 0, false, 0, 0, false, 3>(a, s); else return false;
+        case 121: if constexpr (K == 16 && M == 4) return launch_ws_t<K, M, 4, 512, 1, true, true>(a, s); else return false;
+        case 110: if constexpr (few) return launch_ws_t<K, M, 4, 512, 2, false, true, 83968>(a, s); else return false;
+        case 111: if constexpr (few) return launch_ws_t<K, M, 4, 512, 4, false, true, 83968>(a, s); else return false;
+        case 112: if constexpr (few) return launch_ws_t<K, M, 4, 256, 4, false, true, 83968>(a, s); else return false;
+        case 113: if constexpr (few) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1>(a, s); else return false;
+        case 114: if constexpr (few) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 2>(a, s); else return false;
+        case 115: if constexpr (few) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3>(a, s); else return false;
+        case 116: if constexpr (few) return launch_ws_t<K, M, 4, 512, 4, false, true, 83968, false, 0, 0, false, 2>(a, s); else return false;
+        case 61: if constexpr (deep) return launch_ehx_t<K, M, 8, 1, 2, false, 1>(a, s); else return false;
+        case 64: if constexpr (deep) return launch_ehx_t<K, M, 8, 2, 2, false, 1>(a, s); else return false;
+        default: return false;
+    }
+}
+#endif  // ZS3_DIAG
+
+}  // namespace zs3k

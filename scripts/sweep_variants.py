@@ -21,7 +21,7 @@ ALIAS = os.environ.get("SWEEP_ALIAS", "0") == "1"
 res = []
 for k, m, nobj in SHAPES:
     blen = 1 << 20
-    S = blen // k
+    S = -(-blen // k)  # reedsolomon shard size (ceil)
     stride = (k + m) * S
     codec = z.Codec(k, m)
     buf = torch.empty(nobj * stride, dtype=torch.uint8, device="cuda")

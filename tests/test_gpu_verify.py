@@ -76,7 +76,8 @@ WS_CASES = [(8, 4, 1 << 16, []), (8, 4, 1 << 16, [0, 5]), (8, 4, 1 << 16, [3, 9]
 @pytest.mark.parametrize("k,m,blen,erased", WS_CASES)
 @pytest.mark.parametrize("data_only", [True, False])
 @pytest.mark.parametrize("heal", [False, True])
-@pytest.mark.parametrize("variant", [0, 210, 211, 212, 213, 214, 216, 218, 230, 231, 232, 240, 241, 246])
+@pytest.mark.parametrize("variant", [0, 210, 211, 212, 213, 214, 216, 218, 230, 231, 232, 240, 241, 246,
+                                     260, 261, 262, 263])
 def test_verify_reconstruct_ws(oracle, k, m, blen, erased, data_only, heal, variant):
     """Variant 0: the product dispatch; at 17 blocks it takes the small-batch latency
     path (k_reconstruct + one chain per quad).  231 = the product dispatch without that
@@ -89,6 +90,10 @@ def test_verify_reconstruct_ws(oracle, k, m, blen, erased, data_only, heal, vari
     if variant in (231, 240, 241, 246):  # 240 / 241: scalar-table batching flipped / pairs; 246: plain loads
         want = 2
     if variant == 232 and heal and e >= 3:  # heal 3-4 on k_vr_ws (padded pair form)
+        want = 2
+    if variant in (260, 261, 262) and heal and e >= 1:  # r03 longer-tile heal instances
+        want = 2
+    if variant == 263 and not heal and e >= 1:  # r03 8-stripe rebuild, 384-byte tiles
         want = 2
     with variant_ctx(variant):
         run_verify_case(oracle, k, m, blen, erased, data_only, heal, nb=17, want_path=want)
@@ -110,6 +115,7 @@ def test_verify_reconstruct_ws_rs42(oracle, k, m, blen, erased, data_only, heal,
 
 
 WS16_HEAL_CASES = [(16, 4, 1 << 16, [0, 5]), (16, 4, 1 << 16, [3, 17]), (16, 4, 16 * 48, [2, 19]),
+                   (16, 4, 16 * 1536, [3, 17]), (16, 4, 16 * 1536, [0, 1, 16, 19]), (16, 4, 16 * 768, [5]),
                    (16, 4, 16 * (256 * 3 + 16), [0, 1, 16, 19]), (16, 4, 16 * 256, [4, 5, 6, 7]),
                    (16, 4, 16 * (256 * 2 + 48), [15, 18]), (16, 4, 1 << 16, [7]), (16, 4, 16 * 48, [18]),
                    (16, 4, 16 * (256 * 3 + 16), [16]), (16, 4, 16 * (256 * 2 + 48), [2, 9, 19]),
@@ -117,7 +123,7 @@ WS16_HEAL_CASES = [(16, 4, 1 << 16, [0, 5]), (16, 4, 1 << 16, [3, 17]), (16, 4, 
 
 
 @pytest.mark.parametrize("k,m,blen,erased", WS16_HEAL_CASES)
-@pytest.mark.parametrize("variant", [0, 215, 216, 218, 231, 232, 240, 241, 246])
+@pytest.mark.parametrize("variant", [0, 215, 216, 218, 231, 232, 240, 241, 242, 246, 250, 256, 259])
 def test_heal_ws_rs164(oracle, k, m, blen, erased, variant):
     """RS(16+4) heal (rebuild 1-4 shards and hash them) on k_vr_ws: the defaults (231 =
     the product dispatch without the small-batch latency path that variant 0 takes at 11
@@ -128,7 +134,7 @@ def test_heal_ws_rs164(oracle, k, m, blen, erased, variant):
     tails and dead stripes of the 8-stripe workgroup."""
     e = len(erased)
     want = {0: 4, 231: 2, 215: 2 if e in (2, 4) else None, 216: 2, 218: 2,
-            232: 2 if e >= 2 else 1, 240: 2, 241: 2, 246: 2}[variant]
+            232: 2, 240: 2, 241: 2, 242: 2, 246: 2, 250: None, 256: None, 259: 2}[variant]
     with variant_ctx(variant):
         run_verify_case(oracle, k, m, blen, erased, False, True, nb=11, want_path=want)
 
@@ -136,14 +142,14 @@ def test_heal_ws_rs164(oracle, k, m, blen, erased, variant):
 # RS(16+4) GET on the default k_vr_ws (8-byte rebuild columns, e = 2 and e = 4): tile
 # edges, ragged tails and dead stripes of the 8-stripe workgroup (nb = 11)
 WS16_GET_CASES = [(16, 4, blen, erased, data_only)
-                  for blen in (1 << 16, 16 * 48, 16 * (256 * 3 + 16), 16 * (256 * 2 + 48))
+                  for blen in (1 << 16, 16 * 48, 16 * (256 * 3 + 16), 16 * (256 * 2 + 48), 16 * 1536)
                   for erased, data_only in (([0, 5], True), ([4, 15], True), ([3, 17], False),
                                             ([0, 1, 16, 19], False), ([2, 7, 9, 12], True), ([6], True),
                                             ([1, 7, 15], True), ([5, 18], True), ([0, 13, 16], False))]
 
 
 @pytest.mark.parametrize("k,m,blen,erased,data_only", WS16_GET_CASES)
-@pytest.mark.parametrize("variant", [0, 216, 217, 219, 231, 240, 241, 246])
+@pytest.mark.parametrize("variant", [0, 216, 217, 219, 231, 240, 241, 242, 246, 250, 256, 259])
 def test_verify_reconstruct_ws_rs164(oracle, k, m, blen, erased, data_only, variant):
     """The RS(16+4) rebuild-1..4 defaults (231: without the small-batch latency path
     that variant 0 takes at 11 blocks) run the warp-specialised kernel (asserted through

@@ -1353,10 +1353,11 @@ static bool vr16(const VrArgs& a, hipStream_t s) {
 
 #if ZS3_DIAG
 // Encode variants of the diagnostics build, one translation unit per shape
-// (fused_v2_km84.hip, fused_v2_km42.hip, fused_v2_km164.hip)
+// (fused_v2_km84.hip, fused_v2_km42.hip, fused_v2_km164.hip, fused_v2_km124.hip)
 bool launch_ehx_km_8_4(int v, const EncArgs& a, hipStream_t s);
 bool launch_ehx_km_4_2(int v, const EncArgs& a, hipStream_t s);
 bool launch_ehx_km_16_4(int v, const EncArgs& a, hipStream_t s);
+bool launch_ehx_km_12_4(int v, const EncArgs& a, hipStream_t s);
 #endif
 
 }  // namespace zs3k

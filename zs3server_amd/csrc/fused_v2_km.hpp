@@ -70,6 +70,13 @@ static bool launch_ehx_km(int v, const EncArgs& a, hipStream_t s) {
         case 184: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, true, 1, 0, false, 3>(a, s); else return false;
         case 185: if constexpr (deep) return launch_ws_t<K, M, 16, 256, 1, false, false, 0, false, 1, 0, false, 3>(a, s); else return false;
         case 186: if constexpr (deep) return launch_ws_t<K, M, 8, 512, 1, false, false, 0, false, 1, 0, false, 3>(a, s); else return false;
+        // issue priority on the product shape (r03 stamps: the SIMDs holding one hash and
+        // two encode waves are the critical path): 191 younger encode wave of each pair at
+        // 2 (PM = 2), 192 hash waves at 1 (PM = 3), 193 no priorities, 194 = 191 + WT stamps
+        case 191: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 2, 0, false, 3>(a, s); else return false;
+        case 192: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 3, 0, false, 3>(a, s); else return false;
+        case 193: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 0, 0, false, 3>(a, s); else return false;
+        case 194: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, true, 2, 0, false, 3>(a, s); else return false;
         // config 2 (latency-bound chains): longer tiles = fewer per-step barriers and LDS
         // read latencies on the chain's critical path
         case 177: if constexpr (few) return launch_ws_t<K, M, 4, 1024, 4, false, true, 83968, false, 0, 0, false, 3>(a, s); else return false;

@@ -1,0 +1,27 @@
+// fused_v2_km124.hip — RS(12+4) encode variants on 1 MiB blocks (diagnostics build only).
+// RS(12+4) is the server's default for 16-drive sets (cmd/format-erasure.go:870-881);
+// 1 MiB blocks give S = 87 382 (rows 2-byte aligned), so every instance runs k_ehx_ws in
+// UA mode with buffer-addressed rows.  The product instance (launch_ehx_ua: 8 stripes,
+// 8-byte columns of 384-byte tiles) has 4 hash + 6 encode waves, i.e. two SIMDs with
+// two encode waves and two with one; these shapes put the same work on every SIMD:
+//  195: 16 stripes, 8-byte columns of 256-byte tiles: 8 hash + 8 encode waves (16 waves,
+//       2 + 2 per SIMD, 128 VGPRs)
+//  196: 8 stripes, 8-byte columns of 512-byte tiles: 4 hash + 8 encode waves (1 + 2 per
+//       SIMD), data rows written to LDS before the encode
+//  197: 196 without the early data write
+#include "fused_v2.hpp"
+
+namespace zs3k {
+
+#if ZS3_DIAG
+bool launch_ehx_km_12_4(int v, const EncArgs& a, hipStream_t s) {
+    switch (v) {
+        case 195: return launch_ws_t<12, 4, 16, 256, 1, true, false, 0, false, 0, 8, false, 3, false, 0, 0, true>(a, s);
+        case 196: return launch_ws_t<12, 4, 8, 512, 1, true, false, 0, false, 0, 8, false, 3, false, 2, 0, true>(a, s);
+        case 197: return launch_ws_t<12, 4, 8, 512, 1, true, false, 0, false, 0, 8, false, 3, false, 0, 0, true>(a, s);
+        default: return false;
+    }
+}
+#endif
+
+}  // namespace zs3k

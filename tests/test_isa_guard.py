@@ -31,7 +31,7 @@ def test_untracked_loads_never_touched_in_flight(tmp_path, diag):
 
     # every translation unit that instantiates fused_v2.hpp's kernels, compiled in parallel
     units = ["fused_v2.hip", "fused_v2_get.hip"] + (
-        ["fused_v2_get_diag.hip", "fused_v2_km84.hip", "fused_v2_km42.hip", "fused_v2_km164.hip",
+        ["fused_v2_get_diag4.hip", "fused_v2_get_diag8.hip", "fused_v2_get_diag16.hip", "fused_v2_km84.hip", "fused_v2_km42.hip", "fused_v2_km164.hip",
          "fused_v2_km124.hip"] if diag else [])
     procs = []
     for u in units:

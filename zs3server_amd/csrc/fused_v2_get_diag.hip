@@ -6,191 +6,18 @@
 namespace zs3k {
 
 #if ZS3_DIAG
-// Diagnostics variants of the GET / heal pass (v != 0): A/B instances measured against
-// the product defaults (fused_v2_get.hip) in profiles/r02 and profiles/r03.
+// Diagnostics variants of the GET / heal pass (v != 0), one translation unit per data
+// shard count (compiled in parallel): A/B instances measured against the product
+// defaults (fused_v2_get.hip) in profiles/r02 and profiles/r03.
+bool launch_vr_ws_diag_k4(int v, const VrArgs& a, hipStream_t s);   // fused_v2_get_diag4.hip
+bool launch_vr_ws_diag_k8(int v, const VrArgs& a, hipStream_t s);   // fused_v2_get_diag8.hip
+bool launch_vr_ws_diag_k16(int v, const VrArgs& a, hipStream_t s);  // fused_v2_get_diag16.hip
+
 bool launch_vr_ws_diag(int v, const VrArgs& a, hipStream_t s) {
-    if (a.k == 16 && v >= 250 && v <= 259 && a.e >= 1) {
-        const bool h = a.sums_out != nullptr;
-        switch (v) {
-            case 250: return h ? vr16<128, 2, true, 4>(a, s) : vr16<256, 2, false, 0>(a, s);
-            case 251: return h ? vr16<128, 3, true, 0>(a, s) : vr16<128, 3, false, 4>(a, s);
-            case 252: return h ? vr16<256, 2, true, 4>(a, s) : vr16<256, 3, false, 0>(a, s);
-            case 253: return h ? vr16<256, 1, true, 4>(a, s) : vr16<512, 1, false, 0>(a, s);
-            case 254: return h ? vr16<128, 3, true, 4>(a, s) : vr16<128, 2, false, 0>(a, s);
-            case 255: return h ? vr16<256, 2, true, 0>(a, s) : vr16<256, 2, false, 4>(a, s);
-            case 256: return h ? vr16<256, 1, true, 4, 8>(a, s) : vr16<512, 1, false, 4, 8>(a, s);
-            case 257: return h ? vr16<512, 1, true, 4, 8>(a, s) : vr16<256, 2, false, 4, 8>(a, s);
-            case 259: return h ? vr16<384, 1, true, 4, 8>(a, s) : vr16<384, 1, false, 4, 8>(a, s);
-            default: return false;
-        }
-    }
-    if (a.k == 4 && v == 214) {
-        // the RS(4+2)-shaped product instances (quad-form hash waves, 8 stripes)
-        if (a.sums_out != nullptr)
-            return a.e == 2 && launch_vr_ws_t<4, 2, true, 8, 256, 4, 16, true>(a, s);
-        if (a.e == 0) return launch_vr_ws_t<4, 0, false, 8, 256, 4, 16, true>(a, s);
-        if (a.e == 1) return launch_vr_ws_t<4, 1, false, 8, 256, 4, 16, true>(a, s);
-        if (a.e == 2) return launch_vr_ws_t<4, 2, false, 8, 256, 4, 16, true>(a, s);
-        return false;
-    }
-    if (a.k == 4 && v == 210) {
-        // RS(4+2)-shaped GET / heal, pair-form hash waves: 16 stripes, 256-byte tiles
-        if (a.sums_out != nullptr)
-            return a.e == 2 && launch_vr_ws_t<4, 2, true, 16, 256, 2>(a, s);
-        if (a.e == 0) return launch_vr_ws_t<4, 0, false, 16, 256, 2>(a, s);
-        if (a.e == 1) return launch_vr_ws_t<4, 1, false, 16, 256, 2>(a, s);
-        if (a.e == 2) return launch_vr_ws_t<4, 2, false, 16, 256, 2>(a, s);
-        return false;
-    }
-    if (a.k == 16 && (v == 242 || v == 219) && a.sums_out == nullptr && a.e >= 1) {
-        // round-2 RS(16+4) rebuild instances (4-byte columns, one table per scalar wait)
-        if (a.e == 1) return launch_vr_ws_t<16, 1, false, 8, 256, 1, 4, false, true>(a, s);
-        if (a.e == 2) return launch_vr_ws_t<16, 2, false, 8, 256, 1, 4, false, true>(a, s);
-        if (a.e == 3) return launch_vr_ws_t<16, 3, false, 8, 256, 1, 4, false, true>(a, s);
-        if (a.e == 4) return launch_vr_ws_t<16, 4, false, 8, 256, 1, 4, false, true>(a, s);
-        return false;
-    }
-    if ((v == 242 || v == 232) && a.k == 16 && a.sums_out != nullptr && a.e >= 1) {
-        // round-2 RS(16+4) heal instances: heal 1 with 8-byte columns, heal 2-4 with
-        // 4-byte columns of 128-byte tiles
-        if (a.e == 1) return launch_vr_ws_t<16, 1, true, 8, 256, 1, 8, false, false>(a, s);
-        if (a.e == 2) return launch_vr_ws_t<16, 2, true, 8, 128, 1, 4, false, true, 4>(a, s);
-        if (a.e == 3) return launch_vr_ws_t<16, 3, true, 8, 128, 1, 4, false, true, 4>(a, s);
-        if (a.e == 4) return launch_vr_ws_t<16, 4, true, 8, 128, 1, 4, false, true, 4>(a, s);
-        return false;
-    }
-    if (a.k == 8 && v >= 260 && v <= 263 && a.e >= 1) {
-        // RS(8+4) GET / heal with longer tiles (round 3): 260 / 261 heal on 8 stripes with
-        // 8-byte columns of 384 / 256-byte tiles; 262 heal on 16 stripes, 16-byte columns
-        // of 256-byte tiles; 263 rebuild on 8 stripes, 8-byte columns of 384-byte tiles
-        const bool h = a.sums_out != nullptr;
-        switch (v * 8 + a.e) {
-            case 260 * 8 + 1: return h && launch_vr_ws_t<8, 1, true, 8, 384, 1, 8, false, true, 4>(a, s);
-            case 260 * 8 + 2: return h && launch_vr_ws_t<8, 2, true, 8, 384, 1, 8, false, true, 4>(a, s);
-            case 260 * 8 + 3: return h && launch_vr_ws_t<8, 3, true, 8, 384, 1, 8, false, true, 4>(a, s);
-            case 260 * 8 + 4: return h && launch_vr_ws_t<8, 4, true, 8, 384, 1, 8, false, true, 4>(a, s);
-            case 261 * 8 + 1: return h && launch_vr_ws_t<8, 1, true, 8, 256, 1, 8, false, true, 4>(a, s);
-            case 261 * 8 + 2: return h && launch_vr_ws_t<8, 2, true, 8, 256, 1, 8, false, true, 4>(a, s);
-            case 261 * 8 + 3: return h && launch_vr_ws_t<8, 3, true, 8, 256, 1, 8, false, true, 4>(a, s);
-            case 261 * 8 + 4: return h && launch_vr_ws_t<8, 4, true, 8, 256, 1, 8, false, true, 4>(a, s);
-            case 262 * 8 + 1: return h && launch_vr_ws_t<8, 1, true, 16, 256, 1, 16, false, true, 4>(a, s);
-            case 262 * 8 + 2: return h && launch_vr_ws_t<8, 2, true, 16, 256, 1, 16, false, true, 4>(a, s);
-            case 262 * 8 + 3: return h && launch_vr_ws_t<8, 3, true, 16, 256, 1, 16, false, true, 4>(a, s);
-            case 262 * 8 + 4: return h && launch_vr_ws_t<8, 4, true, 16, 256, 1, 16, false, true, 4>(a, s);
-            case 263 * 8 + 1: return !h && launch_vr_ws_t<8, 1, false, 8, 384, 1, 8, false, true, 4>(a, s);
-            case 263 * 8 + 2: return !h && launch_vr_ws_t<8, 2, false, 8, 384, 1, 8, false, true, 4>(a, s);
-            case 263 * 8 + 3: return !h && launch_vr_ws_t<8, 3, false, 8, 384, 1, 8, false, true, 4>(a, s);
-            case 263 * 8 + 4: return !h && launch_vr_ws_t<8, 4, false, 8, 384, 1, 8, false, true, 4>(a, s);
-            default: return false;
-        }
-    }
-    if (v == 232 && a.k == 8 && a.sums_out != nullptr && a.e >= 3) {
-        // round-2 RS(8+4) heal 3-4 instances: 8-byte columns of 128-byte tiles, two tiles
-        // of survivor prefetch (1.41 / 1.61 ms vs 1.49 / 1.79 unbatched and 2.01 / 2.32 for
-        // the first-generation kernel; profiles/r02/get_ab_bt.jsonl, get_ab_waves.jsonl)
-        if (a.e == 3) return launch_vr_ws_t<8, 3, true, 16, 128, 2, 8, false, true, 4>(a, s);
-        if (a.e == 4) return launch_vr_ws_t<8, 4, true, 16, 128, 2, 8, false, true, 4>(a, s);
-        return false;
-    }
-    if (a.k == 16 && v == 217 && a.sums_out == nullptr) {
-        // twice the rebuild waves (12 waves, 3 per SIMD): 4-byte columns of 256-byte
-        // tiles (8-byte columns of 512-byte tiles spill in the hash role)
-        if (a.e == 1) return launch_vr_ws_t<16, 1, false, 8, 256, 1, 4>(a, s);
-        if (a.e == 2) return launch_vr_ws_t<16, 2, false, 8, 256, 1, 4>(a, s);
-        if (a.e == 3) return launch_vr_ws_t<16, 3, false, 8, 256, 1, 4>(a, s);
-        if (a.e == 4) return launch_vr_ws_t<16, 4, false, 8, 256, 1, 4>(a, s);
-        return false;
-    }
-    if (a.k == 16 && (v == 210 || v == 215 || v == 216)) {
-        // RS(16+4)-shaped GET: 8 stripes, 256-byte tiles; rebuilds with 8-byte columns
-        // (16-byte columns spill: 16 survivors x 2 tiles beside 32-64 generic products).
-        if (a.sums_out != nullptr && v == 216) {
-            // Heal (17..20 hashed rows): 8 stripes per workgroup, pair-form hash waves
-            // padded to whole waves (e.g. heal 2: 288 -> 320 threads) beside 2-4 rebuild
-            // waves with 8-byte columns; e >= 2 reads the rebuild tables with scalar loads
-            // (the VGPR copy spills).  Product default for heal 1 only: 0.535 vs 0.785 ms
-            // (first generation) on 2048 x 1 MiB; heal 2/3/4 measured 0.967/1.31/1.58 vs
-            // 0.946/1.13/1.31 ms (2 rebuild waves are the bound), diagnostics 216
-            // (profiles/r02/get_ab.txt)
-            if (a.e == 1) return launch_vr_ws_t<16, 1, true, 8, 256, 1, 8, false, false>(a, s);
-            if (a.e == 2) return launch_vr_ws_t<16, 2, true, 8, 128, 1, 8, false, false>(a, s);
-            if (a.e == 3) return launch_vr_ws_t<16, 3, true, 8, 128, 1, 8, false, true>(a, s);
-            if (a.e == 4) return launch_vr_ws_t<16, 4, true, 8, 128, 1, 8, false, true>(a, s);
-            return false;
-        }
-        if (a.sums_out != nullptr) {
-            // Heal (18 / 20 hashed rows): 2*8*18 pair-form threads are not whole waves,
-            // so the hash role runs in quad form (padded to 9 / 10 waves) beside 4
-            // rebuild waves.  Measured slower than the first-generation kernel on
-            // 2048 x 1 MiB (heal 2: 1.29 vs 0.95 ms, heal 4: 2.86 vs 1.31 ms; 13 waves
-            // leave 128 VGPRs), so opt-in only (variant 215).
-            if (v == 215) {
-                if (a.e == 2) return launch_vr_ws_t<16, 2, true, 8, 256, 1, 8, true>(a, s);
-                if (a.e == 4) return launch_vr_ws_t<16, 4, true, 8, 256, 1, 8, true>(a, s);
-            }
-            return false;
-        }
-        if (v == 215) return false;
-        if (v == 210) {  // 8-byte rebuild columns (4 rebuild waves), the round-2 first cut
-            if (a.e == 1) return launch_vr_ws_t<16, 1, false, 8, 256, 1, 8>(a, s);
-            if (a.e == 3) return launch_vr_ws_t<16, 3, false, 8, 256, 1, 8>(a, s);
-        }
-        if (v == 216) {  // scalar coefficient tables in the rebuild role
-            if (a.e == 1) return launch_vr_ws_t<16, 1, false, 8, 256, 1, 8, false, true>(a, s);
-            if (a.e == 3) return launch_vr_ws_t<16, 3, false, 8, 256, 1, 8, false, true>(a, s);
-            if (a.e == 2) return launch_vr_ws_t<16, 2, false, 8, 256, 1, 8, false, true>(a, s);
-            if (a.e == 4) return launch_vr_ws_t<16, 4, false, 8, 256, 1, 8, false, true>(a, s);
-            return false;
-        }
-        if (a.e == 0) return launch_vr_ws_t<16, 0, false, 8, 256, 2>(a, s);
-        if (a.e == 2) return launch_vr_ws_t<16, 2, false, 8, 256, 1, 8>(a, s);
-        if (a.e == 4) return launch_vr_ws_t<16, 4, false, 8, 256, 1, 8>(a, s);
-        return false;
-    }
-    if (a.k != 8) return false;
-    if (a.sums_out != nullptr) {
-        // heal (10 hashed rows): 8-byte rebuild columns and 128-byte tiles keep the
-        // 9-wave workgroup inside 168 VGPRs (1.50 -> 1.25 ms, 1 data + 1 parity)
-        // (scalar coefficient tables, variant 216: 1.28 -> 1.18 ms on 4096 x 1 MiB,
-        // profiles/r02/get_ab.txt)
-        if (v == 216 && a.e == 1) return launch_vr_ws_t<8, 1, true, 16, 128, 2, 8, false, true, 4>(a, s);
-        if (a.e != 2) return false;
-        if (v == 216) return launch_vr_ws_t<8, 2, true, 16, 128, 2, 8, false, true, 4>(a, s);
-        if (v == 212) return launch_vr_ws_t<8, 2, true, 16, 128, 2, 8>(a, s);
-        if (v == 213) return launch_vr_ws_t<8, 2, true, 16, 256, 1, 8>(a, s);
-        return false;
-    }
-    switch (v) {
-        case 210:
-            if (a.e == 0) return launch_vr_ws_t<8, 0, false, 16, 256, 2>(a, s);
-            if (a.e == 1) return launch_vr_ws_t<8, 1, false, 16, 256, 2>(a, s);
-            if (a.e == 2) return launch_vr_ws_t<8, 2, false, 16, 256, 2>(a, s);
-            // rebuild 3/4: 8-byte columns (8 rebuild waves, scalar tables): 4096 x 1 MiB
-            // 1.27 / 1.42 ms vs 1.35 / 1.58 with 16-byte columns (get_ab_waves.jsonl);
-            // batched scalar tables: 1.34 vs 1.40 ms for rebuild 4
-            if (a.e == 3) return launch_vr_ws_t<8, 3, false, 16, 256, 1>(a, s);
-            if (a.e == 4) return launch_vr_ws_t<8, 4, false, 16, 256, 1>(a, s);
-            return false;
-        case 211:
-            if (a.e == 0) return launch_vr_ws_t<8, 0, false, 16, 256, 1>(a, s);
-            if (a.e == 2) return launch_vr_ws_t<8, 2, false, 16, 256, 1>(a, s);
-            return false;
-        case 214:  // twice the rebuild waves: 8-byte columns (12 waves, 3 per SIMD);
-                   // e >= 2 with scalar coefficient tables (VGPR tables spill at 168)
-            if (a.e == 1) return launch_vr_ws_t<8, 1, false, 16, 256, 1, 8>(a, s);
-            if (a.e == 2) return launch_vr_ws_t<8, 2, false, 16, 256, 1, 8, false, true>(a, s);
-            if (a.e == 3) return launch_vr_ws_t<8, 3, false, 16, 256, 1, 8, false, true>(a, s);
-            if (a.e == 4) return launch_vr_ws_t<8, 4, false, 16, 256, 1, 8, false, true>(a, s);
-            return false;
-        case 216:
-            if (a.e == 1) return launch_vr_ws_t<8, 1, false, 16, 256, 2, 16, false, true>(a, s);
-            if (a.e == 2) return launch_vr_ws_t<8, 2, false, 16, 256, 2, 16, false, true>(a, s);
-            if (a.e == 3) return launch_vr_ws_t<8, 3, false, 16, 256, 1, 16, false, true>(a, s);
-            if (a.e == 4) return launch_vr_ws_t<8, 4, false, 16, 256, 1, 16, false, true>(a, s);
-            return false;
-        default:
-            return false;
-    }
+    if (a.k == 4) return launch_vr_ws_diag_k4(v, a, s);
+    if (a.k == 8) return launch_vr_ws_diag_k8(v, a, s);
+    if (a.k == 16) return launch_vr_ws_diag_k16(v, a, s);
+    return false;
 }
 #endif
 

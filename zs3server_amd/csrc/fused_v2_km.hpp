@@ -77,6 +77,15 @@ static bool launch_ehx_km(int v, const EncArgs& a, hipStream_t s) {
         case 192: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 3, 0, false, 3>(a, s); else return false;
         case 193: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 0, 0, false, 3>(a, s); else return false;
         case 194: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, true, 2, 0, false, 3>(a, s); else return false;
+        // RS(8+4) mid batches (641-1024 stripes run the first-generation kernel): 4 stripes
+        // per workgroup with quad-form hash waves, as config 2 / RS(16+4) <= 1024
+        case 187: if constexpr (deep) return launch_ws_t<K, M, 4, 512, 1, false, true, 0, false, 0, 0, false, 3>(a, s); else return false;
+        case 188: if constexpr (deep) return launch_ws_t<K, M, 4, 512, 2, false, true, 83968, false, 0, 0, false, 3>(a, s); else return false;
+        case 189: if constexpr (deep) return launch_ws_t<K, M, 4, 1024, 2, false, true, 83968, false, 0, 0, false, 3>(a, s); else return false;
+        // the same with the register budget of 2 waves per SIMD (7-waves workgroups)
+        case 197: if constexpr (deep) return launch_ws_t<K, M, 4, 512, 1, false, true, 83968, false, 0, 0, false, 3, false, 0, 0, false, 2>(a, s); else return false;
+        case 198: if constexpr (deep) return launch_ws_t<K, M, 4, 512, 2, false, true, 83968, false, 0, 0, false, 3, false, 0, 0, false, 2>(a, s); else return false;
+        case 199: if constexpr (deep) return launch_ws_t<K, M, 4, 1024, 2, false, true, 83968, false, 0, 0, false, 3, false, 0, 0, false, 2>(a, s); else return false;
         // config 2 (latency-bound chains): longer tiles = fewer per-step barriers and LDS
         // read latencies on the chain's critical path
         case 177: if constexpr (few) return launch_ws_t<K, M, 4, 1024, 4, false, true, 83968, false, 0, 0, false, 3>(a, s); else return false;

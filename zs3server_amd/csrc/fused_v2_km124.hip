@@ -9,6 +9,9 @@
 //  196: 8 stripes, 8-byte columns of 512-byte tiles: 4 hash + 8 encode waves (1 + 2 per
 //       SIMD), data rows written to LDS before the encode
 //  197: 196 without the early data write
+//  198 / 199: 8 stripes, 16-byte columns of 512-byte tiles: 4 hash + 4 encode waves (one
+//       of each per SIMD), with / without the early data write; 165 / 166 the same with
+//       the 2-waves-per-SIMD register budget (256 VGPRs)
 #include "fused_v2.hpp"
 
 namespace zs3k {
@@ -19,6 +22,10 @@ bool launch_ehx_km_12_4(int v, const EncArgs& a, hipStream_t s) {
         case 195: return launch_ws_t<12, 4, 16, 256, 1, true, false, 0, false, 0, 8, false, 3, false, 0, 0, true>(a, s);
         case 196: return launch_ws_t<12, 4, 8, 512, 1, true, false, 0, false, 0, 8, false, 3, false, 2, 0, true>(a, s);
         case 197: return launch_ws_t<12, 4, 8, 512, 1, true, false, 0, false, 0, 8, false, 3, false, 0, 0, true>(a, s);
+        case 198: return launch_ws_t<12, 4, 8, 512, 1, true, false, 0, false, 0, 16, false, 3, false, 2, 0, true>(a, s);
+        case 199: return launch_ws_t<12, 4, 8, 512, 1, true, false, 0, false, 0, 16, false, 3, false, 0, 0, true>(a, s);
+        case 165: return launch_ws_t<12, 4, 8, 512, 1, true, false, 0, false, 0, 16, false, 3, false, 2, 0, true, 2>(a, s);
+        case 166: return launch_ws_t<12, 4, 8, 512, 1, true, false, 0, false, 0, 16, false, 3, false, 0, 0, true, 2>(a, s);
         default: return false;
     }
 }

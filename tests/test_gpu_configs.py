@@ -82,13 +82,12 @@ def test_config4_per_gpu_share(oracle, nb):
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("nb", [1, 7, 256, 512, 640, 641, 1000, 1024, 1025, 2047, 2048, 2049, 2304, 3001, 4096, 4097,
-                                8192 + 5])
+@pytest.mark.parametrize("nb", [1, 7, 128, 129, 256, 511, 512, 640, 641, 1000, 1024, 1025, 2047, 2048, 2049, 2304,
+                                3001, 4096, 4097, 8192 + 5])
 def test_rs84_batch_sizes_no_cliff(oracle, nb):
     """Every batch size runs a specialised kernel (the launch shape follows the batch:
-    the small-batch latency path up to 640 stripes, first-generation up to 1024,
-    warp-specialised at 8 (1025-2048) or 16 stripes per workgroup above), bit-exact over
-    the whole output."""
+    the small-batch latency path up to 128 stripes, warp-specialised at 4 (129-2048) or
+    16 stripes per workgroup above), bit-exact over the whole output."""
     k, m = 8, 4
     S = MiB // k
     R = k + m
@@ -98,7 +97,7 @@ def test_rs84_batch_sizes_no_cliff(oracle, nb):
     sums = torch.zeros(nb * R * 32, dtype=torch.uint8, device=DEV)
     codec.encode_batch(d, R * S, MiB, nb, parity=d, parity_offset=k * S, parity_stride=R * S, sums=sums)
     torch.cuda.synchronize()
-    assert z.last_path() == (2 if nb > 1024 else 1 if nb > 640 else 4)
+    assert z.last_path() == (2 if nb > 128 else 4)
     digest_check(oracle, k, m, d, sums, nb, S, seed=nb)
     del d, sums
     torch.cuda.empty_cache()

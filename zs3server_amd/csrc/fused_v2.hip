@@ -36,12 +36,10 @@ namespace zs3k {
 //  RS(8+4)  n > 2048:  k_ehx_ws G = 16 (variant 151: 6 pair-form hash waves + 6 encode
 //                      waves with 16-byte columns, encode waves at s_setprio 1, nt policy;
 //                      one workgroup of 12 waves per CU)
-//           1024 < n <= 2048: G = 8 (variant 133: 129-256 workgroups, one per CU, nt
-//                      loads and stores: 2048 stripes 0.737 -> 0.710 ms over variant 130,
-//                      profiles/r02/ab_encode_nt_small.jsonl)
-//           n <= 1024: PATH_NONE -> the first-generation kernel (4 stripes per
-//                      workgroup, quad-form hash lanes: more threads per stripe when
-//                      there are too few stripes to fill 256 CUs with 8 each)
+//           128 < n <= 2048: G = 4 with quad-form hash waves, 1 KiB tiles, two tiles
+//                      of prefetch, 256-VGPR budget (variant 199, round 3; replaced the
+//                      8-stripe kernel above 1024 and the first-generation kernel
+//                      below); n <= 128: the small-batch latency path (kernels.hip)
 //  RS(16+4) n > 1024:  k_ehx_ws G = 8 (variant 162: 5 pair-form hash waves + 6 encode
 //                      waves with 8-byte buffer-addressed columns, nt policy, data rows
 //                      written to LDS before the encode (EP = 2): 0.577 -> 0.590 of HBM
@@ -58,8 +56,15 @@ static int launch_ehx_default(const EncArgs& a, hipStream_t s) {
     if constexpr (K == 8 && M == 4) {
         if (n > 2048)
             return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3>(a, s) ? PATH_WS : PATH_NONE;
-        if (n > 1024)
-            return launch_ws_t<K, M, 8, 384, 1, false, false, 0, false, 1, 0, false, 3>(a, s) ? PATH_WS : PATH_NONE;
+        // up to 2048 stripes (round 3, variant 199): 4 stripes per workgroup, quad-form
+        // hash waves (3) beside 4 encode waves, 1 KiB tiles, two tiles of prefetch, and
+        // the 2-waves-per-SIMD register budget (7-wave workgroups: no spills, where the
+        // 168-VGPR budget spilled 26): 256 / 512 / 640 / 1024 / 1536 / 2048 stripes
+        // 0.275 / 0.285 / 0.281 / 0.336 / 0.611 / 0.676 ms vs 0.32 / 0.42 / 0.47 / 0.555 /
+        // 0.684 / 0.73-0.78 for the latency path, first-generation and 8-stripe kernels
+        // (profiles/r03/ab_rs84_mid_batches.jsonl, sweep_rs84_sizes199.jsonl)
+        return launch_ws_t<K, M, 4, 1024, 2, false, true, 83968, false, 0, 0, false, 3, false, 0, 0, false, 2>(a, s)
+                   ? PATH_WS : PATH_NONE;
     } else if constexpr (K == 16 && M == 4) {
         if (n > 4 * 256)
             return launch_ws_t<K, M, 8, 384, 1, true, false, 0, false, 0, 0, false, 3, false, 2>(a, s) ? PATH_WS : PATH_NONE;

@@ -7,17 +7,14 @@ namespace zs3k {
 
 #if ZS3_DIAG
 bool launch_vr_ws_diag_k16(int v, const VrArgs& a, hipStream_t s) {
+    // survivor prefetch depth / tile length / column width candidates (round 3); the
+    // rejected ones (251-255, 257: 8-45 % slower, profiles/r03/get_ab_rs164_vr16.jsonl)
+    // are no longer compiled; 250 / 256 / 259 became the product instances
     if (a.k == 16 && v >= 250 && v <= 259 && a.e >= 1) {
         const bool h = a.sums_out != nullptr;
         switch (v) {
             case 250: return h ? vr16<128, 2, true, 4>(a, s) : vr16<256, 2, false, 0>(a, s);
-            case 251: return h ? vr16<128, 3, true, 0>(a, s) : vr16<128, 3, false, 4>(a, s);
-            case 252: return h ? vr16<256, 2, true, 4>(a, s) : vr16<256, 3, false, 0>(a, s);
-            case 253: return h ? vr16<256, 1, true, 4>(a, s) : vr16<512, 1, false, 0>(a, s);
-            case 254: return h ? vr16<128, 3, true, 4>(a, s) : vr16<128, 2, false, 0>(a, s);
-            case 255: return h ? vr16<256, 2, true, 0>(a, s) : vr16<256, 2, false, 4>(a, s);
             case 256: return h ? vr16<256, 1, true, 4, 8>(a, s) : vr16<512, 1, false, 4, 8>(a, s);
-            case 257: return h ? vr16<512, 1, true, 4, 8>(a, s) : vr16<256, 2, false, 4, 8>(a, s);
             case 259: return h ? vr16<384, 1, true, 4, 8>(a, s) : vr16<384, 1, false, 4, 8>(a, s);
             default: return false;
         }

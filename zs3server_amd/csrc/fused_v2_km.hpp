@@ -50,6 +50,10 @@ static bool launch_ehx_km(int v, const EncArgs& a, hipStream_t s) {
         case 117: if constexpr (few) return launch_ws_t<K, M, 4, 512, 4, false, true, 83968, false, 0, 0, false, 3>(a, s); else return false;
         case 133: if constexpr (deep) return launch_ws_t<K, M, 8, 384, 1, false, false, 0, false, 1, 0, false, 3>(a, s); else return false;
         case 125: if constexpr (K == 16 && M == 4) return launch_ws_t<K, M, 4, 512, 1, true, true, 0, false, 0, 0, false, 3>(a, s); else return false;
+        // RS(16+4) small batches with 16-byte columns on 7-wave workgroups (2 waves per
+        // SIMD's register budget), two / one tile of prefetch
+        case 126: if constexpr (K == 16 && M == 4) return launch_ws_t<K, M, 4, 512, 2, true, true, 83968, false, 0, 16, false, 3, false, 0, 0, false, 2>(a, s); else return false;
+        case 127: if constexpr (K == 16 && M == 4) return launch_ws_t<K, M, 4, 512, 1, true, true, 83968, false, 0, 16, false, 3, false, 0, 0, false, 2>(a, s); else return false;
         case 156: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 1>(a, s); else return false;
         case 157: if constexpr (few) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 1>(a, s); else return false;
         case 160: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 2>(a, s); else return false;

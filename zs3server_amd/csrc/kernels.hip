@@ -686,6 +686,9 @@ template <int K, int M>
 static bool small_batch(int64_t n_blocks, int64_t S) {
     if (K == 4 && M == 2) return false;
     if (K == 16 && M == 4) return n_blocks < 512;
+    // RS(8+4): the 4-stripe fused kernel wins from ~256 stripes of 128 KiB shards (round 3:
+    // 0.275 vs 0.32 ms at 256, 0.272 vs 0.269 at 128; profiles/r03/sweep_rs84_sizes199.jsonl)
+    if (K == 8 && M == 4) return n_blocks * S <= (int64_t)128 * 131072;
     return n_blocks * (K + M) * S <= (int64_t)640 * 12 * 131072;
 }
 

@@ -18,7 +18,7 @@ echo "=== pmc WRITE_SIZE"
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmcw -o p --output-format csv -- \
     python bench.py --steps 3 --warmup 1 --no-cpu > $OUT/pmcw.log 2>&1 || { tail -5 $OUT/pmcw.log; exit 7; }
 python scripts/pmc_traffic.py $(find $OUT/pmcf -name '*counter_collection.csv' | head -1) \
-    $(find $OUT/pmcw -name '*counter_collection.csv' | head -1) $P/pmc_traffic.json
+    $(find $OUT/pmcw -name '*counter_collection.csv' | head -1) $P/pmc_traffic.json 65536
 echo "=== pmc VALU"
 timeout -k 10 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_LDS \
     -d $OUT/pmcv -o p --output-format csv -- \

@@ -70,7 +70,9 @@ def encoded(k, m, nobj, seed):
 if "encode" in PATHS:
     for k, m, nobj, label in ((4, 2, 1024, "config 2: RS(4+2) 1024 x 1 MiB"),
                               (8, 4, 4096, "config 3: RS(8+4) 4096 x 1 MiB"),
-                              (16, 4, 2048, "RS(16+4) 2048 x 1 MiB")):
+                              (16, 4, 2048, "RS(16+4) 2048 x 1 MiB"),
+                              (12, 4, 4096, "RS(12+4) 4096 x 1 MiB (16-drive default)"),
+                              (4, 4, 4096, "RS(4+4) 4096 x 1 MiB (8-drive default)")):
         codec, buf, sums, S, stride = encoded(k, m, nobj, 1)
         ms = timeit(lambda: codec.encode_batch(buf, stride, MiB, nobj, parity=buf, parity_offset=k * S,
                                                parity_stride=stride, sums=sums))
@@ -103,7 +105,9 @@ if "get" in PATHS:
             (4, 2, 2048, (([], True, False), ([1], True, False), ([0, 3], True, False), ([0, 5], False, True))),
             (16, 4, 2048, (([], True, False), ([6], True, False), ([0, 5], True, False), ([1, 7, 15], True, False),
                            ([0, 5, 9, 14], True, False), ([5], False, True), ([3, 17], False, True),
-                           ([0, 1, 16, 19], False, True)))):
+                           ([0, 1, 16, 19], False, True))),
+            (12, 4, 4096, (([], True, False), ([0, 5], True, False), ([1, 12], False, True))),
+            (4, 4, 4096, (([], True, False), ([0, 1], True, False), ([1, 4], False, True)))):
         codec, buf, sums, S, stride = encoded(k, m, nobj, 5)
         R = k + m
         vbad = torch.empty(nobj * R, dtype=torch.int32, device="cuda")

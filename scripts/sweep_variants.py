@@ -18,9 +18,11 @@ steps = int(os.environ.get("SWEEP_STEPS", "10"))
 # SWEEP_ALIAS=1: every block reads stripe 0 and writes stripe 0's parity (strides 0), so
 # the data stays in L2 and the launch measures the kernel's compute-bound time.
 ALIAS = os.environ.get("SWEEP_ALIAS", "0") == "1"
+# SWEEP_BLEN: block length (default 1 MiB); e.g. 12 * 87392 gives RS(12+4) 16-byte-aligned rows
+BLEN = int(os.environ.get("SWEEP_BLEN", str(1 << 20)))
 res = []
 for k, m, nobj in SHAPES:
-    blen = 1 << 20
+    blen = BLEN
     S = -(-blen // k)  # reedsolomon shard size (ceil)
     stride = (k + m) * S
     codec = z.Codec(k, m)
@@ -50,7 +52,8 @@ for k, m, nobj in SHAPES:
         ms = e0.elapsed_time(e1) / steps
         ab = nobj * (blen + m * S + 32 * (k + m))
         r = {"k": k, "m": m, "objects": nobj, "variant": v, "ms": round(ms, 4),
-             "GiBps": round(nobj * blen / ms / 1e-3 / 2**30, 1), "hbm_GBps": round(ab / ms / 1e6, 1), "match": ok, "alias": ALIAS}
+             "GiBps": round(nobj * blen / ms / 1e-3 / 2**30, 1), "hbm_GBps": round(ab / ms / 1e6, 1), "match": ok, "alias": ALIAS,
+             "blen": blen, "S": S, "path": z.last_path()}
         print(json.dumps(r), flush=True)
         res.append(r)
         ctx.__exit__(None, None, None)

@@ -238,7 +238,7 @@ def test_masks_on_ws_kernel(oracle, k, m, blen, heal):
         assert bool(eq[ok][lost[ok]].all()), "heal sums of the rebuilt rows"
 
 
-@pytest.mark.parametrize("k,m,nb", [(12, 4, 4096), (12, 4, 1024), (12, 4, 5), (4, 4, 4096), (4, 4, 1024), (4, 4, 3)])
+@pytest.mark.parametrize("k,m,nb", [(12, 4, 4096), (12, 4, 2051), (12, 4, 1025), (12, 4, 1024), (12, 4, 5), (4, 4, 4096), (4, 4, 1024), (4, 4, 3)])
 def test_server_default_geometries(oracle, k, m, nb):
     """The server's default erasure geometries (getDefaultParityBlocks,
     cmd/format-erasure.go:870-881): RS(12+4) for 16-drive sets (1 MiB blocks: S = 87 382,

@@ -79,6 +79,16 @@ def test_other_shapes_variants(oracle, variant, k, m, blen):
     run_case(oracle, k, m, blen, 3, variant, seed=k + m)
 
 
+# RS(12+4) on blocks whose shard rows are not 16-byte aligned (1 MiB: S = 87 382) runs
+# k_ehx_ws in UA mode; the diagnostics variants reach it since round 3 (fused_v2_km124.hip)
+@pytest.mark.parametrize("variant", [0, 175, 176, 177, 178, 179, 180, 181, 195, 196, 197, 198, 199, 165, 166])
+@pytest.mark.parametrize("blen,nb", [(1 << 20, 3), (1 << 20, 9), (12 * (512 * 3 + 100) - 6, 17)])
+def test_rs124_ua_variants(oracle, variant, blen, nb):
+    with variant_ctx(variant):
+        _run_case(oracle, 12, 4, blen, nb, variant, seed=nb)
+        assert z.last_path() == 2, z.last_path()  # the warp-specialised kernel, not a fallback
+
+
 def test_variants_are_per_thread(oracle):
     """The diagnostics build's variant selection is thread-local (no process-wide tuning
     state): two threads encode concurrently with different variants — and a third on

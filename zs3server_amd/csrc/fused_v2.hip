@@ -99,8 +99,15 @@ static int launch_ehx_default(const EncArgs& a, hipStream_t s) {
 
 int launch_ehx_ua(const EncArgs& a, hipStream_t s) {
     if (a.k == 12 && a.m == 4) {
+        // n > 1024 (round 3, diagnostics 179): 8 stripes of 8-byte columns of 512-byte
+        // tiles (4 hash + 8 encode waves: one hash and two encode waves on every SIMD,
+        // where 384-byte tiles left two SIMDs with one encode wave), data rows written to
+        // LDS before the encode, and the hash waves touching every line of the data rows
+        // two tiles ahead (PFD = 2) so the unaligned row loads of the encode waves hit L2:
+        // 4096 / 16384 x 1 MiB 1.72-1.79 / 6.72 -> 1.41 / 5.48 ms
+        // (profiles/r03/ab_rs124_pfd.jsonl; 196 = no prefetch 1.54-1.59 / 5.98-6.01)
         if (a.n_blocks > 4 * 256)
-            return launch_ws_t<12, 4, 8, 384, 1, true, false, 0, false, 0, 0, false, 3, false, 2, 0, true>(a, s)
+            return launch_ws_t<12, 4, 8, 512, 1, true, false, 0, false, 0, 8, false, 3, false, 2, 2, true>(a, s)
                        ? PATH_WS : PATH_NONE;
         return launch_ws_t<12, 4, 4, 512, 1, true, true, 0, false, 0, 0, false, 3, false, 0, 0, true>(a, s)
                    ? PATH_WS : PATH_NONE;

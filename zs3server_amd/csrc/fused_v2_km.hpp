@@ -98,6 +98,9 @@ static bool launch_ehx_km(int v, const EncArgs& a, hipStream_t s) {
         case 176: if constexpr (few) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 0, 3>(a, s); else return false;
         case 168: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 8>(a, s); else return false;
         case 169: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 9>(a, s); else return false;
+        // RS(16+4) product 162 + L2 prefetch by the hash waves 2 / 3 tiles ahead (round 3)
+        case 158: if constexpr (K == 16 && M == 4) return launch_ws_t<K, M, 8, 384, 1, true, false, 0, false, 0, 0, false, 3, false, 2, 2>(a, s); else return false;
+        case 159: if constexpr (K == 16 && M == 4) return launch_ws_t<K, M, 8, 384, 1, true, false, 0, false, 0, 0, false, 3, false, 2, 3>(a, s); else return false;
         case 162: if constexpr (K == 16 && M == 4) return launch_ws_t<K, M, 8, 384, 1, true, false, 0, false, 0, 0, false, 3, false, 2>(a, s); else return false;
         case 152: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 2, false, false, 0, false, 1>(a, s); else return false;
         case 140: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, true>(a, s); else return false;

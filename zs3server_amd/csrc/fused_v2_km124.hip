@@ -12,6 +12,12 @@
 //  198 / 199: 8 stripes, 16-byte columns of 512-byte tiles: 4 hash + 4 encode waves (one
 //       of each per SIMD), with / without the early data write; 165 / 166 the same with
 //       the 2-waves-per-SIMD register budget (256 VGPRs)
+//  (195-199 / 165-166 first ran in session 3 of round 3: before that, launch_encode sent
+//  every non-zero variant with unaligned rows to the any-geometry kernels)
+//  175 / 176: the product instance + L2 prefetch by the hash waves, 2 / 3 tiles ahead
+//  177: the product instance with two tiles of register prefetch
+//  179 / 180 / 181: 196 + L2 prefetch by the hash waves, 2 / 3 / 1 tiles ahead
+//  178: 16 stripes, 16-byte columns of 256-byte tiles: 8 hash + 4 encode waves (2 + 1 per SIMD)
 #include "fused_v2.hpp"
 
 namespace zs3k {
@@ -19,6 +25,13 @@ namespace zs3k {
 #if ZS3_DIAG
 bool launch_ehx_km_12_4(int v, const EncArgs& a, hipStream_t s) {
     switch (v) {
+        case 175: return launch_ws_t<12, 4, 8, 384, 1, true, false, 0, false, 0, 0, false, 3, false, 2, 2, true>(a, s);
+        case 176: return launch_ws_t<12, 4, 8, 384, 1, true, false, 0, false, 0, 0, false, 3, false, 2, 3, true>(a, s);
+        case 177: return launch_ws_t<12, 4, 8, 384, 2, true, false, 0, false, 0, 0, false, 3, false, 2, 0, true>(a, s);
+        case 178: return launch_ws_t<12, 4, 16, 256, 1, true, false, 0, false, 0, 16, false, 3, false, 2, 0, true>(a, s);
+        case 179: return launch_ws_t<12, 4, 8, 512, 1, true, false, 0, false, 0, 8, false, 3, false, 2, 2, true>(a, s);
+        case 180: return launch_ws_t<12, 4, 8, 512, 1, true, false, 0, false, 0, 8, false, 3, false, 2, 3, true>(a, s);
+        case 181: return launch_ws_t<12, 4, 8, 512, 1, true, false, 0, false, 0, 8, false, 3, false, 2, 1, true>(a, s);
         case 195: return launch_ws_t<12, 4, 16, 256, 1, true, false, 0, false, 0, 8, false, 3, false, 0, 0, true>(a, s);
         case 196: return launch_ws_t<12, 4, 8, 512, 1, true, false, 0, false, 0, 8, false, 3, false, 2, 0, true>(a, s);
         case 197: return launch_ws_t<12, 4, 8, 512, 1, true, false, 0, false, 0, 8, false, 3, false, 0, 0, true>(a, s);

@@ -86,7 +86,8 @@ if "encode" in PATHS:
 # ---- reconstruct (ReconstructData / Reconstruct), BASELINE config 3 and RS(16+4)
 if "rec" in PATHS:
     for k, m, nobj, cases in ((8, 4, 4096, (([0, 5], True), ([2, 10], False))),
-                              (16, 4, 2048, (([0, 5], True), ([0, 5, 9, 14], True), ([3, 17], False)))):
+                              (16, 4, 2048, (([0, 5], True), ([0, 5, 9, 14], True), ([3, 17], False))),
+                              (12, 4, 4096, (([0, 5], True), ([1, 13], False)))):
         codec, buf, sums, S, stride = encoded(k, m, nobj, 3)
         for erased, data_only in cases:
             pres = [i not in erased for i in range(k + m)]

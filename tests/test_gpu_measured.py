@@ -360,3 +360,34 @@ def test_any_geometry_get_heal(oracle, k, m, erased, heal):
                 assert bool((sv == refs[None, :, i, :]).all(dim=2)[okv].all()), f"heal sum {i}"
         else:
             assert bool((dv[:, :, i, :] == 0x5A).all())
+    for i in range(R):  # nothing written outside the rebuilt rows (ragged last column)
+        if i not in erased:
+            assert bool((dv[:, :, i, :] == ref[None, :, i, :]).all(dim=2)[okv].all()), f"survivor {i}"
+
+
+@pytest.mark.parametrize("k,m,blen,erased,data_only", [
+    (12, 4, MiB, [0, 5], True), (12, 4, MiB, [1, 13, 14, 15], False), (12, 4, MiB, [0, 1, 2, 3], True),
+    (10, 6, MiB, [0, 1, 2, 3], True), (6, 3, MiB, [2, 7], False), (5, 4, MiB, [4], True),
+    (4, 2, MiB + 7, [0, 5], False), (8, 4, 8 * 1000 + 3, [3, 9, 10], False), (2, 1, 21, [0], True)],
+    ids=lambda v: str(v))
+def test_reconstruct_unaligned_rows(oracle, k, m, blen, erased, data_only):
+    """ReconstructData / Reconstruct at shard sizes that are not a multiple of 16 (1 MiB
+    blocks of RS(12+4), RS(10+6), RS(5+4); ragged block lengths): the specialised
+    reconstruct kernel with unaligned rows and a byte-wise last column, every byte of
+    every block vs the oracle's encode (rows outside the rebuilt ones untouched)."""
+    R = k + m
+    nb = 9
+    S = -(-blen // k)
+    mat = oracle.build_matrix(k, m)
+    base = np.stack([oracle.encode_data(k, m, oracle.fill(41, b, blen), mat).reshape(R, S) for b in range(nb)])
+    d = torch.from_numpy(base).to(DEV).contiguous()
+    for e in erased:
+        d[:, e, :] = 0xA5
+    z.Codec(k, m, MiB).reconstruct_batch(d, R * S, S, nb, [i not in erased for i in range(R)], data_only)
+    torch.cuda.synchronize()
+    got = d.cpu().numpy()
+    for i in range(R):
+        if i in erased and i >= k and data_only:
+            assert (got[:, i, :] == 0xA5).all(), f"row {i} written"
+        else:
+            assert np.array_equal(got[:, i, :], base[:, i, :]), f"row {i}"

@@ -706,8 +706,13 @@ static void launch_encode_lat(const EncArgs& a, hipStream_t s) {
 // Reconstruct: E_MAX output rows, each a GF combination of the K valid rows.
 // NTP: non-temporal survivor loads and rebuilt-row stores (launch: S % 16 == 0 and a
 // 16-byte aligned base, so every access is aligned).
-template <int K, int EMAX, int NC = 1, bool NTP = false>
+// UA (round 3): S need not be a multiple of 16 (RS(12+4) / RS(10+6) / RS(5+4) ... on
+// 1 MiB blocks): full columns use the same 16-byte accesses at the rows' byte offsets
+// (unaligned-access mode), the ragged last column is read byte by byte (bytes past the
+// row read as zero) and only its bytes below S are stored.
+template <int K, int EMAX, int NC = 1, bool NTP = false, bool UA = false>
 __global__ void __launch_bounds__(256) k_reconstruct(RecArgs a) {
+    static_assert(!UA || (NC == 1 && !NTP), "unaligned rows: one column per thread, plain accesses");
     // NC columns per thread (256 apart, so every load instruction stays coalesced): all
     // NC*K survivor loads are issued before the first product (more bytes in flight).
     __shared__ __attribute__((aligned(16))) uint32_t tabs[EMAX * K * 8];
@@ -727,6 +732,17 @@ __global__ void __launch_bounds__(256) k_reconstruct(RecArgs a) {
             for (int i = 0; i < NC; ++i) {
                 const int64_t c = c0 + 256 * i;
                 const int64_t o = (c < cols ? c : c0) * 16;
+                if (UA && c == cols - 1 && (S & 15)) {
+                    const int nv = (int)(S & 15);
+#pragma unroll
+                    for (int t = 0; t < K; ++t) {
+                        const uint8_t* p = blk + (int64_t)rows[t] * S + o;
+                        uint32_t w[4] = {0, 0, 0, 0};
+                        for (int q = 0; q < nv; ++q) w[q >> 2] |= (uint32_t)p[q] << (8 * (q & 3));
+                        x[i][t] = make_uint4(w[0], w[1], w[2], w[3]);
+                    }
+                    continue;
+                }
 #pragma unroll
                 for (int t = 0; t < K; ++t)
                     x[i][t] = NTP ? ld16_nt(blk + (int64_t)rows[t] * S + o) : ld16(blk + (int64_t)rows[t] * S + o);
@@ -761,10 +777,15 @@ __global__ void __launch_bounds__(256) k_reconstruct(RecArgs a) {
                     if (r < E) {
                         const uint4 p = make_uint4(acc_done(acc[r][0]), acc_done(acc[r][1]),
                                                    acc_done(acc[r][2]), acc_done(acc[r][3]));
-                        if (NTP)
-                            st16_nt(blk + (int64_t)rows[K + r] * S + o, p);
-                        else
-                            st16(blk + (int64_t)rows[K + r] * S + o, p);
+                        uint8_t* dst = blk + (int64_t)rows[K + r] * S + o;
+                        if (UA && c == cols - 1 && (S & 15)) {
+                            const uint32_t w[4] = {p.x, p.y, p.z, p.w};
+                            for (int q = 0; q < (int)(S & 15); ++q) dst[q] = (uint8_t)(w[q >> 2] >> (8 * (q & 3)));
+                        } else if (NTP) {
+                            st16_nt(dst, p);
+                        } else {
+                            st16(dst, p);
+                        }
                     }
                 }
             }
@@ -1606,6 +1627,18 @@ static hipError_t run_rec_fast(const RecArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
+template <int K>
+static hipError_t run_rec_ua(const RecArgs& a, hipStream_t s) {
+    const int64_t cols = (a.S + 15) >> 4;
+    const unsigned gx = (unsigned)((cols + 255) / 256);
+    const unsigned gy = (unsigned)(a.n_blocks < 65535 ? a.n_blocks : 65535);
+    if (a.e <= 2)
+        hipLaunchKernelGGL((k_reconstruct<K, 2, 1, false, true>), dim3(gx, gy), dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL((k_reconstruct<K, 4, 1, false, true>), dim3(gx, gy), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_reconstruct(const RecArgs& a, hipStream_t s, int* path) {
     if (path) *path = PATH_NONE;
     if (a.n_blocks <= 0 || a.S <= 0 || a.e <= 0) return hipSuccess;
@@ -1621,6 +1654,24 @@ hipError_t launch_reconstruct(const RecArgs& a, hipStream_t s, int* path) {
             case 10: return run_rec_fast<10>(a, s);
             case 12: return run_rec_fast<12>(a, s);
             case 16: return run_rec_fast<16>(a, s);
+            default: break;
+        }
+    }
+    // unaligned shard sizes (1 MiB blocks of RS(12+4), RS(10+6), RS(5+4), ...): the same
+    // specialised kernel with unaligned 16-byte accesses and a byte-wise last column
+    // (diagnostics 97 keeps the any-geometry kernel reachable)
+    if (a.e <= 4 && a.S >= 16 && !(ZS3_DIAG && a.variant == 97)) {
+        if (path) *path = PATH_FIRSTGEN;
+        switch (a.k) {
+            case 2: return run_rec_ua<2>(a, s);
+            case 3: return run_rec_ua<3>(a, s);
+            case 4: return run_rec_ua<4>(a, s);
+            case 5: return run_rec_ua<5>(a, s);
+            case 6: return run_rec_ua<6>(a, s);
+            case 8: return run_rec_ua<8>(a, s);
+            case 10: return run_rec_ua<10>(a, s);
+            case 12: return run_rec_ua<12>(a, s);
+            case 16: return run_rec_ua<16>(a, s);
             default: break;
         }
     }

@@ -189,7 +189,7 @@ def test_constant_input_batches(oracle, k, m, nb, fillv):
     assert bool((d == wt[None]).all()), "reconstruct round trip"
 
 
-@pytest.mark.parametrize("k,m,blen", [(8, 4, 1 << 16), (16, 4, 1 << 16)])
+@pytest.mark.parametrize("k,m,blen", [(8, 4, 1 << 16), (16, 4, 1 << 16), (12, 4, 12 * 5000 + 6)])
 @pytest.mark.parametrize("heal", [False, True])
 def test_masks_on_ws_kernel(oracle, k, m, blen, heal):
     """Per-block patterns whose groups exceed the small-batch path (> 2 048 blocks per
@@ -319,13 +319,17 @@ def test_any_geometry_encode(oracle, k, m, nb):
 
 
 @pytest.mark.parametrize("k,m,erased,heal", [(12, 4, [0, 5], False), (12, 4, [3, 13], True),
-                                             (12, 4, [0, 1, 2, 15], True), (11, 5, [1, 4, 12], True),
+                                             (12, 4, [0, 1, 2, 15], True), (12, 4, [], False), (12, 4, [7], False),
+                                             (12, 4, [2, 9, 14], False), (12, 4, [1, 2, 3, 4], False),
+                                             (12, 4, [6], True), (12, 4, [0, 11, 12], True),
+                                             (11, 5, [1, 4, 12], True),
                                              (10, 6, [0, 9], False), (5, 4, [4, 5, 6, 7], True)])
 def test_any_geometry_get_heal(oracle, k, m, erased, heal):
-    """GET / heal on the geometries without a warp-specialised instance (unaligned
-    shard sizes on 1 MiB blocks): survivors verified in one stripe-mode hash launch,
-    the any-geometry rebuild, rebuilt rows hashed in one launch; one rotted survivor
-    flagged exactly; 512 stripes of 64 distinct oracle stripes."""
+    """GET / heal at unaligned shard sizes on 1 MiB blocks: RS(12+4) (S = 87 382) on the
+    warp-specialised kernel in UA mode (round 3), the other geometries as survivors
+    verified in one stripe-mode hash launch, the rebuild, rebuilt rows hashed in one
+    launch; one rotted survivor flagged exactly; 512 stripes of 64 distinct oracle
+    stripes."""
     R = k + m
     nb = 512
     base, bsum, reps = _tiled_stripes(oracle, k, m, MiB, nb, seed=31)
@@ -343,6 +347,8 @@ def test_any_geometry_get_heal(oracle, k, m, erased, heal):
     codec.verify_reconstruct_batch(d, R * S, S, nb, [i not in erased for i in range(R)], not heal, exp, bad,
                                    sums_out=out)
     torch.cuda.synchronize()
+    if k == 12 and 1 <= len(erased) <= 4:
+        assert z.last_path() == 2, z.last_path()
     want_bad = np.zeros((nb, R), np.int32)
     want_bad[bad_blk, bad_row] = 1
     assert np.array_equal(bad.cpu().numpy(), want_bad)

@@ -1025,8 +1025,13 @@ constexpr int vr_nh() {
 // while batch i's 4 products are computed.  (Scalar loads return out of order, so every
 // wait is lgkmcnt(0); one table per wait serialises the rebuild on scalar-cache latency.)
 // NTL: non-temporal survivor loads and rebuilt-row stores.
+// UA (round 3): S need not be a multiple of 16 (RS(12+4) on 1 MiB blocks: S = 87 382,
+// rows 2-byte aligned).  Full tiles use the same vector accesses at the rows' byte
+// offsets (unaligned-access mode); the ragged tail tile is never prefetched: each lane
+// reads its columns of it byte by byte (zero past the row) and stores only the rebuilt
+// bytes below S.
 template <int K, int EX, bool HOUT, int G, int T, int PF, int CW = 16, bool HQ = false, bool ST = false,
-          int BT = 0, bool NTL = false>
+          int BT = 0, bool NTL = false, bool UA = false>
 __global__ void __launch_bounds__((vr_nh<G, K + (HOUT ? EX : 0), HQ>() + G * (T / CW))) __attribute__((amdgpu_waves_per_eu(2)))
 k_vr_ws(VrArgs a) {
     constexpr int RH = K + (HOUT ? EX : 0);
@@ -1181,8 +1186,30 @@ k_vr_ws(VrArgs a) {
         }
     };
     auto prefetch_any = [&](VT (&xs)[K], int64_t tn) {
-        const bool ok = tn < nfull || (tn == nfull && o < tail);
+        const bool ok = tn < nfull || (!UA && tn == nfull && o < tail);
         load(xs, ok ? tn * T : 0);
+    };
+    // UA tail tile: bytes [o, o + CW) of every survivor row, zero past the row
+    auto tail_cols = [&](VT (&xs)[K]) {
+        const uint8_t* t0p = blk + nfull * T;
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            uint32_t w[NWd];
+#pragma unroll
+            for (int q = 0; q < NWd; ++q) {
+                uint32_t v = 0;
+#pragma unroll
+                for (int bb = 0; bb < 4; ++bb)
+                    if (o + 4 * q + bb < tail) v |= (uint32_t)t0p[roff[j] + 4 * q + bb] << (8 * bb);
+                w[q] = v;
+            }
+            if constexpr (NWd == 1) {
+                xs[j] = w[0];
+            } else {
+#pragma unroll
+                for (int q = 0; q < NWd; ++q) xs[j][q] = w[q];
+            }
+        }
     };
     // survivors to LDS, rebuilt rows into y (and LDS when hashed)
     auto rebuild = [&](VT (&xr)[K], uint8_t* tl, Col<NWd> (&y)[EX > 0 ? EX : 1]) {
@@ -1269,13 +1296,31 @@ k_vr_ws(VrArgs a) {
         store_rows(y, ti * T);
         lds_barrier2();
     };
+    auto store_tail = [&](const Col<NWd> (&y)[EX > 0 ? EX : 1]) {
+        uint8_t* t0p = blk + nfull * T;
+#pragma unroll
+        for (int r = 0; r < EX; ++r)
+#pragma unroll
+            for (int q = 0; q < NWd; ++q)
+#pragma unroll
+                for (int bb = 0; bb < 4; ++bb)
+                    if (o + 4 * q + bb < tail) t0p[ooff[r] + 4 * q + bb] = (uint8_t)(y[r].w[q] >> (8 * bb));
+    };
     auto edge = [&](VT (&xs)[K], int64_t ti) {
         const bool full = ti < nfull, part = ti == nfull && tail;
         vm_wait<0>(xs);
         Col<NWd> y[EX > 0 ? EX : 1];
+        if constexpr (UA) {
+            if (part) tail_cols(xs);
+        }
         if (full || part) rebuild(xs, tile[ti & 1], y);
         prefetch_any(xs, ti + PF);
-        if (full || (part && o < tail)) store_rows(y, ti * T);
+        if constexpr (UA) {
+            if (full) store_rows(y, ti * T);
+            else if (part && o < tail) store_tail(y);
+        } else {
+            if (full || (part && o < tail)) store_rows(y, ti * T);
+        }
         lds_barrier2();
     };
 #pragma unroll
@@ -1297,28 +1342,33 @@ k_vr_ws(VrArgs a) {
     for (int p = 0; p < PF; ++p) vm_wait<0>(x[p]);
 }
 
-template <int K, int EX, bool HOUT, int G, int T, int PF, int CW, bool HQ, bool ST, int BT, bool NTL = false>
+template <int K, int EX, bool HOUT, int G, int T, int PF, int CW, bool HQ, bool ST, int BT, bool NTL = false,
+          bool UA = false>
 static bool launch_vr_ws_bt(const VrArgs& a, hipStream_t s);
 
 template <int K, int EX, bool HOUT, int G, int T, int PF, int CW = 16, bool HQ = false, bool ST = false,
-          int BT = 0>
+          int BT = 0, bool UA = false>
 static bool launch_vr_ws_t(const VrArgs& a, hipStream_t s) {
-    // diagnostics 240: the same launch with the scalar-table batching flipped (off <-> 4
-    // coefficients per batch); 241: batches of 2
-    if constexpr (ZS3_DIAG && ST) {
-        if (a.variant == 240) return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, (BT ? 0 : 4), true>(a, s);
-        if (a.variant == 241) return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, 2, true>(a, s);
+    if constexpr (UA) {
+        return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, BT, true, true>(a, s);
+    } else {
+        // diagnostics 240: the same launch with the scalar-table batching flipped (off <-> 4
+        // coefficients per batch); 241: batches of 2
+        if constexpr (ZS3_DIAG && ST) {
+            if (a.variant == 240) return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, (BT ? 0 : 4), true>(a, s);
+            if (a.variant == 241) return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, 2, true>(a, s);
+        }
+        // Survivor loads and rebuilt-row stores are non-temporal (each byte is touched once):
+        // RS(8+4) verify 0.706 -> 0.627 ms, RS(16+4) verify 0.386 -> 0.351, rebuild 1-4 and
+        // heals 1-5 % faster (profiles/r02/ab_get_nt.jsonl).  Diagnostics 246: plain loads.
+        if constexpr (ZS3_DIAG) {
+            if (a.variant == 246) return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, BT, false>(a, s);
+        }
+        return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, BT, true>(a, s);
     }
-    // Survivor loads and rebuilt-row stores are non-temporal (each byte is touched once):
-    // RS(8+4) verify 0.706 -> 0.627 ms, RS(16+4) verify 0.386 -> 0.351, rebuild 1-4 and
-    // heals 1-5 % faster (profiles/r02/ab_get_nt.jsonl).  Diagnostics 246: plain loads.
-    if constexpr (ZS3_DIAG) {
-        if (a.variant == 246) return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, BT, false>(a, s);
-    }
-    return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, BT, true>(a, s);
 }
 
-template <int K, int EX, bool HOUT, int G, int T, int PF, int CW, bool HQ, bool ST, int BT, bool NTL>
+template <int K, int EX, bool HOUT, int G, int T, int PF, int CW, bool HQ, bool ST, int BT, bool NTL, bool UA>
 static bool launch_vr_ws_bt(const VrArgs& a, hipStream_t s) {
     constexpr int RH = K + (HOUT ? EX : 0);
     constexpr int NT = vr_nh<G, RH, HQ>() + G * (T / CW);
@@ -1328,9 +1378,10 @@ static bool launch_vr_ws_bt(const VrArgs& a, hipStream_t s) {
                   vr_nh<G, RH, HQ>() % 64 != 0 || (G * (T / CW)) % 64 != 0) {
         return false;
     } else {
-        if (a.e != EX || (a.S % 16) != 0 || a.k != K || (HOUT != (a.sums_out != nullptr) && EX > 0)) return false;
+        if (a.e != EX || (!UA && (a.S % 16) != 0) || a.k != K || (HOUT != (a.sums_out != nullptr) && EX > 0))
+            return false;
         if ((int64_t)(a.k + a.m) * a.S >= ((int64_t)1 << 31)) return false;  // 32-bit row offsets
-        auto kern = k_vr_ws<K, EX, HOUT, G, T, PF, CW, HQ, ST, BT, NTL>;
+        auto kern = k_vr_ws<K, EX, HOUT, G, T, PF, CW, HQ, ST, BT, NTL, UA>;
         if (ensure_dyn_lds((const void*)kern, dyn) != hipSuccess) return false;
         const int64_t grid = (a.n_blocks + G - 1) / G;
         hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), dyn, s, a);

@@ -55,6 +55,25 @@ static bool launch_vr_ws_default(const VrArgs& a, hipStream_t s) {
         if (a.e == 4) return launch_vr_ws_t<16, 4, true, 8, 384, 1, 8, false, true, 4>(a, s);
         return false;
     }
+    if (a.k == 12 && (a.S % 16) != 0) {
+        // RS(12+4) on 1 MiB blocks (the 16-drive default; S = 87 382, unaligned rows):
+        // the RS(16+4) shapes in UA mode (round 3) instead of a survivor-verify hash launch
+        // + the reconstruct kernel + a heal hash launch: 4096 x 1 MiB rebuild 2 1.77 ->
+        // 1.48 ms, heal 2 2.09 -> 1.44 ms (profiles/r03/bench_paths_get_ua.jsonl).  Verify
+        // only stays on the stripe-mode hash launch (0.77 vs 0.87 ms).
+        if (!heal) {
+            if (a.e == 1) return launch_vr_ws_t<12, 1, false, 8, 256, 2, 4, false, true, 0, true>(a, s);
+            if (a.e == 2) return launch_vr_ws_t<12, 2, false, 8, 256, 2, 4, false, true, 0, true>(a, s);
+            if (a.e == 3) return launch_vr_ws_t<12, 3, false, 8, 512, 1, 8, false, true, 4, true>(a, s);
+            if (a.e == 4) return launch_vr_ws_t<12, 4, false, 8, 512, 1, 8, false, true, 4, true>(a, s);
+            return false;
+        }
+        if (a.e == 1) return launch_vr_ws_t<12, 1, true, 8, 384, 1, 8, false, true, 4, true>(a, s);
+        if (a.e == 2) return launch_vr_ws_t<12, 2, true, 8, 384, 1, 8, false, true, 4, true>(a, s);
+        if (a.e == 3) return launch_vr_ws_t<12, 3, true, 8, 384, 1, 8, false, true, 4, true>(a, s);
+        if (a.e == 4) return launch_vr_ws_t<12, 4, true, 8, 384, 1, 8, false, true, 4, true>(a, s);
+        return false;
+    }
     if (a.k != 8) return false;
     if (heal) {
         // RS(8+4) heal 1-2 (9-10 hashed rows): 8-byte rebuild columns and 128-byte tiles

@@ -1831,6 +1831,14 @@ hipError_t launch_verify_reconstruct(const VrArgs& a, hipStream_t s, int* path) 
             default: break;
         }
     }
+    // RS(12+4) on 1 MiB blocks (unaligned rows): the warp-specialised kernel in UA mode
+    // (diagnostics 97: the any-geometry launches below)
+    if (a.e <= 4 && a.k == 12 && (a.S % 16) != 0 && !(ZS3_DIAG && a.variant == 97)) {
+        if (launch_vr_ws(0, a, s)) {
+            if (path) *path = PATH_WS;
+            return hipGetLastError();
+        }
+    }
     // Any other shape: one verify launch per survivor row, then the reconstruct
     // kernel, then (heal) one hash launch per rebuilt row.
     if (path) *path = PATH_GENERIC;

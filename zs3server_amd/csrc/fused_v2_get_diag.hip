@@ -13,7 +13,32 @@ bool launch_vr_ws_diag_k4(int v, const VrArgs& a, hipStream_t s);   // fused_v2_
 bool launch_vr_ws_diag_k8(int v, const VrArgs& a, hipStream_t s);   // fused_v2_get_diag8.hip
 bool launch_vr_ws_diag_k16(int v, const VrArgs& a, hipStream_t s);  // fused_v2_get_diag16.hip
 
+// RS(12+4) on unaligned rows (UA), round 3: shape candidates against the product
+// instances (the RS(16+4) shapes; fused_v2_get.hip)
+//  264: 8 stripes, 8-byte columns of 512-byte tiles, batched scalar tables, for every e
+//  (16 stripes with 16-byte columns, the RS(8+4) GET shape, spill 90-4 000 VGPRs at
+//  K = 12 and are not compiled; 16 stripes of 8-byte columns spill 19-24 in heal)
+//  267: 8 stripes, 8-byte columns of 256-byte tiles, two tiles of prefetch, batched tables
+template <int EX, bool H>
+static bool vr12_ua(int v, const VrArgs& a, hipStream_t s) {
+    switch (v) {
+        case 264: return launch_vr_ws_t<12, EX, H, 8, 512, 1, 8, false, true, 4, true>(a, s);
+        case 267: return launch_vr_ws_t<12, EX, H, 8, 256, 2, 8, false, true, 4, true>(a, s);
+        default: return false;
+    }
+}
+
 bool launch_vr_ws_diag(int v, const VrArgs& a, hipStream_t s) {
+    if (a.k == 12 && (a.S % 16) != 0 && v >= 264 && v <= 267) {
+        const bool h = a.sums_out != nullptr;
+        switch (a.e) {
+            case 1: return h ? vr12_ua<1, true>(v, a, s) : vr12_ua<1, false>(v, a, s);
+            case 2: return h ? vr12_ua<2, true>(v, a, s) : vr12_ua<2, false>(v, a, s);
+            case 3: return h ? vr12_ua<3, true>(v, a, s) : vr12_ua<3, false>(v, a, s);
+            case 4: return h ? vr12_ua<4, true>(v, a, s) : vr12_ua<4, false>(v, a, s);
+            default: return false;
+        }
+    }
     if (a.k == 4) return launch_vr_ws_diag_k4(v, a, s);
     if (a.k == 8) return launch_vr_ws_diag_k8(v, a, s);
     if (a.k == 16) return launch_vr_ws_diag_k16(v, a, s);

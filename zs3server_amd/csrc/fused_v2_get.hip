@@ -61,18 +61,22 @@ static bool launch_vr_ws_default(const VrArgs& a, hipStream_t s) {
         // + the reconstruct kernel + a heal hash launch: 4096 x 1 MiB rebuild 2 1.77 ->
         // 1.48 ms, heal 2 2.09 -> 1.44 ms (profiles/r03/bench_paths_get_ua.jsonl).  Verify
         // only stays on the stripe-mode hash launch (0.77 vs 0.87 ms).
+        // Every e: 8-byte rebuild columns of 512-byte tiles with batched scalar tables
+        // (diagnostics 264): 4096 x 1 MiB rebuild 1/2/3 1.35/1.46/1.51 -> 1.21/1.30/1.31 ms,
+        // heal 1/2/3/4 1.28/1.43/1.61/1.78 -> 1.25/1.37/1.50/1.63 (rebuild 4 1.55 vs 1.58);
+        // the RS(16+4) shapes they replace (4-byte columns for rebuild 1-2, 384-byte heal
+        // tiles) and 267 (256-byte tiles) are in profiles/r03/get_ab_rs124.jsonl
+        if (a.e < 1 || a.e > 4) return false;
         if (!heal) {
-            if (a.e == 1) return launch_vr_ws_t<12, 1, false, 8, 256, 2, 4, false, true, 0, true>(a, s);
-            if (a.e == 2) return launch_vr_ws_t<12, 2, false, 8, 256, 2, 4, false, true, 0, true>(a, s);
+            if (a.e == 1) return launch_vr_ws_t<12, 1, false, 8, 512, 1, 8, false, true, 4, true>(a, s);
+            if (a.e == 2) return launch_vr_ws_t<12, 2, false, 8, 512, 1, 8, false, true, 4, true>(a, s);
             if (a.e == 3) return launch_vr_ws_t<12, 3, false, 8, 512, 1, 8, false, true, 4, true>(a, s);
-            if (a.e == 4) return launch_vr_ws_t<12, 4, false, 8, 512, 1, 8, false, true, 4, true>(a, s);
-            return false;
+            return launch_vr_ws_t<12, 4, false, 8, 512, 1, 8, false, true, 4, true>(a, s);
         }
-        if (a.e == 1) return launch_vr_ws_t<12, 1, true, 8, 384, 1, 8, false, true, 4, true>(a, s);
-        if (a.e == 2) return launch_vr_ws_t<12, 2, true, 8, 384, 1, 8, false, true, 4, true>(a, s);
-        if (a.e == 3) return launch_vr_ws_t<12, 3, true, 8, 384, 1, 8, false, true, 4, true>(a, s);
-        if (a.e == 4) return launch_vr_ws_t<12, 4, true, 8, 384, 1, 8, false, true, 4, true>(a, s);
-        return false;
+        if (a.e == 1) return launch_vr_ws_t<12, 1, true, 8, 512, 1, 8, false, true, 4, true>(a, s);
+        if (a.e == 2) return launch_vr_ws_t<12, 2, true, 8, 512, 1, 8, false, true, 4, true>(a, s);
+        if (a.e == 3) return launch_vr_ws_t<12, 3, true, 8, 512, 1, 8, false, true, 4, true>(a, s);
+        return launch_vr_ws_t<12, 4, true, 8, 512, 1, 8, false, true, 4, true>(a, s);
     }
     if (a.k != 8) return false;
     if (heal) {

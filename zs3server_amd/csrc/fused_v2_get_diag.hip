@@ -15,14 +15,18 @@ bool launch_vr_ws_diag_k16(int v, const VrArgs& a, hipStream_t s);  // fused_v2_
 
 // RS(12+4) on unaligned rows (UA), round 3: shape candidates against the product
 // instances (the RS(16+4) shapes; fused_v2_get.hip)
-//  264: 8 stripes, 8-byte columns of 512-byte tiles, batched scalar tables, for every e
+//  264: the first product instances (the RS(16+4) shapes); 8-byte columns of 512-byte
+//       tiles for every e measured fastest and became the product (get_ab_rs124.jsonl)
 //  (16 stripes with 16-byte columns, the RS(8+4) GET shape, spill 90-4 000 VGPRs at
 //  K = 12 and are not compiled; 16 stripes of 8-byte columns spill 19-24 in heal)
 //  267: 8 stripes, 8-byte columns of 256-byte tiles, two tiles of prefetch, batched tables
 template <int EX, bool H>
 static bool vr12_ua(int v, const VrArgs& a, hipStream_t s) {
     switch (v) {
-        case 264: return launch_vr_ws_t<12, EX, H, 8, 512, 1, 8, false, true, 4, true>(a, s);
+        case 264:  // round-3 RS(16+4)-shaped instances (4-byte rebuild-1/2 columns, 384-byte heal tiles)
+            if constexpr (H) return launch_vr_ws_t<12, EX, H, 8, 384, 1, 8, false, true, 4, true>(a, s);
+            else if constexpr (EX <= 2) return launch_vr_ws_t<12, EX, H, 8, 256, 2, 4, false, true, 0, true>(a, s);
+            else return launch_vr_ws_t<12, EX, H, 8, 512, 1, 8, false, true, 4, true>(a, s);
         case 267: return launch_vr_ws_t<12, EX, H, 8, 256, 2, 8, false, true, 4, true>(a, s);
         default: return false;
     }

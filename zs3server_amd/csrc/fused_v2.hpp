@@ -1350,7 +1350,11 @@ template <int K, int EX, bool HOUT, int G, int T, int PF, int CW = 16, bool HQ =
           int BT = 0, bool UA = false>
 static bool launch_vr_ws_t(const VrArgs& a, hipStream_t s) {
     if constexpr (UA) {
-        return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, BT, true, true>(a, s);
+        // plain (temporal) survivor loads: with unaligned rows each tile's first and last
+        // 128-byte lines are shared with the neighbouring tiles, and non-temporal loads
+        // fetched them twice (RS(12+4) rebuild 2: HBM traffic 1.205 x algorithmic,
+        // profiles/r03/final_session3/bench_paths_roofline.jsonl)
+        return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, BT, false, true>(a, s);
     } else {
         // diagnostics 240: the same launch with the scalar-table batching flipped (off <-> 4
         // coefficients per batch); 241: batches of 2

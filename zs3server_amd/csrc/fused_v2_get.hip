@@ -65,7 +65,9 @@ static bool launch_vr_ws_default(const VrArgs& a, hipStream_t s) {
         // (diagnostics 264): 4096 x 1 MiB rebuild 1/2/3 1.35/1.46/1.51 -> 1.21/1.30/1.31 ms,
         // heal 1/2/3/4 1.28/1.43/1.61/1.78 -> 1.25/1.37/1.50/1.63 (rebuild 4 1.55 vs 1.58);
         // the RS(16+4) shapes they replace (4-byte columns for rebuild 1-2, 384-byte heal
-        // tiles) and 267 (256-byte tiles) are in profiles/r03/get_ab_rs124.jsonl
+        // tiles) and 267 (256-byte tiles) are in profiles/r03/get_ab_rs124.jsonl.  Survivor
+        // loads are temporal in UA mode (launch_vr_ws_t): rebuild 1/2/3/4 -> 1.17/1.18/
+        // 1.15/1.43 ms, heal 1/2/3/4 -> 1.14/1.26/1.43/1.60 (get_ab_rs124_temporal.jsonl)
         if (a.e < 1 || a.e > 4) return false;
         if (!heal) {
             if (a.e == 1) return launch_vr_ws_t<12, 1, false, 8, 512, 1, 8, false, true, 4, true>(a, s);

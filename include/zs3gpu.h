@@ -60,7 +60,8 @@ int zs3_set_device(int device);        /* hipSetDevice for the calling OS thread
 int zs3_dev_alloc(void** d_ptr, size_t bytes);
 int zs3_dev_free(void* d_ptr);
 int zs3_host_alloc(void** h_ptr, size_t bytes);   /* pinned; backing for internal/bpool */
-int zs3_host_free(void* h_ptr);
+int zs3_host_free(void* h_ptr);                    /* a zs3_host_alloc pointer, else
+                                                      ZS3_ERR_INVALID_ARG (nothing freed) */
 int zs3_memcpy_h2d(void* d_dst, const void* h_src, size_t bytes, void* stream);
 int zs3_memcpy_d2h(void* h_dst, const void* d_src, size_t bytes, void* stream);
 int zs3_stream_sync(void* stream);
@@ -280,14 +281,22 @@ void zs3_split_range(int64_t total, int world, int rank, int64_t* lo, int64_t* h
  *     copied back by the queue's completion thread.
  * All entry points are thread-safe.  Every submitted request must be waited for
  * exactly once, before zs3_queue_free.  A submit may block while every staging slot
- * is in use, until a batch completes (never on other requests being waited for). */
+ * is in use, until a batch completes (never on other requests being waited for).
+ * A queue serves ONE block size, its codec's: a block of exactly that length is full
+ * (batched), a shorter one is an object's last block (launched on its own), a longer
+ * one is ZS3_ERR_INVALID_ARG.  The reference builds NewErasure(k, m, blockSize) per
+ * object with the object's own block size (1 MiB, or 10 MiB for legacy objects,
+ * cmd/object-api-common.go:37-40), so a server keeps one codec + queue per
+ * (k, m, blockSize). */
 typedef struct zs3_queue zs3_queue;
 typedef struct zs3_req zs3_req;
 typedef struct {
     int device;       /* HIP device ordinal; -1 = the calling thread's current device */
     int max_batch;    /* blocks per device batch (0 = 128).  Memory per lane in use:
                          slots x max_batch x (k+m) x S of pinned host AND of device
-                         memory (+ sums); RS(8+4) 1 MiB, 4 slots, 128: 768 MiB each */
+                         memory (+ sums); RS(8+4) 1 MiB, 4 slots, 128: 768 MiB each.
+                         The shim sizes it by bytes (384 MiB per slot: 256 at 1 MiB,
+                         25 at 10 MiB) */
     int max_wait_us;  /* longest a block waits for its batch to fill (0 = 200) */
     int slots;        /* pinned staging slots (+ streams) per lane (0 = 4; at least 2) */
 } zs3_queue_opts;

@@ -115,3 +115,61 @@ def test_bitrot_shard_file_size():
     assert z.bitrot_shard_file_size(131072, 131072) == 131072 + 32
     assert z.bitrot_shard_file_size(0, 10) == 0
     assert z.bitrot_shard_file_size(4 * 131072 + 1, 131072) == 5 * 32 + 4 * 131072 + 1
+
+
+# Batch layout validation: every case is rejected before any device
+# call, so the fake device addresses below are never dereferenced.
+BASE = 1 << 40
+
+
+def _codec_handle(k, m):
+    c = z.Codec(k, m, 1 << 20)
+    return c, c._h
+
+
+@pytest.mark.parametrize("case", ["neg_stride", "data_overlap", "parity_overlap", "parity_on_data",
+                                  "parity_on_next_block", "parity_span_on_data"])
+def test_encode_batch_rejects_bad_layouts(case):
+    import ctypes as C
+    k, m = 8, 4
+    c, h = _codec_handle(k, m)
+    L = z.lib()
+    S = (1 << 20) // k
+    B, R = 1 << 20, k + m
+    args = {
+        # (data, data_stride, n, parity, parity_stride)
+        "neg_stride": (BASE, -R * S, 4, BASE + k * S, -R * S),
+        "data_overlap": (BASE, B - 16, 4, BASE + 64 * R * S, m * S),
+        "parity_overlap": (BASE, R * S, 4, BASE + 64 * R * S, m * S - 1),
+        "parity_on_data": (BASE, R * S, 4, BASE + k * S - 16, R * S),  # parity row 0 on data row 7
+        "parity_on_next_block": (BASE, R * S - 16, 1 + 3, BASE + k * S, R * S - 16),
+        "parity_span_on_data": (BASE, R * S, 4, BASE + 2 * R * S, m * S),  # separate span inside the data
+    }[case]
+    d, ds, n, p, ps = args
+    rc = L.zs3_encode_batch(h, C.c_void_p(d), ds, B, n, C.c_void_p(p), ps, None, None)
+    assert rc == -8, (case, rc)
+
+
+@pytest.mark.parametrize("fn", ["reconstruct", "verify", "reconstruct_masks", "verify_masks"])
+@pytest.mark.parametrize("stride_delta", [-1, -(1 << 30)])
+def test_stripe_batches_reject_short_strides(fn, stride_delta):
+    import ctypes as C
+    k, m = 8, 4
+    R = k + m
+    c, h = _codec_handle(k, m)
+    L = z.lib()
+    S = (1 << 20) // k
+    n = 4
+    stride = R * S + stride_delta
+    pres = (C.c_uint8 * R)(*([0, 0] + [1] * (R - 2)))
+    presn = (C.c_uint8 * (R * n))(*(([0, 0] + [1] * (R - 2)) * n))
+    fake = C.c_void_p(BASE)
+    if fn == "reconstruct":
+        rc = L.zs3_reconstruct_batch(h, fake, stride, S, n, pres, 1, None)
+    elif fn == "verify":
+        rc = L.zs3_verify_reconstruct_batch(h, fake, stride, S, n, pres, 1, fake, fake, None, None)
+    elif fn == "reconstruct_masks":
+        rc = L.zs3_reconstruct_batch_masks(h, fake, stride, S, n, presn, 1, None, None)
+    else:
+        rc = L.zs3_verify_reconstruct_batch_masks(h, fake, stride, S, n, presn, 1, fake, fake, None, None, None)
+    assert rc == -8, (fn, rc)

@@ -102,15 +102,23 @@ def test_profiled_encode_shapes_full_check(oracle, k, m, nb):
     chunked_check(oracle, k, m, d, sums, nb, S, 42, 0)
 
 
-def _tiled_stripes(oracle, k, m, blen, nb, seed, distinct=64):
+# Distinct oracle stripes per batch: prime, so the period is coprime with every
+# workgroup's stripe count G (4 / 8 / 16) and with the tile loops: a kernel that reads or
+# writes the wrong stripe (shifted by any multiple of G) cannot land on an identical copy.
+PERIOD = 61
+
+
+def _tiled_stripes(oracle, k, m, blen, nb, seed, distinct=PERIOD):
+    """`distinct` oracle stripes (+ their sums) and the device index of the stripe each of
+    the nb batch positions holds (position b holds stripe b % distinct)."""
     R = k + m
     S = -(-blen // k)
     mat = oracle.build_matrix(k, m)
     base = np.stack([oracle.encode_data(k, m, oracle.fill(seed, b, blen), mat).reshape(R, S)
                      for b in range(distinct)])
     bsum = np.stack([oracle.hh256_rows(KEY, s) for s in base])
-    reps = nb // distinct
-    return base, bsum, reps
+    idx = torch.arange(nb, device=DEV) % distinct
+    return base, bsum, idx
 
 
 @pytest.mark.parametrize("k,m,nb,erased,heal", [
@@ -123,16 +131,18 @@ def test_get_heal_profiled_shape(oracle, k, m, nb, erased, heal):
     lost row + hash it) at the profiled shape: 1 MiB blocks, product dispatch, one
     rotted survivor flagged exactly."""
     R = k + m
-    base, bsum, reps = _tiled_stripes(oracle, k, m, MiB, nb, seed=17)
+    base, bsum, idx = _tiled_stripes(oracle, k, m, MiB, nb, seed=17)
     S = base.shape[2]
     codec = z.Codec(k, m, MiB)
-    d = torch.from_numpy(base).to(DEV).repeat(reps, 1, 1).contiguous()
+    ref = torch.from_numpy(base).to(DEV)
+    refs = torch.from_numpy(bsum).to(DEV)
+    d = ref[idx].contiguous()
     for e in erased:
         d[:, e, :] = 0x5A
     surv = [i for i in range(R) if i not in erased][:k]
     bad_blk, bad_row = nb - 3, surv[-1]
     d[bad_blk, bad_row, 12345] ^= 1
-    exp = torch.from_numpy(bsum).to(DEV).repeat(reps, 1, 1).contiguous()
+    exp = refs[idx].contiguous()
     bad = torch.full((nb, R), 7, dtype=torch.int32, device=DEV)
     out = torch.zeros((nb, R, 32), dtype=torch.uint8, device=DEV) if heal else None
     present = [i not in erased for i in range(R)]
@@ -145,19 +155,16 @@ def test_get_heal_profiled_shape(oracle, k, m, nb, erased, heal):
     rebuilt = [i for i in erased if i < k or heal]
     ok = torch.ones(nb, dtype=torch.bool, device=DEV)
     ok[bad_blk] = False  # rebuilt from a rotted survivor: garbage by design
-    ref = torch.from_numpy(base).to(DEV)
-    refs = torch.from_numpy(bsum).to(DEV)
-    dv = d.view(reps, 64, R, S)
-    okv = ok.view(reps, 64)
     for i in rebuilt:
-        same = (dv[:, :, i, :] == ref[None, :, i, :]).all(dim=2)
-        assert bool(same[okv].all()), f"rebuilt shard {i}"
+        same = (d[:, i, :] == ref[idx, i, :]).all(dim=1)
+        assert bool(same[ok].all()), f"rebuilt shard {i}"
         if heal:
-            sv = out.view(reps, 64, R, 32)[:, :, i, :]
-            assert bool((sv == refs[None, :, i, :]).all(dim=2)[okv].all()), f"heal sum of shard {i}"
+            assert bool((out[:, i, :] == refs[idx, i, :]).all(dim=1)[ok].all()), f"heal sum of shard {i}"
     for i in range(R):
         if i in erased and i not in rebuilt:
-            assert bool((dv[:, :, i, :] == 0x5A).all()), "ReconstructData leaves lost parity untouched"
+            assert bool((d[:, i, :] == 0x5A).all()), "ReconstructData leaves lost parity untouched"
+        elif i not in erased:
+            assert bool((d[:, i, :] == ref[idx, i, :]).all(dim=1)[ok].all()), f"survivor {i} untouched"
 
 
 @pytest.mark.parametrize("fillv", [0x00, 0xFF], ids=["zero", "ff"])
@@ -197,7 +204,7 @@ def test_masks_on_ws_kernel(oracle, k, m, blen, heal):
     interleaved patterns over 7 680 blocks, one rotted survivor flagged exactly."""
     R = k + m
     nb = 7680
-    base, bsum, reps = _tiled_stripes(oracle, k, m, blen, nb, seed=23)
+    base, bsum, idx = _tiled_stripes(oracle, k, m, blen, nb, seed=23)
     S = base.shape[2]
     pats_list = [[0, 5], [k, R - 1], [2]] if not heal else [[0, 5], [k, R - 1], [2, k + 1]]
     rng = np.random.default_rng(k + heal)
@@ -205,13 +212,13 @@ def test_masks_on_ws_kernel(oracle, k, m, blen, heal):
     pats = np.ones((nb, R), dtype=bool)
     for b in range(nb):
         pats[b, pats_list[which[b]]] = False
-    d = torch.from_numpy(base).to(DEV).repeat(reps, 1, 1).contiguous()
+    d = torch.from_numpy(base).to(DEV)[idx].contiguous()
     pt = torch.from_numpy(pats).to(DEV)
     d[~pt] = 0x66
     rb = 4000
     surv = [i for i in range(R) if pats[rb, i]][:k]
     d[rb, surv[0], S - 1] ^= 0x80
-    exp = torch.from_numpy(bsum).to(DEV).repeat(reps, 1, 1).contiguous()
+    exp = torch.from_numpy(bsum).to(DEV)[idx].contiguous()
     bad = torch.full((nb, R), 9, dtype=torch.int32, device=DEV)
     out = torch.zeros((nb, R, 32), dtype=torch.uint8, device=DEV) if heal else None
     codec = z.Codec(k, m, blen)
@@ -223,7 +230,7 @@ def test_masks_on_ws_kernel(oracle, k, m, blen, heal):
     want_bad = np.zeros((nb, R), np.int32)
     want_bad[rb, surv[0]] = 1
     assert np.array_equal(bad.cpu().numpy(), want_bad)
-    ref = torch.from_numpy(base).to(DEV).repeat(reps, 1, 1)
+    ref = torch.from_numpy(base).to(DEV)[idx]
     ok = torch.ones(nb, dtype=torch.bool, device=DEV)
     ok[rb] = False
     rows_ok = (d == ref).all(dim=2)  # [nb, R]
@@ -328,20 +335,22 @@ def test_any_geometry_get_heal(oracle, k, m, erased, heal):
     """GET / heal at unaligned shard sizes on 1 MiB blocks: RS(12+4) (S = 87 382) on the
     warp-specialised kernel in UA mode (round 3), the other geometries as survivors
     verified in one stripe-mode hash launch, the rebuild, rebuilt rows hashed in one
-    launch; one rotted survivor flagged exactly; 512 stripes of 64 distinct oracle
+    launch; one rotted survivor flagged exactly; 512 stripes of 61 distinct oracle
     stripes."""
     R = k + m
     nb = 512
-    base, bsum, reps = _tiled_stripes(oracle, k, m, MiB, nb, seed=31)
+    base, bsum, idx = _tiled_stripes(oracle, k, m, MiB, nb, seed=31)
     S = base.shape[2]
     codec = z.Codec(k, m, MiB)
-    d = torch.from_numpy(base).to(DEV).repeat(reps, 1, 1).contiguous()
+    ref = torch.from_numpy(base).to(DEV)
+    refs = torch.from_numpy(bsum).to(DEV)
+    d = ref[idx].contiguous()
     for e in erased:
         d[:, e, :] = 0x5A
     surv = [i for i in range(R) if i not in erased][:k]
     bad_blk, bad_row = 77, surv[2]
     d[bad_blk, bad_row, S - 1] ^= 4
-    exp = torch.from_numpy(bsum).to(DEV).repeat(reps, 1, 1).contiguous()
+    exp = refs[idx].contiguous()
     bad = torch.full((nb, R), 7, dtype=torch.int32, device=DEV)
     out = torch.zeros((nb, R, 32), dtype=torch.uint8, device=DEV) if heal else None
     codec.verify_reconstruct_batch(d, R * S, S, nb, [i not in erased for i in range(R)], not heal, exp, bad,
@@ -354,21 +363,16 @@ def test_any_geometry_get_heal(oracle, k, m, erased, heal):
     assert np.array_equal(bad.cpu().numpy(), want_bad)
     ok = torch.ones(nb, dtype=torch.bool, device=DEV)
     ok[bad_blk] = False
-    ref = torch.from_numpy(base).to(DEV)
-    refs = torch.from_numpy(bsum).to(DEV)
-    dv = d.view(reps, 64, R, S)
-    okv = ok.view(reps, 64)
     for i in erased:
         if i < k or heal:
-            assert bool((dv[:, :, i, :] == ref[None, :, i, :]).all(dim=2)[okv].all()), f"rebuilt shard {i}"
+            assert bool((d[:, i, :] == ref[idx, i, :]).all(dim=1)[ok].all()), f"rebuilt shard {i}"
             if heal:
-                sv = out.view(reps, 64, R, 32)[:, :, i, :]
-                assert bool((sv == refs[None, :, i, :]).all(dim=2)[okv].all()), f"heal sum {i}"
+                assert bool((out[:, i, :] == refs[idx, i, :]).all(dim=1)[ok].all()), f"heal sum {i}"
         else:
-            assert bool((dv[:, :, i, :] == 0x5A).all())
+            assert bool((d[:, i, :] == 0x5A).all())
     for i in range(R):  # nothing written outside the rebuilt rows (ragged last column)
         if i not in erased:
-            assert bool((dv[:, :, i, :] == ref[None, :, i, :]).all(dim=2)[okv].all()), f"survivor {i}"
+            assert bool((d[:, i, :] == ref[idx, i, :]).all(dim=1)[ok].all()), f"survivor {i}"
 
 
 @pytest.mark.parametrize("k,m,blen,erased,data_only", [

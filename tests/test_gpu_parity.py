@@ -319,7 +319,8 @@ def test_full_size_rs84_properties(oracle):
 def test_full_size_ws_defaults(oracle, k, m, nb):
     """BASELINE config 2 (RS(4+2), 1024 x 1 MiB) and RS(16+4) 2048 x 1 MiB at full size
     through the default launches (warp-specialised kernels); sampled blocks against the
-    oracle, every sum against the standalone hash kernel."""
+    oracle, every parity byte and sum against cpu_ref (pinned to the oracle by
+    tests/test_cpuref_pin.py)."""
     blen = 1 << 20
     S = blen // k
     stride = (k + m) * S
@@ -336,11 +337,16 @@ def test_full_size_ws_defaults(oracle, k, m, nb):
         want = oracle.encode_data(k, m, oracle.fill(42, b, blen), mat)
         assert np.array_equal(v[b].cpu().numpy(), want)
         assert np.array_equal(hs[b].cpu().numpy(), oracle.hh256_rows(KEY, want))
-    sums2 = torch.zeros_like(sums)
-    z.hh256_batch(d, S, S, nb * (k + m), sums2)
-    torch.cuda.synchronize()
-    assert torch.equal(sums, sums2)
-    del d, sums, sums2
+    from oracle import cpuref
+    R = k + m
+    host = d.cpu().numpy().reshape(nb, R * S)
+    par = np.empty(nb * m * S, np.uint8)
+    sref = np.empty(nb * R * 32, np.uint8)
+    cpuref.encode_hash(k, m, mat, np.ascontiguousarray(host), blen, nb, R * S, par, m * S, sref, KEY,
+                       cpuref.threads_available())
+    assert np.array_equal(host[:, k * S:], par.reshape(nb, m * S))
+    assert np.array_equal(sums.cpu().numpy(), sref)
+    del d, sums
     torch.cuda.empty_cache()
 
 

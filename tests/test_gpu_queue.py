@@ -216,13 +216,17 @@ def test_queue_batches_concurrent_blocks(oracle):
     q.close()
 
 
-@pytest.mark.parametrize("k,m,bs", [(8, 4, 1 << 20), (5, 3, 100000)])
+@pytest.mark.parametrize("k,m,bs", [(8, 4, 1 << 20), (5, 3, 100000), (12, 4, 1 << 20), (10, 4, 1 << 20)])
 def test_queue_zero_copy_pinned_callers(oracle, k, m, bs):
     """Callers whose block buffers come from zs3_host_alloc (the pinned bpool) are
     served zero-copy (the DMA engine reads the data rows from, and writes the parity
     rows / rebuilt rows into, the caller's buffer), side by side in the same batches
     with pageable callers and with pinned callers' short last blocks (staged); every
-    result vs the oracle, and the queue reports the zero-copy blocks."""
+    result vs the oracle, and the queue reports the zero-copy blocks.  RS(12+4) (the
+    16-drive default, UA kernel) and RS(10+4) (any-geometry kernel) at 1 MiB have Split
+    padding (k*S > blockSize): a zero-copy block DMAs only its `len` data bytes, so the
+    slot's padding bytes hold whatever the slot's previous batch left there, and every
+    encode kernel must read them as zero."""
     codec = z.Codec(k, m, bs)
     q = z.Queue(codec, max_batch=16, max_wait_us=500)
     R = k + m

@@ -21,7 +21,8 @@ DEV = "cuda:0"
 SIZES_84 = [8 * 16, 8 * 384, 8 * 384 * 3, 8 * (384 * 2 + 32), 8 * (384 * 5 + 16), 1 << 20,
             8 * 1024 * 2, 8 * (1024 * 2 + 48), 8 * (1024 * 3 + 512)]
 VARIANTS = [0, 49, 99, 50, 51, 52, 53, 55, 70, 71, 80, 81, 82, 83, 84, 100, 102, 103, 104, 105, 106, 107, 108, 109, 130,
-            140, 141, 150, 151, 152, 153, 154, 155, 156, 160, 163, 133, 187, 191, 192, 193, 197, 198, 199]
+            140, 141, 150, 151, 152, 153, 154, 155, 156, 160, 163, 133, 187, 191, 192, 193, 197, 198, 199,
+            300, 301, 302, 303, 304, 305]
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -65,7 +66,7 @@ def test_rs84_variant_tile_edges(oracle, variant, blen):
 
 
 @pytest.mark.parametrize("variant", [49, 99, 50, 80, 83, 84, 100, 102, 103, 105, 108, 130, 140, 141, 150, 151, 152, 153, 154, 155,
-                                     156, 160, 163, 187, 197, 198, 199])
+                                     156, 160, 163, 187, 197, 198, 199, 300, 301, 302, 303, 304, 305])
 @pytest.mark.parametrize("nb", [1, 17, 33])
 def test_rs84_variant_dead_stripes(oracle, variant, nb):
     run_case(oracle, 8, 4, 8 * (384 * 4 + 128), nb, variant, seed=nb)

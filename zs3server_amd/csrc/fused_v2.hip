@@ -131,7 +131,7 @@ int launch_ehx(int v, const EncArgs& a, hipStream_t s) {
     if (a.k == 4 && a.m == 2) ok = launch_ehx_km_4_2(v, a, s);
     if (a.k == 16 && a.m == 4) ok = launch_ehx_km_16_4(v, a, s);
     if (a.k == 12 && a.m == 4) ok = launch_ehx_km_12_4(v, a, s);
-    if (ok) return (v >= 100 && v < 200) ? PATH_WS : PATH_PIPE;
+    if (ok) return ((v >= 100 && v < 200) || v >= 300) ? PATH_WS : PATH_PIPE;
 #endif
     return PATH_NONE;
 }

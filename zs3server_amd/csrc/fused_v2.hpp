@@ -448,6 +448,18 @@ template <int K, int CWX = 0>
 constexpr int ws_cwe() {
     return CWX ? CWX : (K > 8 ? 8 : 16);
 }
+// LDS row stride of the hash tiles.  TSP = 0: the round-1 padding (T + 16 pair form,
+// T + 32 quad form).  TSP = 1: bank-conflict-free for both read forms: the pair form's
+// ds_read_b128 serves 16 lanes = 8 chains per LDS cycle from lane groups
+// {0-3,12-15,20-27} / {4-11,16-19,28-31} (MI355X_MICROARCH.md §LDS), the quad form's
+// ds_read_b64 8 chains per 32-lane half; both are conflict-free iff consecutive rows
+// start 32 mod 64 bytes apart (row r's 16-byte slot pair then lands on a distinct pair
+// of the 256-byte bank row for every group).  T + 16 put every group 2-way
+// (SQ_LDS_BANK_CONFLICT = 20 % of SQ_LDS_IDX_ACTIVE on the RS(8+4) bench launch).
+template <int T, bool HQ, int TSP>
+constexpr int ws_ts() {
+    return TSP ? T + (T % 64 == 0 ? 32 : 0) : (HQ ? T + 32 : T + 16);
+}
 
 // WT (diagnostic): per-wave shader cycles spent waiting at barriers, into the dbg stamps.
 // PM (issue-priority experiments): 1 = encode waves s_setprio 1 over hash waves; 2 = as 1
@@ -484,9 +496,11 @@ constexpr int ws_cwe() {
 // and everything past the row read as zero, and stores only the parity bytes below S.
 // WPE: minimum waves per SIMD the register allocation is sized for (3 = 168 VGPRs; 2 =
 // 256, for workgroups of at most 8 waves, one per CU).
+// TSP: LDS row stride rule (ws_ts).  ABL (timing-only diagnostics, output differs):
+// bit 0 = the pair-form hash waves XOR the words instead of running HighwayHash.
 template <int K, int M, int G, int T, int PF, bool BUF = false, bool HQ = false, bool WT = false, int PM = 0,
           int CWX = 0, bool RING = false, int NTM = 0, bool STB = false, int EP = 0, int PFD = 0, bool UA = false,
-          int WPE = 3>
+          int WPE = 3, int TSP = 0, int ABL = 0>
 __global__ void __launch_bounds__((ws_nh<K, M, G, T, HQ>() + G * (T / ws_cwe<K, CWX>()))) __attribute__((amdgpu_waves_per_eu(WPE)))
 k_ehx_ws(EncArgs a) {
     constexpr int R = K + M;
@@ -495,7 +509,7 @@ k_ehx_ws(EncArgs a) {
     constexpr int CPS = T / CWE;    // encode columns per stripe row
     constexpr int NE = G * CPS;     // encode threads
     constexpr int NT = NH + NE;
-    constexpr int TS = HQ ? T + 32 : T + 16;  // conflict-free b64 (quad) / b128 (pair) row reads
+    constexpr int TS = ws_ts<T, HQ, TSP>();
     constexpr int NPK = T / 32;
     constexpr int NTAB = K * 8;
     static_assert(M == 2 || M == 4, "dyadic shapes only");
@@ -671,7 +685,13 @@ k_ehx_ws(EncArgs a) {
                         __builtin_amdgcn_sched_barrier(0);
                     }
                 }
-                hh2_update(st, ((uint64_t)w[i].y << 32) | w[i].x, ((uint64_t)w[i].w << 32) | w[i].z);
+                if constexpr (ABL & 1) {
+                    // timing ablation (diagnostics only; sums differ): no HighwayHash arithmetic
+                    st.v0[0] ^= ((uint64_t)w[i].y << 32) | w[i].x;
+                    st.v0[1] ^= ((uint64_t)w[i].w << 32) | w[i].z;
+                } else {
+                    hh2_update(st, ((uint64_t)w[i].y << 32) | w[i].x, ((uint64_t)w[i].w << 32) | w[i].z);
+                }
             }
             bar();
         }
@@ -945,11 +965,11 @@ k_ehx_ws(EncArgs a) {
 
 template <int K, int M, int G, int T, int PF, bool BUF = false, bool HQ = false, int LDSMIN = 0, bool WT = false,
           int PM = 0, int CWX = 0, bool RING = false, int NTM = 0, bool STB = false, int EP = 0, int PFD = 0,
-          bool UA = false, int WPE = 3>
+          bool UA = false, int WPE = 3, int TSP = 0, int ABL = 0>
 static bool launch_ws_t(const EncArgs& a, hipStream_t s) {
     constexpr int R = K + M;
     constexpr int NT = ws_nh<K, M, G, T, HQ>() + G * (T / ws_cwe<K, CWX>());
-    constexpr size_t tiles = (size_t)2 * G * R * (HQ ? T + 32 : T + 16);
+    constexpr size_t tiles = (size_t)2 * G * R * ws_ts<T, HQ, TSP>();
     constexpr size_t dyn = tiles > (size_t)LDSMIN ? tiles : (size_t)LDSMIN;
     if constexpr (dyn + K * 32 > 163840 || NT > 1024) {
         return false;
@@ -965,7 +985,7 @@ static bool launch_ws_t(const EncArgs& a, hipStream_t s) {
         if (BUF && ((G - 1) * a.data_stride + K * a.S > 0x7FFFFFFF ||
                     (G - 1) * a.parity_stride + M * a.S > 0x7FFFFFFF || a.data_stride < 0 || a.parity_stride < 0))
             return false;
-        auto kern = k_ehx_ws<K, M, G, T, PF, BUF, HQ, WT, PM, CWX, RING, NTM, STB, EP, PFD, UA, WPE>;
+        auto kern = k_ehx_ws<K, M, G, T, PF, BUF, HQ, WT, PM, CWX, RING, NTM, STB, EP, PFD, UA, WPE, TSP, ABL>;
         if (ensure_dyn_lds((const void*)kern, dyn) != hipSuccess) return false;
         const int64_t grid = (a.n_blocks + G - 1) / G;
         hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), dyn, s, a);

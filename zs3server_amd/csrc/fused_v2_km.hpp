@@ -122,6 +122,21 @@ static bool launch_ehx_km(int v, const EncArgs& a, hipStream_t s) {
         case 116: if constexpr (few) return launch_ws_t<K, M, 4, 512, 4, false, true, 83968, false, 0, 0, false, 2>(a, s); else return false;
         case 61: if constexpr (deep) return launch_ehx_t<K, M, 8, 1, 2, false, 1>(a, s); else return false;
         case 64: if constexpr (deep) return launch_ehx_t<K, M, 8, 2, 2, false, 1>(a, s); else return false;
+        // round 4: conflict-free LDS rows (TSP = 1), buffer-addressed
+        // encode columns (no VGPR spills) with one / two tiles of register prefetch
+        case 300: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3, false, 0, 0, false, 3, 1>(a, s); else return false;
+        case 301: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 2, true, false, 0, false, 1, 0, false, 3, false, 0, 0, false, 3, 1>(a, s); else return false;
+        case 302: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, true, false, 0, false, 1, 0, false, 3, false, 0, 0, false, 3, 1>(a, s); else return false;
+        case 303: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 2, true, false, 0, false, 0, 0, false, 3, false, 0, 0, false, 3, 1>(a, s); else return false;
+        case 304: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 2, true, false, 0, false, 1, 0, false, 3, false, 2, 0, false, 3, 1>(a, s); else return false;
+        case 305: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 2, true, false, 0, false, 1, 0, false, 3, false, 0, 0, false, 3, 0>(a, s); else return false;
+        case 306: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 2, true, false, 0, true, 1, 0, false, 3, false, 0, 0, false, 3, 1>(a, s); else return false;
+        case 307: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, false, false, 0, true, 1, 0, false, 3, false, 0, 0, false, 3, 1>(a, s); else return false;
+        // energy / pipeline ablations of 302 (timing only): no hash arithmetic, no GF
+        // arithmetic, neither
+        case 310: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, true, false, 0, false, 1, 0, false, 3, false, 0, 0, false, 3, 1, 1>(a, s); else return false;
+        case 311: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, true, false, 0, false, 1, 0, false, 3, false, 9, 0, false, 3, 1, 0>(a, s); else return false;
+        case 312: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, true, false, 0, false, 1, 0, false, 3, false, 9, 0, false, 3, 1, 1>(a, s); else return false;
         default: return false;
     }
 }

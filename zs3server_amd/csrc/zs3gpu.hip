@@ -360,8 +360,11 @@ int zs3_host_alloc(void** h_ptr, size_t bytes) {
 }
 int zs3_host_free(void* h_ptr) {
     {
+        // only what zs3_host_alloc returned: the pinned bpool's Go-heap fallback buffers
+        // (and any other pointer) are refused untouched, so a pool may call this on every
+        // buffer it drops
         std::lock_guard<std::mutex> g(g_pin_mu);
-        g_pinned.erase((uintptr_t)h_ptr);
+        if (g_pinned.erase((uintptr_t)h_ptr) == 0) return ZS3_ERR_INVALID_ARG;
     }
     return map_hip(hipHostFree(h_ptr));
 }
@@ -430,6 +433,36 @@ int64_t zs3_bitrot_shard_file_size(int64_t size, int64_t shard_size) {
     return ceil_frac(size, shard_size) * 32 + size;
 }
 
+// Batch layout checks: a caller's layout error comes back as
+// ZS3_ERR_INVALID_ARG instead of becoming an out-of-bounds or overlapping device access.
+// Encode: block b reads d_data + b*ds + [0, len) and writes d_parity + b*ps + [0, m*S);
+// blocks must not overlap (ds >= len, ps >= m*S when n > 1) and no parity row may land
+// on a data byte (the kernels read a tile's data rows before its parity rows are
+// written, but a later tile's data must survive).  Equal strides (the reference's
+// in-place Split layout, parity = data + k*S) are checked per period; distinct strides
+// (separate data / parity regions, as the queue's slots) as two disjoint spans.  The
+// diagnostics build also accepts ds = ps = 0: every block aliased onto block 0
+// (timing-only L2-resident runs, scripts/sweep_variants.py SWEEP_ALIAS).
+static bool encode_layout_ok(const uint8_t* data, int64_t ds, int64_t len, int64_t n, const uint8_t* parity,
+                             int64_t ps, int64_t mS) {
+#if ZS3_DIAG
+    if (ds == 0 && ps == 0) return true;
+#endif
+    if (ds < 0 || ps < 0) return false;
+    if (n > 1 && (ds < len || ps < mS)) return false;
+    const int64_t off = (int64_t)((uintptr_t)parity - (uintptr_t)data);
+    if (n == 1 || ds != ps) {
+        const int64_t d_end = (n - 1) * ds + len, p_end = off + (n - 1) * ps + mS;
+        return p_end <= 0 || off >= d_end;
+    }
+    // equal strides: the parity rows of every block sit in the gap of one period
+    const int64_t r = ((off % ds) + ds) % ds;
+    return r >= len && r + mS <= ds;
+}
+
+// Reconstruct / verify: block b's k+m shard rows at d_shards + b*stride + i*S.
+static bool stripe_layout_ok(int64_t stride, int64_t n, int64_t RS) { return stride >= 0 && (n <= 1 || stride >= RS); }
+
 int zs3_encode_batch(const zs3_codec* cc, const uint8_t* d_data, int64_t data_stride, int64_t block_len,
                      int64_t n_blocks, uint8_t* d_parity, int64_t parity_stride, uint8_t* d_sums,
                      void* stream) {
@@ -438,6 +471,8 @@ int zs3_encode_batch(const zs3_codec* cc, const uint8_t* d_data, int64_t data_st
     if (block_len == 0 || n_blocks == 0) return ZS3_OK;  // EncodeData len 0: k+m empty shards
     if (!d_data || !d_parity) return ZS3_ERR_INVALID_ARG;
     const int64_t S = ceil_frac(block_len, c->k);
+    if (!encode_layout_ok(d_data, data_stride, block_len, n_blocks, d_parity, parity_stride, (int64_t)c->m * S))
+        return ZS3_ERR_INVALID_ARG;
     zs3k::EncArgs a{};
     int rc = codec_device(c, &a.tables, &a.matrix);
     if (rc) return rc;
@@ -473,6 +508,8 @@ int zs3_reconstruct_batch(const zs3_codec* cc, uint8_t* d_shards, int64_t block_
     if (plan->status) return plan->status;
     if (shard_len == 0) return ZS3_ERR_SHARD_NO_DATA;
     if (plan->noop || n_blocks == 0) return ZS3_OK;
+    if (!d_shards || !stripe_layout_ok(block_stride, n_blocks, (int64_t)(c->k + c->m) * shard_len))
+        return ZS3_ERR_INVALID_ARG;
     zs3k::RecArgs a{};
     int rc = plan_device(c, plan.get(), &a.tables, &a.coef, &a.rows);
     if (rc) return rc;
@@ -500,6 +537,7 @@ int zs3_verify_reconstruct_batch(const zs3_codec* cc, uint8_t* d_shards, int64_t
     if (n_blocks == 0) return ZS3_OK;
     if (!d_shards || !d_expect || !d_bad) return ZS3_ERR_INVALID_ARG;
     const int R = c->k + c->m;
+    if (!stripe_layout_ok(block_stride, n_blocks, (int64_t)R * shard_len)) return ZS3_ERR_INVALID_ARG;
     int rc = map_hip(hipMemsetAsync(d_bad, 0, (size_t)n_blocks * R * 4, (hipStream_t)stream));
     if (rc) return rc;
     zs3k::VrArgs a{};
@@ -614,6 +652,8 @@ int zs3_reconstruct_batch_masks(const zs3_codec* cc, uint8_t* d_shards, int64_t 
     std::vector<PatternGroup> groups;
     const int first = group_patterns(c, present, n_blocks, data_only, status, groups);
     if (shard_len == 0) return first ? first : (n_blocks ? ZS3_ERR_SHARD_NO_DATA : ZS3_OK);
+    if (n_blocks > 0 && (!d_shards || !stripe_layout_ok(block_stride, n_blocks, (int64_t)(c->k + c->m) * shard_len)))
+        return ZS3_ERR_INVALID_ARG;
     hipStream_t s = (hipStream_t)stream;
     int last = zs3k::PATH_NONE;
     int32_t* d_ids = nullptr;
@@ -654,6 +694,7 @@ int zs3_verify_reconstruct_batch_masks(const zs3_codec* cc, uint8_t* d_shards, i
     if (!d_shards || !d_expect || !d_bad) return ZS3_ERR_INVALID_ARG;
     hipStream_t s = (hipStream_t)stream;
     const int R = c->k + c->m;
+    if (!stripe_layout_ok(block_stride, n_blocks, (int64_t)R * shard_len)) return ZS3_ERR_INVALID_ARG;
     int rc = map_hip(hipMemsetAsync(d_bad, 0, (size_t)n_blocks * R * 4, s));
     if (rc) return rc;
     int last = zs3k::PATH_NONE;

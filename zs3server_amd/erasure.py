@@ -8,6 +8,7 @@ All arithmetic runs in the HIP kernels (host-staged through pinned memory).
 from __future__ import annotations
 
 import io
+import threading
 
 import numpy as np
 
@@ -34,11 +35,52 @@ ERR_FILE_NOT_FOUND = "errFileNotFound"
 ERR_FILE_CORRUPT_NAME = "errFileCorrupt"
 
 
+# objectOpIgnoredErrs (cmd/erasure-object.go:48 = baseIgnoredErrs, storage-errors.go:127-133,
+# + errDiskAccessDenied, errUnformattedDisk): not counted by reduceWriteQuorumErrs
+OBJECT_OP_IGNORED_ERRS = frozenset({"errDiskNotFound", "errFaultyDisk", "errFaultyRemoteDisk",
+                                    "errDiskAccessDenied", "errUnformattedDisk"})
+
+
+def _err_name(e: BaseException) -> str:
+    """The Go identifier of a writer / reader error (DiskError.name, a ZS3Error's
+    reedsolomon sentinel), else the exception's own text."""
+    name = getattr(e, "name", None)
+    if name:
+        return name
+    if isinstance(e, ZS3Error) and e.code == ERR_FILE_CORRUPT:
+        return "errFileCorrupt"
+    return str(e) or type(e).__name__
+
+
+def reduce_write_quorum_errs(errs: list, write_quorum: int):
+    """reduceWriteQuorumErrs (cmd/erasure-metadata-utils.go:36-87): the most frequent
+    non-ignored error value (None counts as a value, and wins ties) if it occurs at
+    least write_quorum times, else errErasureWriteQuorum.  Returns None or raises."""
+    counts: dict = {}
+    for e in errs:
+        if e in OBJECT_OP_IGNORED_ERRS:
+            continue
+        counts[e] = counts.get(e, 0) + 1
+    max_count, max_err = 0, None
+    for e, c in counts.items():
+        if c > max_count:
+            max_count, max_err = c, e
+        elif c == max_count and e is None:
+            max_err = None
+    if max_count >= write_quorum:
+        if max_err is None:
+            return None
+        from .bitrot import DiskError
+        raise DiskError(max_err)
+    raise ErasureWriteQuorum(f"{sum(e is None for e in errs)} writers ok < quorum {write_quorum}")
+
+
 class ParallelWriter:
-    """parallelWriter (cmd/erasure-encode.go:29-73): one Write per shard writer, a
-    failed writer is dropped (its slot in the caller's list set to None, as the Go
-    slice is shared), quorum reduced over the per-writer errors.  The fused device
-    encode hands each writer its precomputed HighwayHash sum (WriteWithSum)."""
+    """parallelWriter (cmd/erasure-encode.go:29-73): one Write per shard writer; a writer
+    that fails in any way is dropped (its slot in the caller's list set to None, as the
+    Go slice is shared) with its error recorded; below write quorum the per-writer errors
+    are reduced as reduceWriteQuorumErrs does.  The fused device encode hands each writer
+    its precomputed HighwayHash sum (WriteWithSum)."""
 
     def __init__(self, writers: list, write_quorum: int):
         self.writers = writers  # shared with the caller, like the Go slice
@@ -46,7 +88,6 @@ class ParallelWriter:
         self.errs = [None] * len(writers)
 
     def Write(self, blocks: list, sums=None) -> None:
-        from .bitrot import DiskError
         for i, w in enumerate(self.writers):
             if w is None:
                 self.errs[i] = "errDiskNotFound"
@@ -61,13 +102,13 @@ class ParallelWriter:
                 if n != len(blocks[i]):
                     self.errs[i] = "io.ErrShortWrite"
                     self.writers[i] = None
-            except DiskError as e:
-                self.errs[i] = e.name
+            except Exception as e:  # noqa: BLE001 - every write error drops that writer (:51-58)
+                self.errs[i] = _err_name(e)
                 self.writers[i] = None
         # HealFile uses writeQuorum 1 (erasure-encode.go:63-69)
         if sum(e is None for e in self.errs) >= self.write_quorum:
             return
-        raise ErasureWriteQuorum(f"{sum(e is None for e in self.errs)} writers ok < quorum {self.write_quorum}")
+        reduce_write_quorum_errs(self.errs, self.write_quorum)
 
 
 class ParallelReader:
@@ -131,9 +172,13 @@ class ParallelReader:
                     want, chunk = rr.read_raw(self.shard_size, self.offset)
                     cand.append((i, bi, want, chunk))
                 except (DiskError, ZS3Error) as err:
-                    name = getattr(err, "name", "")
+                    # erasure-decode.go:165-171: errFileNotFound -> missingPartsHeal,
+                    # errFileCorrupt (a reader that detected the rot itself) -> bitrotHeal
+                    name = _err_name(err)
                     if name == ERR_FILE_NOT_FOUND:
                         missing_heal = True
+                    elif name == ERR_FILE_CORRUPT_NAME:
+                        bitrot_heal = True
                     self.org_readers[bi] = None
                     self.readers[i] = None
             if not cand:
@@ -401,6 +446,78 @@ def _hash_chunks(bufs: list, key: bytes, hh256_batch) -> list:
     hh256_batch(d, stride, L, n, out, key=key)
     o = out.cpu().numpy().reshape(n, 32)
     return [o[i].tobytes() for i in range(n)]
+
+
+# ---------------------------------------------------------------------------------------
+# The rocm build's codec cache (getGPUCodec), mirrored so the tests can
+# drive it.  NewErasure(k, m, blockSize) is called per request with the object's own block
+# size (cmd/erasure-object.go:283 with fi.Erasure.BlockSize, erasure-healing.go:467-468):
+# blockSizeV2 = 1 MiB for new objects, blockSizeV1 = 10 MiB for legacy ones
+# (cmd/object-api-common.go:37-40).  A queue batches blocks of ONE shard size, and a full
+# block is exactly its codec's block size, so the cache is keyed by (k, m, blockSize): a
+# legacy object's full 10 MiB blocks batch together in their own queue, and a 1 MiB
+# object's full blocks are never mistaken for short blocks of a 10 MiB queue (nor
+# rejected by it).
+QUEUE_SLOT_BYTES = 384 << 20  # pinned staging per queue slot (and as much device memory)
+QUEUE_MAX_BATCH = 512
+
+
+def queue_max_batch(k: int, m: int, block_size: int) -> int:
+    """Blocks per queue batch for a geometry: as many stripes as one slot's byte budget
+    holds (RS(8+4) at 1 MiB: 256, so a closed batch leaves the <= 128-stripe latency path
+    for the tuned kernels; at blockSizeV1 = 10 MiB: 25), at least 4, at most 512."""
+    S = -(-block_size // k)
+    return max(4, min(QUEUE_MAX_BATCH, QUEUE_SLOT_BYTES // ((k + m) * S)))
+
+
+class GPUCodec:
+    """gpuCodec: the (k, m, blockSize) coding matrix and its batching
+    queue, shared by every request of that geometry and block size."""
+
+    def __init__(self, k: int, m: int, block_size: int, queue_factory=None):
+        from . import Queue
+        self.key = (k, m, block_size)
+        self.codec = Codec(k, m, block_size)  # ErrInvShardNum / ErrMaxShardNum as NewErasure
+        factory = queue_factory or (lambda c, mb: Queue(c, max_batch=mb, max_wait_us=200, slots=4))
+        self.max_batch = queue_max_batch(k, m, block_size)
+        self.queue = factory(self.codec, self.max_batch)
+
+    def encode_data(self, buf, length: int, sums: bool = True):
+        """encodeDataGPU: Split + Encode in place (+ the k+m bitrot sums) through the queue."""
+        return self.queue.encode_data(buf, length, sums=sums)
+
+    def decode(self, shards, present, data_only: bool, expect=None, bad=None, sums_out=None) -> int:
+        """reconstructGPU: DecodeDataBlocks / DecodeDataAndParityBlocks (+ verify / heal sums)."""
+        return self.queue.decode(shards, present, data_only, expect=expect, bad=bad, sums_out=sums_out)
+
+
+_GPU_CODECS: dict = {}
+_GPU_CODECS_MU = threading.Lock()
+
+
+def get_gpu_codec(k: int, m: int, block_size: int, queue_factory=None) -> GPUCodec:
+    """getGPUCodec: the process-wide GPUCodec of (k, m, blockSize), created on first use
+    (LoadOrStore: concurrent first callers get the same one)."""
+    key = (k, m, block_size)
+    c = _GPU_CODECS.get(key)
+    if c is not None:
+        return c
+    with _GPU_CODECS_MU:
+        c = _GPU_CODECS.get(key)
+        if c is None:
+            c = GPUCodec(k, m, block_size, queue_factory)
+            _GPU_CODECS[key] = c
+        return c
+
+
+def drop_gpu_codecs() -> None:
+    """Release every cached codec and queue (tests; process shutdown flushes them)."""
+    with _GPU_CODECS_MU:
+        for c in _GPU_CODECS.values():
+            close = getattr(c.queue, "close", None)
+            if close:
+                close()
+        _GPU_CODECS.clear()
 
 
 def NewErasure(data_blocks: int, parity_blocks: int, block_size: int) -> Erasure:

@@ -3,7 +3,7 @@ BASELINE shapes, each as one JSON line with its roofline (algorithmic HBM bytes 
 launch / median launch time, against the 8 TB/s HBM3E spec), plus the batching queue
 and the end-to-end host stream.
 
-  PATHS=encode,rec,get,hash,deep,digest,queue,e2e  python scripts/bench_paths.py
+  PATHS=encode,geom,rec,get,hash,deep,digest,queue,e2e  python scripts/bench_paths.py
 (default: all).  Kernel-only sections (encode..digest) are what scripts/profile_paths.sh
 runs under rocprofv3; queue and e2e include host copies and PCIe.
 """
@@ -23,7 +23,7 @@ import zs3server_amd as z  # noqa: E402
 PEAK = 8000.0  # GB/s, MI355X HBM3E spec
 MiB = 1 << 20
 KEY = z.MAGIC_HH256_KEY
-PATHS = set(os.environ.get("PATHS", "encode,rec,get,hash,deep,digest,queue,e2e").split(","))
+PATHS = set(os.environ.get("PATHS", "encode,geom,rec,get,hash,deep,digest,queue,e2e").split(","))
 REPS = int(os.environ.get("REPS", "10"))
 
 
@@ -81,6 +81,37 @@ if "encode" in PATHS:
                                                parity_stride=stride))
         out("encode_only", label, ms, nobj * (MiB + m * S), objects=nobj)
         del buf, sums
+        torch.cuda.empty_cache()
+
+# ---- the server's other default geometries (getDefaultParityBlocks,
+# cmd/format-erasure.go:870-881: set size 4..16 -> RS(2+2), (3+2), (3+3), (4+3), (4+4),
+# (5+4), ..., (12+4)): encode + sums, encode only, GET rebuild 2 and heal 2 at 4096 x 1 MiB
+# (PATHS=geom; GEOMS="6:4,10:4" selects)
+if "geom" in PATHS:
+    geoms = [tuple(int(x) for x in g.split(":")) for g in os.environ.get(
+        "GEOMS", "2:2,3:2,3:3,4:3,5:4,6:4,7:4,9:4,10:4,11:4").split(",")]
+    for k, m in geoms:
+        nobj = 4096
+        codec, buf, sums, S, stride = encoded(k, m, nobj, 11)
+        R = k + m
+        label = f"RS({k}+{m}) {nobj} x 1 MiB (default for {R}-drive sets)"
+        ms = timeit(lambda: codec.encode_batch(buf, stride, MiB, nobj, parity=buf, parity_offset=k * S,
+                                               parity_stride=stride, sums=sums))
+        out("encode_hash", label, ms, nobj * (MiB + m * S + 32 * R), objects=nobj)
+        ms = timeit(lambda: codec.encode_batch(buf, stride, MiB, nobj, parity=buf, parity_offset=k * S,
+                                               parity_stride=stride))
+        out("encode_only", label, ms, nobj * (MiB + m * S), objects=nobj)
+        vbad = torch.empty(nobj * R, dtype=torch.int32, device="cuda")
+        hsum = torch.empty_like(sums)
+        for erased, heal in (([0, 1], False), ([0, k], True)):
+            pres = [i not in erased for i in range(R)]
+            e = len(erased)
+            ms = timeit(lambda: codec.verify_reconstruct_batch(buf, stride, S, nobj, pres, not heal, sums, vbad,
+                                                               sums_out=hsum if heal else None))
+            out("verify_reconstruct", f"RS({k}+{m}) {nobj} x 1 MiB: verify {k} + rebuild {e}" +
+                (" + hash rebuilt (heal)" if heal else ""), ms,
+                nobj * (k * S + e * S + 32 * k + (32 * e if heal else 0)), objects=nobj, bad=int(vbad.sum()))
+        del buf, sums, vbad, hsum
         torch.cuda.empty_cache()
 
 # ---- reconstruct (ReconstructData / Reconstruct), BASELINE config 3 and RS(16+4)

@@ -1,5 +1,10 @@
-"""A/B of the GET / heal kernel launch shapes on one device (variant 0 = default,
-200 = small-workgroup launch), interleaved rounds."""
+"""A/B of GET / heal launches (product vs diagnostics variants) on 1 MiB stripes:
+verify the k survivors + rebuild e rows (+ hash them for heal), median of REPS launches,
+% of 8 TB/s on the algorithmic bytes k*S + e*S + 32*k (+ 32*e).
+
+  SHAPE=16:4:2048 VARIANTS=0,250,251 CASES="0,5;0,5,9,14;h3,17;h0,1,16,19" python scripts/get_ab.py
+(a case is a comma list of erased shards; a leading 'h' = heal)
+"""
 import contextlib
 import json
 import os
@@ -10,41 +15,46 @@ import torch  # noqa: E402
 
 import zs3server_amd as z  # noqa: E402
 
-
-def timeit(fn, steps=10):
-    fn()
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(steps):
-        fn()
-    e1.record()
-    torch.cuda.synchronize()
-    return e0.elapsed_time(e1) / steps
-
-
-k, m, blen, nobj = 8, 4, 1 << 20, 4096
-S = blen // k
-stride = (k + m) * S
-codec = z.Codec(k, m)
-buf = torch.empty(nobj * stride, dtype=torch.uint8, device="cuda")
-z.fill_batch(buf, stride, blen, nobj, seed=3)
-sums = torch.empty(nobj * (k + m) * 32, dtype=torch.uint8, device="cuda")
-codec.encode_batch(buf, stride, blen, nobj, parity=buf, parity_offset=k * S, parity_stride=stride, sums=sums)
-vbad = torch.empty(nobj * (k + m), dtype=torch.int32, device="cuda")
-hsum = torch.empty_like(sums)
-cases = [([], True, False, "verify 8"), ([0, 5], True, False, "verify 8 + rebuild 2"),
-         ([2, 10], False, True, "heal 1d+1p")]
-variants = [int(v) for v in os.environ.get("VARIANTS", "0,200").split(",")]
-for rnd in range(3):
-    for erased, data_only, heal, label in cases:
-        pres = [i not in erased for i in range(k + m)]
-        for v in variants:
+MiB = 1 << 20
+REPS = int(os.environ.get("REPS", "10"))
+k, m, n = (int(x) for x in os.environ.get("SHAPE", "16:4:2048").split(":"))
+VARIANTS = [int(v) for v in os.environ.get("VARIANTS", "0").split(",")]
+CASES = []
+for c in os.environ.get("CASES", "0,5;h3,17").split(";"):
+    heal = c.startswith("h")
+    CASES.append(([int(x) for x in c.lstrip("h").split(",")], heal))
+R = k + m
+S = -(-MiB // k)
+stride = R * S
+d = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
+z.fill_batch(d, stride, MiB, n, seed=3)
+sums = torch.zeros(n * R * 32, dtype=torch.uint8, device="cuda")
+z.Codec(k, m, MiB).encode_batch(d, stride, MiB, n, parity=d, parity_offset=k * S, parity_stride=stride, sums=sums)
+bad = torch.zeros(n * R, dtype=torch.int32, device="cuda")
+hs = torch.zeros_like(sums)
+st = torch.cuda.current_stream()
+for rnd in range(2):
+    for erased, heal in CASES:
+        pres = [i not in erased for i in range(R)]
+        e = len(erased) if heal else len([i for i in erased if i < k])
+        ab = n * (k * S + e * S + 32 * k + (32 * e if heal else 0))
+        for v in VARIANTS:
             with (z.diag(v) if v else contextlib.nullcontext()):
-                cv = z.Codec(k, m)  # a codec belongs to the library (product / diagnostics) that made it
-                ms = timeit(lambda: cv.verify_reconstruct_batch(buf, stride, S, nobj, pres, data_only, sums, vbad,
-                                                                sums_out=hsum if heal else None))
-            e = len(erased)
-            ab = nobj * (k * S + e * S + 32 * k + (32 * e if heal else 0))
-            print(json.dumps({"round": rnd, "case": label, "variant": v, "ms": round(ms, 4),
-                              "hbm_frac": round(ab / ms / 1e6 / 8000, 3), "bad": int(vbad.sum())}), flush=True)
+                c = z.Codec(k, m, MiB)
+
+                def f():
+                    c.verify_reconstruct_batch(d, stride, S, n, pres, not heal, sums, bad, sums_out=hs if heal else None)
+                f()
+                torch.cuda.synchronize()
+                ts = []
+                for _ in range(REPS):
+                    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    a.record(st)
+                    f()
+                    b.record(st)
+                    torch.cuda.synchronize()
+                    ts.append(a.elapsed_time(b))
+                ms = sorted(ts)[REPS // 2]
+                print(json.dumps({"round": rnd, "k": k, "m": m, "objects": n, "erased": erased, "heal": heal,
+                                  "variant": v, "ms": round(ms, 4), "frac": round(ab / (ms * 1e-3) / 8e12, 4),
+                                  "path": z.last_path(), "bad": int(bad.sum())}), flush=True)

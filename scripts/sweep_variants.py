@@ -43,7 +43,7 @@ for k, m, nobj in SHAPES:
         sig = (int(buf.view(torch.int64).sum()), int(sums.view(torch.int64).sum()))
         if ref is None:
             ref = sig
-        ok = sig == ref or v in (41, 42, 168, 169, 310, 311, 312)  # ablations are timing-only builds
+        ok = sig == ref or v in (41, 42, 168, 169) or 310 <= v <= 329  # ablations are timing-only builds
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(steps):

@@ -497,7 +497,8 @@ constexpr int ws_ts() {
 // WPE: minimum waves per SIMD the register allocation is sized for (3 = 168 VGPRs; 2 =
 // 256, for workgroups of at most 8 waves, one per CU).
 // TSP: LDS row stride rule (ws_ts).  ABL (timing-only diagnostics, output differs):
-// bit 0 = the pair-form hash waves XOR the words instead of running HighwayHash.
+// bit 0 = the pair-form hash waves XOR the words instead of running HighwayHash; bit 1 =
+// they skip their LDS reads; bit 2 = the encode waves skip their LDS writes.
 template <int K, int M, int G, int T, int PF, bool BUF = false, bool HQ = false, bool WT = false, int PM = 0,
           int CWX = 0, bool RING = false, int NTM = 0, bool STB = false, int EP = 0, int PFD = 0, bool UA = false,
           int WPE = 3, int TSP = 0, int ABL = 0>
@@ -670,8 +671,14 @@ k_ehx_ws(EncArgs a) {
             }
             const uint4* p = reinterpret_cast<const uint4*>(tile[(s - 1) & 1] + row_off) + hh;
             uint4 w[NPK];
+            if constexpr (ABL & 2) {
+                // timing ablation: no LDS reads (the words are the step number)
 #pragma unroll
-            for (int i = 0; i < NPK; ++i) w[i] = p[2 * i];
+                for (int i = 0; i < NPK; ++i) w[i] = make_uint4((uint32_t)s, (uint32_t)i, 0u, 0u);
+            } else {
+#pragma unroll
+                for (int i = 0; i < NPK; ++i) w[i] = p[2 * i];
+            }
             if constexpr (PM == 4) __builtin_amdgcn_s_setprio(3);
 #pragma unroll
             for (int i = 0; i < NPK; ++i) {
@@ -855,12 +862,16 @@ k_ehx_ws(EncArgs a) {
         } else {
             encode_dyadic<NWd, K, M, true, false, STB>(xs, par, tabs, const_tables(a.dtables));
         }
-        if constexpr (EP != 2 && EP != 3) {
+        if constexpr (ABL & 4) {
+            // timing ablation: no LDS writes (the hash waves read stale tiles)
+        } else {
+            if constexpr (EP != 2 && EP != 3) {
 #pragma unroll
-            for (int j = 0; j < K; ++j) st_col<NWd>(tl + col_off + j * TS, xs[j]);
+                for (int j = 0; j < K; ++j) st_col<NWd>(tl + col_off + j * TS, xs[j]);
+            }
+#pragma unroll
+            for (int r = 0; r < M; ++r) st_col<NWd>(tl + col_off + (K + r) * TS, par[r]);
         }
-#pragma unroll
-        for (int r = 0; r < M; ++r) st_col<NWd>(tl + col_off + (K + r) * TS, par[r]);
     };
     auto store_par = [&](const Col<NWd> (&par)[M], int64_t t0) {
 #pragma unroll

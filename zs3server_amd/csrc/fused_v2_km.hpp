@@ -137,6 +137,17 @@ static bool launch_ehx_km(int v, const EncArgs& a, hipStream_t s) {
         case 310: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, true, false, 0, false, 1, 0, false, 3, false, 0, 0, false, 3, 1, 1>(a, s); else return false;
         case 311: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, true, false, 0, false, 1, 0, false, 3, false, 9, 0, false, 3, 1, 0>(a, s); else return false;
         case 312: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, true, false, 0, false, 1, 0, false, 3, false, 9, 0, false, 3, 1, 1>(a, s); else return false;
+        // pure-memory ablations (no GF, no hash arithmetic) of other shapes / policies
+        case 320: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 2, true, false, 0, false, 1, 0, false, 3, false, 9, 0, false, 3, 1, 1>(a, s); else return false;
+        case 321: if constexpr (deep) return launch_ws_t<K, M, 16, 256, 1, true, false, 0, false, 1, 0, false, 3, false, 9, 0, false, 3, 1, 1>(a, s); else return false;
+        case 322: if constexpr (deep) return launch_ws_t<K, M, 8, 768, 1, true, false, 0, false, 1, 0, false, 3, false, 9, 0, false, 3, 1, 1>(a, s); else return false;
+        case 323: if constexpr (deep) return launch_ws_t<K, M, 8, 512, 1, true, false, 0, false, 1, 0, false, 3, false, 9, 0, false, 3, 1, 1>(a, s); else return false;
+        case 324: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, true, false, 0, false, 1, 0, false, 0, false, 9, 0, false, 3, 1, 1>(a, s); else return false;
+        case 325: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, true, false, 0, false, 1, 0, false, 1, false, 9, 0, false, 3, 1, 1>(a, s); else return false;
+        case 326: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, true, false, 0, false, 1, 0, false, 2, false, 9, 0, false, 3, 1, 1>(a, s); else return false;
+        case 327: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, true, false, 0, false, 1, 0, false, 3, false, 9, 0, false, 3, 1, 3>(a, s); else return false;
+        case 328: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, true, false, 0, false, 1, 0, false, 3, false, 9, 0, false, 3, 1, 7>(a, s); else return false;
+        case 329: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 2, true, false, 0, false, 1, 0, false, 3, false, 9, 0, false, 3, 1, 7>(a, s); else return false;
         default: return false;
     }
 }

@@ -69,11 +69,12 @@ __global__ void __launch_bounds__(2 * NT) k_split(uint8_t* buf, int64_t stride, 
 // k_split with PF tiles of loads in flight (a register ring, unrolled by PF so every
 // register keeps its slot; the loader waves issue no stores, so the compiler's waits are
 // exact) and NW workgroups' worth of stripes per launch row.
-template <int G, int NT, int PF>
+template <int G, int NT, int PF, int SM = 0>
 __global__ void __launch_bounds__(2 * NT) k_split_pf(uint8_t* buf, int64_t stride, int64_t rs) {
     constexpr int CPB = NT / G;
     constexpr int T = CPB * 16;
-    constexpr int64_t NST = S0 / T / PF * PF;  // whole PF-groups of full tiles
+    constexpr int64_t NST = S0 / T / 4 * 4;  // whole groups of 4 full tiles (PF and SM 2 / 4 divide it)
+    constexpr int NB = SM >= 100 ? SM - 100 + 2 : SM >= 2 ? 2 * SM : 2;  // parity tiles in the LDS ring
     constexpr int PT = G * M * T;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int tid = threadIdx.x;
@@ -92,7 +93,7 @@ __global__ void __launch_bounds__(2 * NT) k_split_pf(uint8_t* buf, int64_t strid
 #pragma unroll
             for (int p = 0; p < PF; ++p) {
                 const int64_t s = s0 + p;
-                u4* tl = pt + (s & 1) * (PT / 16) + slot;
+                u4* tl = pt + (s % NB) * (PT / 16) + slot;
 #pragma unroll
                 for (int r = 0; r < M; ++r) tl[r * (T / 16)] = x[p][2 * r] ^ x[p][2 * r + 1];
                 if (s + PF < NST) {
@@ -103,11 +104,34 @@ __global__ void __launch_bounds__(2 * NT) k_split_pf(uint8_t* buf, int64_t strid
             }
         }
     } else {
+        // storer lane mapping for batched stores: SM consecutive tiles of one parity row are
+        // stored as one contiguous run (lane q of the stripe covers 16 B of the run)
         for (int64_t s = 0; s < NST; ++s) {
             __syncthreads();
-            const u4* tl = pt + (s & 1) * (PT / 16) + slot;
+            if constexpr (SM == 0) {
+                const u4* tl = pt + (s % NB) * (PT / 16) + slot;
 #pragma unroll
-            for (int r = 0; r < M; ++r) st_nt(base + (K + r) * rs + s * T, tl[r * (T / 16)]);
+                for (int r = 0; r < M; ++r) st_nt(base + (K + r) * rs + s * T, tl[r * (T / 16)]);
+            } else if constexpr (SM >= 100) {
+                constexpr int D = SM - 100;
+                for (int64_t tt = (s >= D ? s - D : NST); tt <= s - D || (s == NST - 1 && tt < NST); ++tt) {
+                    const u4* tl = pt + (tt % NB) * (PT / 16) + slot;
+#pragma unroll
+                    for (int r = 0; r < M; ++r) st_nt(base + (K + r) * rs + tt * T, tl[r * (T / 16)]);
+                }
+            } else if constexpr (SM >= 2) {
+                if ((s % SM) == SM - 1) {
+                    const int64_t s0 = s - (SM - 1);
+#pragma unroll
+                    for (int u = 0; u < SM; ++u) {
+                        // run byte offset u*T + o within the SM*T-byte run of row r
+                        const int64_t tt = s0 + u;
+                        const u4* tl = pt + (tt % NB) * (PT / 16) + slot;
+#pragma unroll
+                        for (int r = 0; r < M; ++r) st_nt(base + (K + r) * rs + tt * T, tl[r * (T / 16)]);
+                    }
+                }
+            }
         }
     }
 }
@@ -205,16 +229,30 @@ static void stream(uint8_t* d, int64_t rowpad, int64_t skew) {
     timeit(nm, [&] { hipLaunchKernelGGL((k_stream<NT>), dim3(S0 / (NT * 16), NOBJ), dim3(NT), 0, 0, d, stride, rs); });
 }
 
-template <int G, int NT, int PF>
+template <int G, int NT, int PF, int SM = 0>
 static void splitpf(uint8_t* d, int lds) {
     constexpr int T = NT * 16 / G;
-    const int need = 2 * G * M * T;
+    constexpr int NB = SM >= 100 ? SM - 100 + 2 : SM >= 2 ? 2 * SM : 2;
+    const int need = NB * G * M * T;
     const int dyn = need > lds ? need : lds;
     if (dyn > 163840 || 2 * NT > 1024) return;
-    (void)hipFuncSetAttribute((const void*)k_split_pf<G, NT, PF>, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
+    (void)hipFuncSetAttribute((const void*)k_split_pf<G, NT, PF, SM>, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
     char nm[160];
-    snprintf(nm, sizeof nm, "splitpf G%d T%d NT%d PF%d lds%dK", G, T, NT, PF, dyn >> 10);
-    timeit(nm, [&] { hipLaunchKernelGGL((k_split_pf<G, NT, PF>), dim3(NOBJ / G), dim3(2 * NT), dyn, 0, d, R * S0, S0); });
+    snprintf(nm, sizeof nm, "splitpf G%d T%d NT%d PF%d stores%s lds%dK", G, T, NT, PF,
+             SM == 0 ? "each" : SM == 1 ? "none" : SM == 2 ? "batch2" : SM == 4 ? "batch4" : SM == 104 ? "delay4" : "delay8",
+             dyn >> 10);
+    timeit(nm, [&] { hipLaunchKernelGGL((k_split_pf<G, NT, PF, SM>), dim3(NOBJ / G), dim3(2 * NT), dyn, 0, d, R * S0, S0); });
+}
+
+// stream without stores (the read half of the traffic alone)
+template <int NT>
+__global__ void __launch_bounds__(NT) k_stream_ro(uint8_t* buf, int64_t stride, int64_t rs) {
+    uint8_t* base = buf + (int64_t)blockIdx.y * stride + ((int64_t)blockIdx.x * NT + threadIdx.x) * 16;
+    u4 x[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) x[j] = ld_nt(base + j * rs);
+    u4 a = x[0] ^ x[1] ^ x[2] ^ x[3] ^ x[4] ^ x[5] ^ x[6] ^ x[7];
+    if (a.x == 0x9E3779B9u && a.y == 0x7F4A7C15u) buf[0] = 1;  // keep the loads
 }
 
 template <int NT, int SPAN>
@@ -233,32 +271,15 @@ int main() {
     const int ONE = 96 << 10;  // one workgroup per CU
     stream<256>(d, 0, 0);
     timeit("stream transposed NT256", [&] { hipLaunchKernelGGL((k_stream_t<256>), dim3(NOBJ, S0 / 4096), dim3(256), 0, 0, d, R * S0, S0); });
-    splitpf<16, 384, 1>(d, 96 << 10);
-    splitpf<16, 384, 2>(d, 96 << 10);
-    splitpf<16, 384, 3>(d, 96 << 10);
-    splitpf<16, 512, 2>(d, 96 << 10);
-    splitpf<16, 256, 2>(d, 96 << 10);
-    splitpf<16, 256, 3>(d, 96 << 10);
-    splitpf<8, 256, 2>(d, 0);
-    splitpf<8, 256, 3>(d, 0);
-    splitpf<4, 128, 2>(d, 0);
-    splitpf<4, 128, 4>(d, 0);
-    splitpf<16, 384, 2>(d, 0);
+    timeit("stream no stores NT256 (read bytes only)", [&] { hipLaunchKernelGGL((k_stream_ro<256>), dim3(S0 / 4096, NOBJ), dim3(256), 0, 0, d, R * S0, S0); });
+    splitpf<16, 384, 2, 0>(d, 96 << 10);
+    splitpf<16, 384, 2, 104>(d, 96 << 10);
+    splitpf<8, 384, 2, 104>(d, 96 << 10);
+    splitpf<8, 384, 2, 108>(d, 96 << 10);
+    splitpf<8, 384, 2, 0>(d, 96 << 10);
     // the product's memory shape: 16 stripes, 384-byte tiles, 6 loading waves (+6 storing)
     split<16, 384>(d, 0, 0, ONE);
-    split<16, 384>(d, 128, 0, ONE);
-    split<16, 384>(d, 256, 0, ONE);
-    split<16, 384>(d, 512, 0, ONE);
-    split<16, 384>(d, 4096, 0, ONE);
-    split<16, 384>(d, 0, 4096, ONE);
-    split<16, 384>(d, 0, 65536, ONE);
-    split<16, 384>(d, 0, 1 << 19, ONE);
-    split<8, 384>(d, 0, 0, ONE);
-    split<8, 384>(d, 256, 0, ONE);
-    split<4, 256>(d, 0, 0, ONE);
-    split<4, 256>(d, 256, 0, ONE);
-    split<16, 384>(d, 0, 0, 0);
-    split<16, 384>(d, 256, 0, 0);
+
     stream<256>(d, 0, 0);
     (void)hipFree(d);
     return 0;

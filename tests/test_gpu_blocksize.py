@@ -98,7 +98,8 @@ def test_legacy_block_get_heal(oracle, k, m, erased, heal):
     z.Codec(k, m, BS1).verify_reconstruct_batch(d, R * S, S, nb, [i not in erased for i in range(R)], not heal,
                                                  exp, bad, sums_out=out)
     torch.cuda.synchronize()
-    assert z.last_path() == 2, z.last_path()
+    # the fused GET kernel, or for a batch this small (96 stripes) the latency-regime path
+    assert z.last_path() in (2, 4), z.last_path()
     want_bad = np.zeros((nb, R), np.int32)
     want_bad[bad_blk, bad_row] = 1
     assert np.array_equal(bad.cpu().numpy(), want_bad)

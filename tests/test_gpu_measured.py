@@ -427,3 +427,40 @@ def test_encode_only_unaligned_rows(oracle, k, m, blen):
         want = oracle.encode_data(k, m, oracle.fill(k * 7 + m, b, blen), mat).reshape(-1)
         assert np.array_equal(host[b, k * S:], want[k * S:]), f"parity, block {b}"
         assert np.array_equal(host[b, :blen], want[:blen]), f"data, block {b}"
+
+
+GEN_GEOMS = [(2, 2), (3, 2), (3, 3), (4, 3), (5, 4), (6, 4), (7, 4), (9, 4), (10, 4), (11, 4)]
+
+
+@pytest.mark.parametrize("nb", [1024, 1031])
+@pytest.mark.parametrize("k,m", GEN_GEOMS, ids=lambda v: str(v))
+def test_default_geometries_ws_encode(oracle, k, m, nb):
+    """The server's non-dyadic default geometries (getDefaultParityBlocks,
+    cmd/format-erasure.go:870-881: 4-7 and 9-15-drive sets) on the warp-specialised
+    kernel with a general coding matrix (fused_v2_gen.hip, round 4): 1 MiB blocks, Split
+    padding poisoned in memory, a last workgroup with dead stripes (nb = 1031), every
+    parity byte and bitrot sum vs cpu_ref, two blocks vs the scalar oracle."""
+    R = k + m
+    S = -(-MiB // k)
+    codec = z.Codec(k, m, MiB)
+    d = torch.zeros(nb * R * S, dtype=torch.uint8, device=DEV)
+    z.fill_batch(d, R * S, MiB, nb, seed=k * 31 + m, obj0=0)
+    if k * S > MiB:
+        d.view(nb, R * S)[:, MiB:k * S] = 0xEE
+    sums = torch.zeros(nb * R * 32, dtype=torch.uint8, device=DEV)
+    codec.encode_batch(d, R * S, MiB, nb, parity=d, parity_offset=k * S, parity_stride=R * S, sums=sums)
+    torch.cuda.synchronize()
+    assert z.last_path() == 2, "warp-specialised kernel (general matrix)"
+    mat = oracle.build_matrix(k, m)
+    host = d.cpu().numpy().reshape(nb, R * S)
+    hs = sums.cpu().numpy()
+    par = np.empty(nb * m * S, np.uint8)
+    sref = np.empty(nb * R * 32, np.uint8)
+    cpuref.encode_hash(k, m, mat, np.ascontiguousarray(host), MiB, nb, R * S, par, m * S, sref, KEY,
+                       cpuref.threads_available())
+    assert np.array_equal(host[:, k * S:], par.reshape(nb, m * S)), "parity"
+    assert np.array_equal(hs, sref), "sums"
+    for b in (0, nb - 1):
+        want = oracle.encode_data(k, m, oracle.fill(k * 31 + m, b, MiB), mat)
+        assert np.array_equal(host[b, k * S:].reshape(m, S), want[k:]), b
+        assert np.array_equal(hs[b * R * 32:(b + 1) * R * 32].reshape(R, 32), oracle.hh256_rows(KEY, want)), b

@@ -440,7 +440,8 @@ __global__ void __launch_bounds__(4 * G * (K + M)) __attribute__((amdgpu_waves_p
 // pad quads hash a real row and discard the digest.
 template <int K, int M, int G, int T, bool HQ>
 constexpr int ws_nh() {
-    return HQ ? ((4 * G * (K + M) + 63) / 64) * 64 : 2 * G * (K + M);
+    // whole wavefronts; pad pairs / quads past G*(K+M) chains hash a real row and discard it
+    return HQ ? ((4 * G * (K + M) + 63) / 64) * 64 : ((2 * G * (K + M) + 63) / 64) * 64;
 }
 // Encode column width: 16 bytes, 8 for K > 8 (16 rows of 16-byte columns do not fit
 // the 168-VGPR budget beside the encode's working set).
@@ -496,12 +497,14 @@ constexpr int ws_ts() {
 // and everything past the row read as zero, and stores only the parity bytes below S.
 // WPE: minimum waves per SIMD the register allocation is sized for (3 = 168 VGPRs; 2 =
 // 256, for workgroups of at most 8 waves, one per CU).
+// GEN: any M x K coding matrix (the server's non-power-of-two geometries, not dyadic): the
+// encode role multiplies every data row into every parity row (encode_general, a.tables).
 // TSP: LDS row stride rule (ws_ts).  ABL (timing-only diagnostics, output differs):
 // bit 0 = the pair-form hash waves XOR the words instead of running HighwayHash; bit 1 =
 // they skip their LDS reads; bit 2 = the encode waves skip their LDS writes.
 template <int K, int M, int G, int T, int PF, bool BUF = false, bool HQ = false, bool WT = false, int PM = 0,
           int CWX = 0, bool RING = false, int NTM = 0, bool STB = false, int EP = 0, int PFD = 0, bool UA = false,
-          int WPE = 3, int TSP = 0, int ABL = 0>
+          int WPE = 3, int TSP = 0, int ABL = 0, bool GEN = false>
 __global__ void __launch_bounds__((ws_nh<K, M, G, T, HQ>() + G * (T / ws_cwe<K, CWX>()))) __attribute__((amdgpu_waves_per_eu(WPE)))
 k_ehx_ws(EncArgs a) {
     constexpr int R = K + M;
@@ -512,8 +515,8 @@ k_ehx_ws(EncArgs a) {
     constexpr int NT = NH + NE;
     constexpr int TS = ws_ts<T, HQ, TSP>();
     constexpr int NPK = T / 32;
-    constexpr int NTAB = K * 8;
-    static_assert(M == 2 || M == 4, "dyadic shapes only");
+    constexpr int NTAB = GEN ? M * K * 8 : K * 8;
+    static_assert(GEN || M == 2 || M == 4, "dyadic shapes only (GEN: any M x K matrix)");
     static_assert(NH % 64 == 0 && NE % 64 == 0 && T % 32 == 0, "whole wavefronts per role");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_dyn[];
     uint8_t(*tile)[G * R * TS] = reinterpret_cast<uint8_t(*)[G * R * TS]>(smem_dyn);
@@ -526,7 +529,7 @@ k_ehx_ws(EncArgs a) {
     const int tid = threadIdx.x;
     const int64_t blk0 = (int64_t)blockIdx.x * G;
     const int64_t S = a.S;
-    for (int i = tid; i < NTAB; i += NT) tabs[i] = a.dtables[i];
+    for (int i = tid; i < NTAB; i += NT) tabs[i] = GEN ? a.tables[i] : a.dtables[i];
     if (RING && tid < 4) ring[tid] = 0;
     const int64_t nfull = S / T;
     const int tail = (int)(S - nfull * T);  // multiple of 16 unless UA
@@ -612,7 +615,10 @@ k_ehx_ws(EncArgs a) {
     }
     if (!HQ && __builtin_amdgcn_readfirstlane(tid) < NH) {
         // ---- hash role: lanes (2hh, 2hh+1) of chain `chain` = shard row s of stripe g
-        const int chain = tid >> 1, hh = tid & 1;
+        // (pad pairs past the G*R chains of a workgroup hash chain - G*R and discard it)
+        const int chain0 = tid >> 1, hh = tid & 1;
+        const bool hpad = chain0 >= G * R;
+        const int chain = hpad ? chain0 - G * R : chain0;
         const int row_off = chain * TS;
         HHPair st = hh2_init(hh, a.key[0], a.key[1], a.key[2], a.key[3]);
         bar();  // tables (matches the encode role)
@@ -637,7 +643,7 @@ k_ehx_ws(EncArgs a) {
             }
             uint64_t d0, d1;
             hh2_finalize256(st, d0, d1);
-            if (blk0 + chain / R < a.n_blocks) {
+            if (!hpad && blk0 + chain / R < a.n_blocks) {
                 const int64_t bb = blk0 + chain / R;
                 uint64_t* out = reinterpret_cast<uint64_t*>(a.sums + (bb * R + chain % R) * 32 + 16 * hh);
                 out[0] = d0;
@@ -702,16 +708,17 @@ k_ehx_ws(EncArgs a) {
             }
             bar();
         }
+        // the L2 prefetches have all retired before the tail code may reuse the sink register
+        if constexpr (PFD > 0) asm volatile("s_waitcnt vmcnt(0)" : "+v"(sink)::"memory");
         if (tail) {
             const uint8_t* row = tile[nfull & 1] + row_off;
             hh2_packets(st, row, tail >> 5, hh);
             if (tail & 31) hh2_remainder(st, row + (tail & ~31), (uint32_t)(tail & 31), hh);
         }
         for (int64_t s = nfull + 1; s < total; ++s) bar();
-        if constexpr (PFD > 0) asm volatile("s_waitcnt vmcnt(0)" : "+v"(sink)::"memory");
         uint64_t d0, d1;
         hh2_finalize256(st, d0, d1);
-        if (blk0 + chain / R < a.n_blocks) {
+        if (!hpad && blk0 + chain / R < a.n_blocks) {
             const int64_t bb = blk0 + chain / R;
             uint64_t* out = reinterpret_cast<uint64_t*>(a.sums + (bb * R + chain % R) * 32 + 16 * hh);
             out[0] = d0;
@@ -828,7 +835,13 @@ k_ehx_ws(EncArgs a) {
         Col<NWd> xs[K];
 #pragma unroll
         for (int j = 0; j < K; ++j) xs[j] = to_col<NWd>(xr[j]);
-        if constexpr (EP == 9) {
+        if constexpr (GEN) {
+            // general M x K matrix: the data rows go to LDS first (they drain under the
+            // products), then every parity row from all K data rows
+#pragma unroll
+            for (int j = 0; j < K; ++j) st_col<NWd>(tl + col_off + j * TS, xs[j]);
+            encode_general<NWd, K, M>(xs, par, tabs);
+        } else if constexpr (EP == 9) {
             // timing ablation (diagnostics only; output differs): no GF arithmetic
 #pragma unroll
             for (int r = 0; r < M; ++r)
@@ -865,7 +878,7 @@ k_ehx_ws(EncArgs a) {
         if constexpr (ABL & 4) {
             // timing ablation: no LDS writes (the hash waves read stale tiles)
         } else {
-            if constexpr (EP != 2 && EP != 3) {
+            if constexpr (EP != 2 && EP != 3 && !GEN) {
 #pragma unroll
                 for (int j = 0; j < K; ++j) st_col<NWd>(tl + col_off + j * TS, xs[j]);
             }
@@ -976,16 +989,17 @@ k_ehx_ws(EncArgs a) {
 
 template <int K, int M, int G, int T, int PF, bool BUF = false, bool HQ = false, int LDSMIN = 0, bool WT = false,
           int PM = 0, int CWX = 0, bool RING = false, int NTM = 0, bool STB = false, int EP = 0, int PFD = 0,
-          bool UA = false, int WPE = 3, int TSP = 0, int ABL = 0>
+          bool UA = false, int WPE = 3, int TSP = 0, int ABL = 0, bool GEN = false>
 static bool launch_ws_t(const EncArgs& a, hipStream_t s) {
     constexpr int R = K + M;
     constexpr int NT = ws_nh<K, M, G, T, HQ>() + G * (T / ws_cwe<K, CWX>());
     constexpr size_t tiles = (size_t)2 * G * R * ws_ts<T, HQ, TSP>();
     constexpr size_t dyn = tiles > (size_t)LDSMIN ? tiles : (size_t)LDSMIN;
-    if constexpr (dyn + K * 32 > 163840 || NT > 1024) {
+    if constexpr (dyn + (GEN ? M * K : K) * 32 > 163840 || NT > 1024) {
         return false;
     } else {
-        if (a.dyb != M) return false;
+        if (!GEN && a.dyb != M) return false;
+        if (a.k != K || a.m != M) return false;
         if constexpr (UA) {
             // the Split padding (n .. k*S) must lie in the last data row's tail tile
             const int64_t tail = a.S % T;
@@ -996,7 +1010,7 @@ static bool launch_ws_t(const EncArgs& a, hipStream_t s) {
         if (BUF && ((G - 1) * a.data_stride + K * a.S > 0x7FFFFFFF ||
                     (G - 1) * a.parity_stride + M * a.S > 0x7FFFFFFF || a.data_stride < 0 || a.parity_stride < 0))
             return false;
-        auto kern = k_ehx_ws<K, M, G, T, PF, BUF, HQ, WT, PM, CWX, RING, NTM, STB, EP, PFD, UA, WPE, TSP, ABL>;
+        auto kern = k_ehx_ws<K, M, G, T, PF, BUF, HQ, WT, PM, CWX, RING, NTM, STB, EP, PFD, UA, WPE, TSP, ABL, GEN>;
         if (ensure_dyn_lds((const void*)kern, dyn) != hipSuccess) return false;
         const int64_t grid = (a.n_blocks + G - 1) / G;
         hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), dyn, s, a);

@@ -286,6 +286,61 @@ __device__ __forceinline__ void encode_dyadic(const Col<NWd> (&x)[K], Col<NWd> (
     encode_dyadic_f<NWd, K, M, SB, PRS, ST>([&](int j) { return x[j]; }, out, dtabs, ctabs);
 }
 
+// General (non-dyadic) encode of one column: out[r] = sum_j M[r][j] * x[j] over GF(2^8),
+// the coefficient tables of parity row r, data row j at tabs[(r*K + j)*8] (LDS, read with
+// wave-uniform addresses: broadcast, no bank conflicts).  Each data dword is nibble-split
+// once and multiplied into all M rows (3 v_perm per product, folded with XOR3); the
+// server's non-power-of-two geometries (RS(6+4), RS(10+4), RS(3+3), ...) are not dyadic,
+// so every parity row needs its K products.
+// An SGPR zero that depends on `v`: table reads addressed with it cannot be issued before
+// v is computed (an opaque base alone does not stop the compiler from clustering every
+// table read of a long unrolled sequence at its start).
+__device__ __forceinline__ int opaque_zero_after(uint32_t v) {
+    int z = 0;
+    asm volatile("" : "+s"(z) : "v"(v));
+    return z;
+}
+
+template <int NWd, int K, int M>
+__device__ __forceinline__ void encode_general(const Col<NWd> (&x)[K], Col<NWd> (&out)[M], const uint32_t* tabs) {
+    GfAcc acc[M][NWd];
+#pragma unroll
+    for (int r = 0; r < M; ++r)
+#pragma unroll
+        for (int w = 0; w < NWd; ++w) acc_init(acc[r][w]);
+    // the M tables of data row j+1 are read while row j's products run (issued right after
+    // row j's nibble split, which their opaque base depends on): two rows of tables live,
+    // where letting the compiler cluster all M*K reads spilled 338 VGPRs for RS(10+4)
+    CoefTab tn[M];
+    {
+        const uint32_t* tb = tabs + opaque_zero();
+#pragma unroll
+        for (int r = 0; r < M; ++r) tn[r] = load_coef(tb, r * K);
+    }
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        CoefTab t[M];
+#pragma unroll
+        for (int r = 0; r < M; ++r) t[r] = tn[r];
+        Nib n[NWd];
+#pragma unroll
+        for (int w = 0; w < NWd; ++w) n[w] = split_nibbles(x[j].w[w]);
+        if (j + 1 < K) {
+            const uint32_t* tb = tabs + opaque_zero_after(n[0].a);
+#pragma unroll
+            for (int r = 0; r < M; ++r) tn[r] = load_coef(tb, r * K + j + 1);
+        }
+#pragma unroll
+        for (int r = 0; r < M; ++r)
+#pragma unroll
+            for (int w = 0; w < NWd; ++w) acc_add(acc[r][w], gf_lookup(n[w], t[r]));
+    }
+#pragma unroll
+    for (int r = 0; r < M; ++r)
+#pragma unroll
+        for (int w = 0; w < NWd; ++w) out[r].w[w] = acc_done(acc[r][w]);
+}
+
 // Scalar GF multiply with log/exp tables (generic byte path).
 __device__ __forceinline__ uint8_t gf_mul_log(const uint8_t* lg, const uint8_t* ex, uint8_t a, uint8_t b) {
     return (a && b) ? ex[(int)lg[a] + (int)lg[b]] : (uint8_t)0;

@@ -1550,6 +1550,17 @@ bool has_fast_encode(int k, int m) {
 hipError_t launch_encode(const EncArgs& a, hipStream_t s, int* path) {
     if (path) *path = PATH_NONE;
     if (a.n_blocks <= 0 || a.S <= 0) return hipSuccess;
+    // The server's non-dyadic default geometries (RS(6+4), RS(10+4), RS(3+3), ... and
+    // RS(2+2) / RS(4+3)) on the warp-specialised kernel with a general matrix
+    // (fused_v2_gen.hip) once the batch fills the chip (a workgroup takes 8-16 stripes);
+    // smaller batches keep the latency-bound paths below.
+    if (a.sums && a.variant == 0 && a.n_blocks >= 1024 && has_gen_encode(a.k, a.m)) {
+        const int p = launch_ehx_gen(a, s);
+        if (p != PATH_NONE) {
+            if (path) *path = p;
+            return hipGetLastError();
+        }
+    }
     // Vectorised kernels: 16-byte shard columns and no Split padding.
     const bool vec_ok = (a.S % 16) == 0 && a.n == (int64_t)a.k * a.S;
 #define X(K, M)                                  \

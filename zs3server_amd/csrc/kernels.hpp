@@ -158,6 +158,11 @@ int launch_ehx(int v, const EncArgs& a, hipStream_t s);
 // Fused encode + sums for shard sizes that are not a multiple of 16 (k_ehx_ws UA mode,
 // e.g. RS(12+4) on 1 MiB blocks); PATH_NONE when the shape has no such instance.
 int launch_ehx_ua(const EncArgs& a, hipStream_t s);
+// The same kernel for the server's non-dyadic default geometries (fused_v2_gen.hip: a
+// general M x K matrix in the encode role); PATH_NONE when (k, m) has no instance or the
+// layout does not fit.
+int launch_ehx_gen(const EncArgs& a, hipStream_t s);
+bool has_gen_encode(int k, int m);
 // LDS-DMA fused encode (fused_dma.hip); PATH_NONE when the shape / layout does not fit.
 int launch_ehx_dma(int v, const EncArgs& a, hipStream_t s);
 // Warp-specialised GET / heal pass (fused_v2.hip); false if the shape has no instance.

@@ -464,3 +464,60 @@ def test_default_geometries_ws_encode(oracle, k, m, nb):
         want = oracle.encode_data(k, m, oracle.fill(k * 31 + m, b, MiB), mat)
         assert np.array_equal(host[b, k * S:].reshape(m, S), want[k:]), b
         assert np.array_equal(hs[b * R * 32:(b + 1) * R * 32].reshape(R, 32), oracle.hh256_rows(KEY, want)), b
+
+
+def _gen_get_cases():
+    cases = []
+    for k, m in GEN_GEOMS:
+        R = k + m
+        e = min(m, 4)
+        # every parity row + the lowest data rows lost, healed; two data rows rebuilt
+        cases.append((k, m, sorted(list(range(k, R))[: e - 1] + [0]), True))
+        cases.append((k, m, [k // 2, k - 1] if k > 2 else [0, 1], False))
+    cases += [(5, 4, [1], False), (11, 4, [2, 12, 13], False), (3, 3, [1], True), (2, 2, [3], True)]
+    return cases
+
+
+@pytest.mark.parametrize("k,m,erased,heal", _gen_get_cases(), ids=lambda v: str(v))
+def test_default_geometries_ws_get_heal(oracle, k, m, erased, heal):
+    """GET / heal of the non-dyadic server-default geometries on the warp-specialised
+    k_vr_ws (fused_v2_get_gen.hip, round 4; UA mode for every k but 2): 1 MiB blocks,
+    1031 stripes (a last workgroup with dead stripes) tiled from 61 distinct oracle
+    stripes, one rotted survivor flagged exactly, every rebuilt byte and heal sum vs the
+    oracle, survivors and lost parity (ReconstructData) untouched."""
+    R = k + m
+    nb = 1031
+    base, bsum, idx = _tiled_stripes(oracle, k, m, MiB, nb, seed=k * 13 + m)
+    S = base.shape[2]
+    codec = z.Codec(k, m, MiB)
+    ref = torch.from_numpy(base).to(DEV)
+    refs = torch.from_numpy(bsum).to(DEV)
+    d = ref[idx].contiguous()
+    for e in erased:
+        d[:, e, :] = 0x5A
+    surv = [i for i in range(R) if i not in erased][:k]
+    bad_blk, bad_row = nb - 2, surv[-1]
+    d[bad_blk, bad_row, S - 1] ^= 0x10
+    exp = refs[idx].contiguous()
+    bad = torch.full((nb, R), 7, dtype=torch.int32, device=DEV)
+    out = torch.zeros((nb, R, 32), dtype=torch.uint8, device=DEV) if heal else None
+    codec.verify_reconstruct_batch(d, R * S, S, nb, [i not in erased for i in range(R)], not heal, exp, bad,
+                                   sums_out=out)
+    torch.cuda.synchronize()
+    if k != 4:
+        assert z.last_path() == 2, z.last_path()
+    want_bad = np.zeros((nb, R), np.int32)
+    want_bad[bad_blk, bad_row] = 1
+    assert np.array_equal(bad.cpu().numpy(), want_bad)
+    ok = torch.ones(nb, dtype=torch.bool, device=DEV)
+    ok[bad_blk] = False
+    for i in erased:
+        if i < k or heal:
+            assert bool((d[:, i, :] == ref[idx, i, :]).all(dim=1)[ok].all()), f"rebuilt shard {i}"
+            if heal:
+                assert bool((out[:, i, :] == refs[idx, i, :]).all(dim=1)[ok].all()), f"heal sum {i}"
+        else:
+            assert bool((d[:, i, :] == 0x5A).all())
+    for i in range(R):
+        if i not in erased:
+            assert bool((d[:, i, :] == ref[idx, i, :]).all(dim=1)[ok].all()), f"survivor {i}"

@@ -33,7 +33,7 @@ def test_untracked_loads_never_touched_in_flight(tmp_path, diag):
     # fused_dma.hip (product and diagnostics) issues its loads with global_load_lds_*: the data
     # goes straight to LDS, no VGPR is a load destination, so the VGPR dataflow check does not
     # apply; it is compiled here for the SGPR-hazard check all the same.
-    units = ["fused_v2.hip", "fused_v2_gen.hip", "fused_v2_get.hip", "fused_dma.hip"] + (
+    units = ["fused_v2.hip", "fused_v2_gen.hip", "fused_v2_get.hip", "fused_v2_get_gen.hip", "fused_dma.hip"] + (
         ["fused_v2_get_diag.hip", "fused_v2_get_diag4.hip", "fused_v2_get_diag8.hip", "fused_v2_get_diag16.hip",
          "fused_v2_km84.hip", "fused_v2_km42.hip", "fused_v2_km164.hip", "fused_v2_km124.hip"] if diag else [])
     procs = []

@@ -1268,9 +1268,11 @@ k_vr_ws(VrArgs a) {
             const ctab_ptr tg = const_tables(a.tables) + opaque_zero();
             constexpr int NB = BT > 0 ? BT : 4;  // BT: coefficients per scalar batch
             CoefTab tbat[2][NB];
+            // (a batch may straddle two rebuilt rows; the last one re-reads table EX*K-1
+            // for its slots past the end)
             auto load_batch = [&](CoefTab (&d)[NB], int c0) {
 #pragma unroll
-                for (int i = 0; i < NB; ++i) d[i] = load_coef_s(tg, c0 + i);
+                for (int i = 0; i < NB; ++i) d[i] = load_coef_s(tg, c0 + i < EX * K ? c0 + i : EX * K - 1);
             };
             // BT: consume batch d (the wait for its scalar loads sits here), then issue the
             // next batch's loads, then compute; the scheduling barriers keep that order
@@ -1280,10 +1282,7 @@ k_vr_ws(VrArgs a) {
                     asm volatile("" ::"s"(d[i].ab.x), "s"(d[i].ab.y), "s"(d[i].ab.z), "s"(d[i].ab.w), "s"(d[i].c));
                 __builtin_amdgcn_sched_barrier(0);
             };
-            if constexpr (ST && BT) {
-                static_assert(K % NB == 0, "whole batches per rebuilt row");
-                load_batch(tbat[0], 0);
-            }
+            if constexpr (ST && BT) load_batch(tbat[0], 0);
 #pragma unroll
             for (int r = 0; r < EX; ++r) {
                 GfAcc acc[NWd];

@@ -1830,6 +1830,13 @@ static hipError_t run_vr_k(const VrArgs& a, hipStream_t s, int* path) {
 hipError_t launch_verify_reconstruct(const VrArgs& a, hipStream_t s, int* path) {
     if (path) *path = PATH_NONE;
     if (a.n_blocks <= 0 || a.S <= 0) return hipSuccess;
+    // Server-default geometries whose k is not 4, 8, 12 or 16 (RS(2+2), (3+2), (5+4),
+    // (6+4), ...; fused_v2_get_gen.hip): rebuild / heal on the warp-specialised kernel
+    // in one launch (4096 x 1 MiB: see that file); small batches keep the launches below
+    if (a.variant == 0 && a.e >= 1 && a.e <= 4 && a.n_blocks >= 1024 && launch_vr_ws_gen(a, s)) {
+        if (path) *path = PATH_WS;
+        return hipGetLastError();
+    }
     if (a.e <= 4 && (a.S % 16) == 0) {
         switch (a.k) {
             case 2: return run_vr_k<2>(a, s, path);

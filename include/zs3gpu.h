@@ -203,6 +203,18 @@ int zs3_md5_batch(const uint8_t* d_msgs, int64_t msg_stride, int64_t msg_len, co
 int zs3_sha256_batch(const uint8_t* d_msgs, int64_t msg_stride, int64_t msg_len, const int64_t* d_lens,
                      int64_t n_msgs, uint8_t* d_out, void* stream);
 
+/* Independent messages of any lengths at any offsets in one launch (the parts of
+ * multipart uploads: PutObjectPartHandler, cmd/object-handlers.go:2753, wraps each
+ * part in hash.NewReader, :2919, for its ETag and content SHA-256,
+ * internal/hash/reader.go:123-153): message i = d_base + d_offsets[i] with length
+ * d_lens[i] (both device int64 arrays); digest i at d_out + 16*i (MD5) or 32*i
+ * (SHA-256).  One lane per message: a launch takes as long as its longest message
+ * (per-block latency roof in DESIGN.md §4), so group parts of similar size. */
+int zs3_md5_parts(const uint8_t* d_base, const int64_t* d_offsets, const int64_t* d_lens, int64_t n_msgs,
+                  uint8_t* d_out, void* stream);
+int zs3_sha256_parts(const uint8_t* d_base, const int64_t* d_offsets, const int64_t* d_lens, int64_t n_msgs,
+                     uint8_t* d_out, void* stream);
+
 /* etag.Multipart (internal/etag/etag.go:211-226): h_etags holds n_etags ETags,
  * etag i at h_etags + offsets[i] with length lens[i] (16 = singlepart MD5; longer =
  * multipart "-N" or encrypted, both skipped as the reference skips them).  Writes

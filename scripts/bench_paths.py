@@ -192,8 +192,26 @@ if "digest" in PATHS:
     for name, fn, width in (("md5_batch", z.md5_batch, 16), ("sha256_batch", z.sha256_batch, 32)):
         dout = torch.empty(nobj * width, dtype=torch.uint8, device="cuda")
         ms = timeit(lambda: fn(buf, MiB, MiB, nobj, dout), reps=3)
-        out(name, f"{nobj} x 1 MiB objects, one lane per object", ms, nobj * (MiB + width), objects=nobj)
-    del buf
+        # per-block latency of one lane's chain: the launch is one 1 MiB message long
+        # (16 385 blocks with the padding block); the roof is the compression wave's
+        # VALU count per block x 4 cycles (digest.hip header)
+        blk = MiB // 64 + 1
+        out(name, f"{nobj} x 1 MiB objects, one lane per object", ms, nobj * (MiB + width), objects=nobj,
+            us_per_block=round(ms * 1e3 / blk, 4))
+    # the parts of multipart uploads: one 5 MiB part alone (the latency of one part), and
+    # 256 parts of 5 MiB at arbitrary offsets in one launch (zs3_*_parts)
+    part = 5 * MiB
+    pbuf = torch.empty(256 * part + 4096, dtype=torch.uint8, device="cuda")
+    z.fill_batch(pbuf, part, part, 256, seed=3)
+    for nparts in (1, 256):
+        offs = torch.arange(nparts, dtype=torch.int64, device="cuda") * (part + 7)
+        lens = torch.full((nparts,), part, dtype=torch.int64, device="cuda")
+        for name, fn, width in (("md5_parts", z.md5_parts, 16), ("sha256_parts", z.sha256_parts, 32)):
+            dout = torch.empty(nparts * width, dtype=torch.uint8, device="cuda")
+            ms = timeit(lambda: fn(pbuf, offs, lens, nparts, dout), reps=2)
+            out(name, f"{nparts} x 5 MiB parts at unaligned offsets, one launch", ms, nparts * (part + width),
+                objects=nparts, us_per_block=round(ms * 1e3 / (part // 64 + 1), 4))
+    del buf, pbuf
     torch.cuda.empty_cache()
 
 

@@ -24,6 +24,11 @@ timeout -k 10 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCL
     -d $OUT/pmcv -o p --output-format csv -- \
     python bench.py --steps 3 --warmup 1 --no-cpu > $OUT/pmcv.log 2>&1 || { tail -5 $OUT/pmcv.log; exit 8; }
 python scripts/pmc_summary.py $(find $OUT/pmcv -name '*counter_collection.csv' | head -1) | tee $P/pmc_valu.txt
+echo "=== pmc LDS"
+timeout -k 10 600 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAIT_ANY SQ_WAVE_CYCLES \
+    -d $OUT/pmcl -o p --output-format csv -- \
+    python bench.py --steps 3 --warmup 1 --no-cpu > $OUT/pmcl.log 2>&1 || { tail -5 $OUT/pmcl.log; exit 9; }
+python scripts/pmc_summary.py $(find $OUT/pmcl -name '*counter_collection.csv' | head -1) | tee $P/pmc_lds.txt
 echo "=== bench $(date +%T)"
 timeout -k 10 600 python bench.py > $OUT/bench.log 2>&1 || { cat $OUT/bench.log; exit 4; }
 grep '"metric"' $OUT/bench.log | tee $P/bench.json

@@ -173,3 +173,15 @@ def test_stripe_batches_reject_short_strides(fn, stride_delta):
     else:
         rc = L.zs3_verify_reconstruct_batch_masks(h, fake, stride, S, n, presn, 1, fake, fake, None, None, None)
     assert rc == -8, (fn, rc)
+
+
+@pytest.mark.parametrize("fn", ["zs3_md5_parts", "zs3_sha256_parts"])
+def test_parts_digests_reject_missing_arrays(fn):
+    """zs3_md5_parts / zs3_sha256_parts need both the offsets and the lengths arrays
+    (rejected before any device call); zero messages is a no-op."""
+    import ctypes as C
+    L = z.lib()
+    fake = C.c_void_p(BASE)
+    assert getattr(L, fn)(fake, None, fake, 3, fake, None) == -8
+    assert getattr(L, fn)(fake, fake, None, 3, fake, None) == -8
+    assert getattr(L, fn)(fake, fake, fake, -1, fake, None) == -8

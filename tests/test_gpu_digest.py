@@ -83,3 +83,28 @@ def test_reference_multipart_vectors_on_device():
 def test_content_sha256_mirror():
     objs = [b"", b"abc", os.urandom(1000), os.urandom(65536 + 7)]
     assert ze.content_sha256(objs) == [eo.sha256(o) for o in objs]
+
+
+@pytest.mark.parametrize("algo", ["md5", "sha256"])
+def test_parts_at_offsets_one_launch(algo):
+    """Independent messages of very different lengths at arbitrary (unaligned,
+    overlapping) offsets of one buffer in one launch (zs3_md5_parts / zs3_sha256_parts:
+    the parts of multipart uploads), including empty, 55/56/64-byte boundaries and
+    multi-MiB parts next to 1-byte ones in the same wave."""
+    rng = np.random.default_rng(11)
+    total = 9 << 20
+    host = rng.integers(0, 256, total, dtype=np.uint8)
+    lens = [0, 1, 55, 56, 63, 64, 65, 119, 120, 4096, (5 << 20) + 3, 3 << 20, 777777, 1 << 20] + \
+        [int(x) for x in rng.integers(0, 300000, 150)]
+    offs = [int(rng.integers(0, total - n + 1)) for n in lens]
+    d = torch.from_numpy(host).cuda()
+    do = torch.tensor(offs, dtype=torch.int64, device="cuda")
+    dl = torch.tensor(lens, dtype=torch.int64, device="cuda")
+    width = 16 if algo == "md5" else 32
+    out = torch.zeros(len(lens) * width, dtype=torch.uint8, device="cuda")
+    (z.md5_parts if algo == "md5" else z.sha256_parts)(d, do, dl, len(lens), out)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().reshape(len(lens), width)
+    ref = hashlib.md5 if algo == "md5" else hashlib.sha256
+    for i, (o, n) in enumerate(zip(offs, lens)):
+        assert got[i].tobytes() == ref(host[o:o + n].tobytes()).digest(), (i, n)

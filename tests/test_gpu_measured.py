@@ -408,9 +408,8 @@ def test_reconstruct_unaligned_rows(oracle, k, m, blen, erased, data_only):
                          ids=lambda v: str(v))
 def test_encode_only_unaligned_rows(oracle, k, m, blen):
     """EncodeData without sums at shard sizes that are not a multiple of 16 and with Split
-    padding (RS(12+4) / RS(10+4) on 1 MiB blocks, ragged lengths): the any-geometry encode
-    (a UA mode of the specialised encode-only kernel measured slower, 2.11 vs 1.68 ms on
-    RS(12+4) 4096 x 1 MiB, and was dropped); padding bytes poisoned in memory must read as
+    padding (RS(12+4) / RS(10+4) on 1 MiB blocks, ragged lengths): the specialised
+    encode-only kernel in UA mode (round 4); padding bytes poisoned in memory must read as
     zero, every parity byte vs the oracle."""
     R = k + m
     nb = 9
@@ -475,13 +474,17 @@ def _gen_get_cases():
         cases.append((k, m, sorted(list(range(k, R))[: e - 1] + [0]), True))
         cases.append((k, m, [k // 2, k - 1] if k > 2 else [0, 1], False))
     cases += [(5, 4, [1], False), (11, 4, [2, 12, 13], False), (3, 3, [1], True), (2, 2, [3], True)]
+    # RS(4+4), the 8-drive default: 1, 3 and 4 lost rows (round 4 instances)
+    cases += [(4, 4, [0, 2, 5], True), (4, 4, [0, 1, 2, 3], False), (4, 4, [1, 4, 6, 7], True), (4, 4, [3], True),
+              (4, 4, [1, 2, 7], False)]
     return cases
 
 
 @pytest.mark.parametrize("k,m,erased,heal", _gen_get_cases(), ids=lambda v: str(v))
 def test_default_geometries_ws_get_heal(oracle, k, m, erased, heal):
     """GET / heal of the non-dyadic server-default geometries on the warp-specialised
-    k_vr_ws (fused_v2_get_gen.hip, round 4; UA mode for every k but 2): 1 MiB blocks,
+    k_vr_ws (fused_v2_get_gen.hip, round 4; UA mode for every k but 2) and RS(4+4) with
+    1, 3 or 4 lost rows (fused_v2_get.hip, round 4): 1 MiB blocks,
     1031 stripes (a last workgroup with dead stripes) tiled from 61 distinct oracle
     stripes, one rotted survivor flagged exactly, every rebuilt byte and heal sum vs the
     oracle, survivors and lost parity (ReconstructData) untouched."""
@@ -504,7 +507,7 @@ def test_default_geometries_ws_get_heal(oracle, k, m, erased, heal):
     codec.verify_reconstruct_batch(d, R * S, S, nb, [i not in erased for i in range(R)], not heal, exp, bad,
                                    sums_out=out)
     torch.cuda.synchronize()
-    if k != 4:
+    if k != 4 or m == 4:
         assert z.last_path() == 2, z.last_path()
     want_bad = np.zeros((nb, R), np.int32)
     want_bad[bad_blk, bad_row] = 1
@@ -521,3 +524,33 @@ def test_default_geometries_ws_get_heal(oracle, k, m, erased, heal):
     for i in range(R):
         if i not in erased:
             assert bool((d[:, i, :] == ref[idx, i, :]).all(dim=1)[ok].all()), f"survivor {i}"
+
+
+@pytest.mark.parametrize("k,m", GEN_GEOMS + [(12, 4)], ids=lambda v: str(v))
+def test_default_geometries_encode_only(oracle, k, m):
+    """EncodeData without sums for the server-default geometries on 1 MiB blocks (UA mode
+    of the specialised encode-only kernel for every unaligned k, round 4): 1031 stripes,
+    Split padding poisoned in memory, every parity byte vs cpu_ref, two blocks vs the
+    scalar oracle."""
+    R = k + m
+    nb = 1031
+    S = -(-MiB // k)
+    d = torch.zeros(nb * R * S, dtype=torch.uint8, device=DEV)
+    z.fill_batch(d, R * S, MiB, nb, seed=k * 17 + m, obj0=0)
+    if k * S > MiB:
+        d.view(nb, R * S)[:, MiB:k * S] = 0xEE
+    z.Codec(k, m, MiB).encode_batch(d, R * S, MiB, nb, parity=d, parity_offset=k * S, parity_stride=R * S)
+    torch.cuda.synchronize()
+    assert z.last_path() == 1, z.last_path()
+    mat = oracle.build_matrix(k, m)
+    host = d.cpu().numpy().reshape(nb, R * S)
+    clean = host.copy()
+    clean[:, MiB:k * S] = 0
+    par = np.empty(nb * m * S, np.uint8)
+    cpuref.encode_hash(k, m, mat, np.ascontiguousarray(clean), MiB, nb, R * S, par, m * S, None, KEY,
+                       cpuref.threads_available())
+    assert np.array_equal(host[:, k * S:], par.reshape(nb, m * S)), "parity"
+    assert (host[:, MiB:k * S] == 0xEE).all(), "Split padding left as it was"
+    for b in (0, nb - 1):
+        want = oracle.encode_data(k, m, oracle.fill(k * 17 + m, b, MiB), mat)
+        assert np.array_equal(host[b, k * S:].reshape(m, S), want[k:]), b

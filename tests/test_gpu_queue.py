@@ -216,8 +216,10 @@ def test_queue_batches_concurrent_blocks(oracle):
     q.close()
 
 
-@pytest.mark.parametrize("k,m,bs", [(8, 4, 1 << 20), (5, 3, 100000), (12, 4, 1 << 20), (10, 4, 1 << 20)])
-def test_queue_zero_copy_pinned_callers(oracle, k, m, bs):
+@pytest.mark.parametrize("k,m,bs,zc_mode", [(8, 4, 1 << 20, 1), (5, 3, 100000, 1), (12, 4, 1 << 20, 1),
+                                             (10, 4, 1 << 20, 1), (8, 4, 1 << 20, 2), (12, 4, 1 << 20, 2),
+                                             (8, 4, 1 << 20, 3), (12, 4, 1 << 20, 3), (10, 4, 1 << 20, 3)])
+def test_queue_zero_copy_pinned_callers(oracle, k, m, bs, zc_mode, monkeypatch):
     """Callers whose block buffers come from zs3_host_alloc (the pinned bpool) are
     served zero-copy (the DMA engine reads the data rows from, and writes the parity
     rows / rebuilt rows into, the caller's buffer), side by side in the same batches
@@ -226,7 +228,11 @@ def test_queue_zero_copy_pinned_callers(oracle, k, m, bs):
     16-drive default, UA kernel) and RS(10+4) (any-geometry kernel) at 1 MiB have Split
     padding (k*S > blockSize): a zero-copy block DMAs only its `len` data bytes, so the
     slot's padding bytes hold whatever the slot's previous batch left there, and every
-    encode kernel must read them as zero."""
+    encode kernel must read them as zero.  Pinned-caller modes (queue.hip,
+    ZS3_QUEUE_ZC): 1 = zero-copy for the first block of a batch, the rest staged (the
+    default); 2 = every full block by a DMA of its own; 3 = copy-list kernels over the
+    mapped pinned pages."""
+    monkeypatch.setenv("ZS3_QUEUE_ZC", str(zc_mode))
     codec = z.Codec(k, m, bs)
     q = z.Queue(codec, max_batch=16, max_wait_us=500)
     R = k + m
@@ -276,9 +282,13 @@ def test_queue_zero_copy_pinned_callers(oracle, k, m, bs):
     batches, blocks = q.stats()
     assert blocks == nthr * per * 2
     zc = q.zero_copy_blocks()
-    # pinned threads: every full encode block and every decode block
+    # pinned threads: every full encode block and every decode block (modes 2, 3); mode 1
+    # only those that opened their batch
     n_short = sum(1 for t in range(0, nthr, 2) if t % 4 == 0)
-    assert zc == (nthr // 2) * per * 2 - n_short, zc
+    if zc_mode == 1:
+        assert 0 <= zc <= (nthr // 2) * per * 2 - n_short, zc
+    else:
+        assert zc == (nthr // 2) * per * 2 - n_short, zc
     q.close()
     for p in pins + pins_dec:
         p.free()

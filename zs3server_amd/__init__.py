@@ -54,7 +54,7 @@ EXPORTS = [
     "zs3_hh256_batch_ragged", "zs3_bitrot_verify_file_batch", "zs3_codec_params",
     "zs3_queue_new", "zs3_queue_free", "zs3_queue_submit_encode", "zs3_queue_submit_decode", "zs3_req_wait",
     "zs3_queue_flush", "zs3_queue_stats", "zs3_queue_zero_copy_blocks", "zs3_queue_encode_data", "zs3_queue_decode_data_blocks",
-    "zs3_stream_encode_multi", "zs3_split_range",
+    "zs3_stream_encode_multi", "zs3_split_range", "zs3_md5_parts", "zs3_sha256_parts",
 ]
 # include/zs3gpu_diag.h: exported by the diagnostics build only
 DIAG_EXPORTS = ["zs3_debug_set_variant", "zs3_debug_set_buffer"]
@@ -147,6 +147,8 @@ def _load(path):
     L.zs3_stream_encode.restype = i64
     L.zs3_md5_batch.argtypes = [vp, i64, i64, vp, i64, vp, vp]
     L.zs3_sha256_batch.argtypes = [vp, i64, i64, vp, i64, vp, vp]
+    L.zs3_md5_parts.argtypes = [vp, vp, vp, i64, vp, vp]
+    L.zs3_sha256_parts.argtypes = [vp, vp, vp, i64, vp, vp]
     L.zs3_etag_multipart.argtypes = [vp, vp, vp, i64, vp]
     L.zs3_host_alloc.argtypes = [C.POINTER(vp), C.c_size_t]
     L.zs3_host_free.argtypes = [vp]
@@ -463,6 +465,19 @@ def sha256_batch(msgs, msg_stride: int, msg_len: int, n_msgs: int, out, lens=Non
     """Content SHA-256 of n device messages (zs3_sha256_batch); digest i at out[32*i:]."""
     _check(lib().zs3_sha256_batch(_ptr(msgs, offset), msg_stride, msg_len, _ptr(lens), n_msgs, _ptr(out),
                                   _stream(stream)), "sha256_batch")
+
+
+def md5_parts(base, offsets, lens, n_msgs: int, out, stream=None) -> None:
+    """MD5 of n independent device messages (multipart parts) in one launch
+    (zs3_md5_parts): message i at base + offsets[i] (device int64), length lens[i]."""
+    _check(lib().zs3_md5_parts(_ptr(base), _ptr(offsets), _ptr(lens), n_msgs, _ptr(out), _stream(stream)),
+           "md5_parts")
+
+
+def sha256_parts(base, offsets, lens, n_msgs: int, out, stream=None) -> None:
+    """SHA-256 of n independent device messages in one launch (zs3_sha256_parts)."""
+    _check(lib().zs3_sha256_parts(_ptr(base), _ptr(offsets), _ptr(lens), n_msgs, _ptr(out), _stream(stream)),
+           "sha256_parts")
 
 
 def etag_multipart(etags) -> bytes:

@@ -9,10 +9,28 @@
 //   internal/hash/reader.go:123-153   content SHA-256 (sha256-simd, FIPS 180-4), compared
 //                                     at EOF -> SHA256Mismatch
 // Both digests are Merkle–Damgård chains over 64-byte blocks, so one message's blocks
-// are processed in order by one lane; messages are independent (one thread each).  A
-// lane's blocks are read with 16-byte loads one block ahead of the compression; the
-// final padded block(s) are assembled per lane.  Integer VALU only: v_bitop3 for the
-// boolean functions, v_alignbit for rotates, v_add3 for the sums.
+// are processed in order by one lane; messages are independent (one lane each).
+//
+// Latency roof (round 4).  A wave issues at most one VALU instruction per 4 cycles
+// (MI355X_MICROARCH.md, 'vector-instruction ISSUE cost'), and one message's blocks are a
+// serial chain, so a message cannot go faster than (VALU instructions per block on its
+// wave) x 4 cycles per block, whatever the batch size; a batch of n messages runs n/64
+// such chains side by side.  The round-3 kernels ran the whole block on one wave: MD5
+// 364 and SHA-256 1733 instructions per block in the compiled loop, and one block of
+// load prefetch, so MD5 also waited on HBM (4096 x 1 MiB: 15.5 / 55.0 ms).  Here two
+// waves share each group of 64 messages:
+//   feeder wave      loads the blocks 4 ahead (compiler-tracked 16-byte loads), builds
+//                    the padded final block(s), and writes per block the 64 words the
+//                    rounds consume, constants folded in: MD5 m[g(t)] + K[t], SHA-256
+//                    the message schedule W[t] + K[t] (byte-swapped, sigma functions)
+//                    into a two-slot LDS ring ([slot][word quad][lane], 16-byte lanes:
+//                    conflict-free ds_read_b128 / ds_write_b128);
+//   compression wave 16 ds_read_b128 + the rounds only: MD5 4 instructions per step
+//                    (bitop3, add3, alignbit, add), SHA-256 14 per round (two xor3-folded
+//                    Sigma functions, bitop3 ch / maj, three adds).
+// One workgroup barrier per block hands the slot over.  The roof is the compression
+// wave's instruction count per block x 4 cycles (DESIGN.md §4 lists the counts and the
+// measured per-block time).
 #include "kernels.hpp"
 
 #include <stdint.h>
@@ -166,12 +184,214 @@ __device__ __forceinline__ void bswap16w(uint32_t (&m)[16]) {
     for (int i = 0; i < 16; ++i) m[i] = __builtin_bswap32(m[i]);
 }
 
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+// One SHA-256 round from the scheduled word + constant wk (FIPS 180-4 §6.2.2 step 3).
+__device__ __forceinline__ void sha_round(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d, uint32_t& e,
+                                          uint32_t& f, uint32_t& g, uint32_t& h, uint32_t wk) {
+    const uint32_t S1 = xor3(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25));
+    const uint32_t ch = __builtin_amdgcn_bitop3_b32(e, f, g, 0xCA);   // e ? f : g
+    const uint32_t t1 = h + S1 + ch + wk;
+    const uint32_t S0 = xor3(rotr32(a, 2), rotr32(a, 13), rotr32(a, 22));
+    const uint32_t mj = __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);   // majority
+    h = g;
+    g = f;
+    f = e;
+    e = d + t1;
+    d = c;
+    c = b;
+    b = a;
+    a = t1 + S0 + mj;
+}
+
+// MD5 step t from mk = m[g(t)] + K[t] (RFC 1321 §3.4).
+template <int T>
+__device__ __forceinline__ void md5_step(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d, uint32_t mk) {
+    constexpr int R[4][4] = {{7, 12, 17, 22}, {5, 9, 14, 20}, {4, 11, 16, 23}, {6, 10, 15, 21}};
+    uint32_t f;
+    if constexpr (T < 16)
+        f = __builtin_amdgcn_bitop3_b32(b, c, d, 0xCA);  // b ? c : d
+    else if constexpr (T < 32)
+        f = __builtin_amdgcn_bitop3_b32(d, b, c, 0xCA);  // d ? b : c
+    else if constexpr (T < 48)
+        f = xor3(b, c, d);
+    else
+        f = __builtin_amdgcn_bitop3_b32(b, c, d, 0x39);  // c ^ (b | ~d)
+    const uint32_t t = a + f + mk;
+    a = d;
+    d = c;
+    c = b;
+    b = b + rotl32(t, R[T >> 4][T & 3]);
+}
+
+// the 64 round words of one block in a two-slot ring: ring[slot][q][lane], word t of the
+// lane in component t % 4 of quad t / 4
+typedef uint4 DgRing[2][16][64];
+
+// Feeder wave: block b of this lane's message -> the 64 round words.
+template <bool SHA>
+__device__ __forceinline__ void dg_produce(uint4 (&slot)[16][64], int lane, int64_t b, int64_t nfull, int64_t nblk,
+                                           const uint4 (&raw)[4], const uint8_t* msg, int nt, int64_t len) {
+    uint32_t m[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        m[4 * q + 0] = raw[q].x;
+        m[4 * q + 1] = raw[q].y;
+        m[4 * q + 2] = raw[q].z;
+        m[4 * q + 3] = raw[q].w;
+    }
+    if constexpr (SHA) bswap16w(m);
+    if (b >= nfull && b < nblk) {
+        // the padded final block(s): tail bytes, 0x80, zeros, bit length
+        uint32_t m0[16], m1[16];
+        pad_tail<SHA>(m0, m1, msg + (nfull << 6), nt, (uint64_t)len);
+        const bool first = b == nfull;
+#pragma unroll
+        for (int w = 0; w < 16; ++w) m[w] = first ? m0[w] : m1[w];
+    }
+    uint32_t wk[64];
+    if constexpr (SHA) {
+#pragma unroll
+        for (int t = 0; t < 64; ++t) {
+            if (t >= 16) {
+                const uint32_t w15 = m[(t - 15) & 15], w2 = m[(t - 2) & 15];
+                const uint32_t s0 = xor3(rotr32(w15, 7), rotr32(w15, 18), w15 >> 3);
+                const uint32_t s1 = xor3(rotr32(w2, 17), rotr32(w2, 19), w2 >> 10);
+                m[t & 15] = m[t & 15] + s0 + m[(t - 7) & 15] + s1;
+            }
+            wk[t] = m[t & 15] + kShaK[t];
+        }
+    } else {
+#pragma unroll
+        for (int t = 0; t < 64; ++t) {
+            const int g = t < 16 ? t : t < 32 ? (5 * t + 1) & 15 : t < 48 ? (3 * t + 5) & 15 : (7 * t) & 15;
+            wk[t] = m[g] + kMd5K[t];
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) slot[q][lane] = make_uint4(wk[4 * q], wk[4 * q + 1], wk[4 * q + 2], wk[4 * q + 3]);
+}
+
+template <int T>
+__device__ __forceinline__ void md5_rounds(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d, const uint32_t (&wk)[64]) {
+    if constexpr (T < 64) {
+        md5_step<T>(a, b, c, d, wk[T]);
+        md5_rounds<T + 1>(a, b, c, d, wk);
+    }
+}
+
 }  // namespace
 
+// Two-wave digest pipeline (see the header): 128 threads = compression wave (0) +
+// feeder wave (1) over the same 64 messages.  Message i: bytes at msgs + offs[i] (or
+// i*stride), length lens[i] (or len).
+template <bool SHA>
+__global__ void __launch_bounds__(128) k_digest_ws(DigestArgs a) {
+    __shared__ DgRing ring;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int64_t i0 = (int64_t)blockIdx.x * 64 + lane;
+    const bool live = i0 < a.n;
+    const int64_t i = live ? i0 : a.n - 1;  // dead lanes repeat the last message
+    const uint8_t* msg = a.msgs + (a.offs ? a.offs[i] : i * a.stride);
+    const int64_t len = a.lens ? a.lens[i] : a.len;
+    const int64_t nfull = len >> 6;
+    const int nt = (int)(len & 63);
+    const int64_t nblk = nfull + (nt < 56 ? 1 : 2);
+    // blocks of the wave's longest message (both waves compute the same value: the
+    // number of barriers below must agree)
+    int nbw = (int)nblk;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) nbw = max(nbw, __shfl_xor(nbw, off));
+    if (__builtin_amdgcn_readfirstlane(tid) >= 64) {
+        // ---- feeder: loads 4 blocks ahead
+        constexpr int P = 4;
+        uint4 raw[P][4];
+        auto issue = [&](uint4 (&r)[4], int64_t b) {
+            if (b < nfull) {
+                const uint8_t* p = msg + (b << 6);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) __builtin_memcpy(&r[q], p + 16 * q, 16);
+            }
+        };
+#pragma unroll
+        for (int p = 0; p < P; ++p) issue(raw[p], p);
+        for (int s0 = 0; s0 <= nbw; s0 += P) {
+#pragma unroll
+            for (int p = 0; p < P; ++p) {
+                const int s = s0 + p;
+                if (s > nbw) break;
+                if (s < nbw) dg_produce<SHA>(ring[s & 1], lane, s, nfull, nblk, raw[p], msg, nt, len);
+                issue(raw[p], s + P);
+                __syncthreads();
+            }
+        }
+        return;
+    }
+    // ---- compression
+    uint32_t h[8];
+    if constexpr (SHA) {
+        h[0] = 0x6a09e667u; h[1] = 0xbb67ae85u; h[2] = 0x3c6ef372u; h[3] = 0xa54ff53au;
+        h[4] = 0x510e527fu; h[5] = 0x9b05688cu; h[6] = 0x1f83d9abu; h[7] = 0x5be0cd19u;
+    } else {
+        h[0] = 0x67452301u; h[1] = 0xefcdab89u; h[2] = 0x98badcfeu; h[3] = 0x10325476u;
+        h[4] = h[5] = h[6] = h[7] = 0;
+    }
+    for (int s = 0; s <= nbw; ++s) {
+        if (s >= 1) {
+            const int b = s - 1;
+            uint32_t wk[64];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const uint4 v = ring[b & 1][q][lane];
+                wk[4 * q] = v.x;
+                wk[4 * q + 1] = v.y;
+                wk[4 * q + 2] = v.z;
+                wk[4 * q + 3] = v.w;
+            }
+            const bool upd = b < nblk;
+            if constexpr (SHA) {
+                uint32_t A = h[0], B = h[1], C = h[2], D = h[3], E = h[4], F = h[5], G = h[6], H = h[7];
+#pragma unroll
+                for (int t = 0; t < 64; ++t) sha_round(A, B, C, D, E, F, G, H, wk[t]);
+                h[0] = upd ? h[0] + A : h[0];
+                h[1] = upd ? h[1] + B : h[1];
+                h[2] = upd ? h[2] + C : h[2];
+                h[3] = upd ? h[3] + D : h[3];
+                h[4] = upd ? h[4] + E : h[4];
+                h[5] = upd ? h[5] + F : h[5];
+                h[6] = upd ? h[6] + G : h[6];
+                h[7] = upd ? h[7] + H : h[7];
+            } else {
+                uint32_t A = h[0], B = h[1], C = h[2], D = h[3];
+                md5_rounds<0>(A, B, C, D, wk);
+                h[0] = upd ? h[0] + A : h[0];
+                h[1] = upd ? h[1] + B : h[1];
+                h[2] = upd ? h[2] + C : h[2];
+                h[3] = upd ? h[3] + D : h[3];
+            }
+        }
+        __syncthreads();
+    }
+    if (!live) return;
+    if constexpr (SHA) {
+        uint32_t* out = reinterpret_cast<uint32_t*>(a.out + i * 32);
+#pragma unroll
+        for (int w = 0; w < 8; ++w) out[w] = __builtin_bswap32(h[w]);  // big-endian digest
+    } else {
+        uint32_t* out = reinterpret_cast<uint32_t*>(a.out + i * 16);
+#pragma unroll
+        for (int w = 0; w < 4; ++w) out[w] = h[w];  // digest = h0..h3 little-endian
+    }
+}
+
+// Round-3 kernels (diagnostics variant 1): the whole block on one wave, one block of
+// load prefetch.
 __global__ void __launch_bounds__(64) k_md5_batch(DigestArgs a) {
     const int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x;
     if (i >= a.n) return;
-    const uint8_t* msg = a.msgs + i * a.stride;
+    const uint8_t* msg = a.msgs + (a.offs ? a.offs[i] : i * a.stride);
     const int64_t len = a.lens ? a.lens[i] : a.len;
     const int64_t nfull = len >> 6;
     uint32_t h[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
@@ -195,7 +415,7 @@ __global__ void __launch_bounds__(64) k_md5_batch(DigestArgs a) {
 __global__ void __launch_bounds__(64) k_sha256_batch(DigestArgs a) {
     const int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x;
     if (i >= a.n) return;
-    const uint8_t* msg = a.msgs + i * a.stride;
+    const uint8_t* msg = a.msgs + (a.offs ? a.offs[i] : i * a.stride);
     const int64_t len = a.lens ? a.lens[i] : a.len;
     const int64_t nfull = len >> 6;
     uint32_t h[8] = {
@@ -221,13 +441,19 @@ __global__ void __launch_bounds__(64) k_sha256_batch(DigestArgs a) {
 
 hipError_t launch_md5(const DigestArgs& a, hipStream_t s) {
     if (a.n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_md5_batch, dim3((unsigned)((a.n + 63) / 64)), dim3(64), 0, s, a);
+    if (ZS3_DIAG && a.variant == 1)
+        hipLaunchKernelGGL(k_md5_batch, dim3((unsigned)((a.n + 63) / 64)), dim3(64), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_digest_ws<false>, dim3((unsigned)((a.n + 63) / 64)), dim3(128), 0, s, a);
     return hipGetLastError();
 }
 
 hipError_t launch_sha256(const DigestArgs& a, hipStream_t s) {
     if (a.n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_sha256_batch, dim3((unsigned)((a.n + 63) / 64)), dim3(64), 0, s, a);
+    if (ZS3_DIAG && a.variant == 1)
+        hipLaunchKernelGGL(k_sha256_batch, dim3((unsigned)((a.n + 63) / 64)), dim3(64), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_digest_ws<true>, dim3((unsigned)((a.n + 63) / 64)), dim3(128), 0, s, a);
     return hipGetLastError();
 }
 

@@ -54,8 +54,13 @@ template <int K, int M>
 static int launch_ehx_default(const EncArgs& a, hipStream_t s) {
     const int64_t n = a.n_blocks;
     if constexpr (K == 8 && M == 4) {
+        // n > 2048: 16 stripes, 384-byte tiles, 4 pair-form hash + 6 encode waves, nt policy;
+        // round 4: buffer-addressed loads and stores (BUF) and the conflict-free LDS row
+        // stride (TSP = 1: SQ_LDS_BANK_CONFLICT 20 % -> 0 % of LDS cycles), diagnostics 302:
+        // 4.98 / 4.84 -> 4.79 ms on 16384 x 1 MiB pairs of runs (profiles/r04/r04_ab1.jsonl)
         if (n > 2048)
-            return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3>(a, s) ? PATH_WS : PATH_NONE;
+            return launch_ws_t<K, M, 16, 384, 1, true, false, 0, false, 1, 0, false, 3, false, 0, 0, false, 3, 1>(a, s)
+                       ? PATH_WS : PATH_NONE;
         // up to 2048 stripes (round 3, variant 199): 4 stripes per workgroup, quad-form
         // hash waves (3) beside 4 encode waves, 1 KiB tiles, two tiles of prefetch, and
         // the 2-waves-per-SIMD register budget (7-wave workgroups: no spills, where the

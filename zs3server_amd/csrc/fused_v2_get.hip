@@ -18,13 +18,27 @@ bool launch_vr_ws_diag(int v, const VrArgs& a, hipStream_t s);  // fused_v2_get_
 static bool launch_vr_ws_default(const VrArgs& a, hipStream_t s) {
     const bool heal = a.sums_out != nullptr;
     if (a.k == 4) {
-        // RS(4+2)-shaped: quad-form hash waves, 8 stripes, one wave of each kind per SIMD
-        // (the 8 192 chains of a 2048-object batch are latency-bound: verify 0.63 ->
-        // 0.44 ms over the pair form)
-        if (heal) return a.e == 2 && launch_vr_ws_t<4, 2, true, 8, 256, 4, 16, true>(a, s);
+        // RS(4+2)- / RS(4+4)-shaped: quad-form hash waves, 8 stripes, one wave of each kind
+        // per SIMD (the 8 192 chains of a 2048-object batch are latency-bound: verify 0.63 ->
+        // 0.44 ms over the pair form).  Verify only: 256-byte tiles, 4 of prefetch.
+        // Rebuild / heal (round 4, diagnostics 270-272): 1 KiB tiles, so each chain runs 32
+        // packets between barriers instead of 8, as config 2's encode: RS(4+2) 2048 x 1 MiB
+        // heal 2 0.85 -> 0.63-0.70 ms, RS(4+4) 4096 x 1 MiB rebuild 2 / 4 1.45 / 2.27 ->
+        // 1.21 / 1.78, heal 2 / 3 1.68 / 2.27 -> 1.24 / 1.65 (4 of prefetch), heal 4 2.69
+        // -> 1.92 (2 of prefetch: the 4-deep instance measured 2.19)
+        // (profiles/r04/get_ab_k4.jsonl, mean of two rounds)
+        if (heal) {
+            if (a.e == 1) return launch_vr_ws_t<4, 1, true, 8, 1024, 4, 16, true>(a, s);
+            if (a.e == 2) return launch_vr_ws_t<4, 2, true, 8, 1024, 4, 16, true>(a, s);
+            if (a.e == 3) return launch_vr_ws_t<4, 3, true, 8, 1024, 4, 16, true>(a, s);
+            if (a.e == 4) return launch_vr_ws_t<4, 4, true, 8, 1024, 2, 16, true>(a, s);
+            return false;
+        }
         if (a.e == 0) return launch_vr_ws_t<4, 0, false, 8, 256, 4, 16, true>(a, s);
-        if (a.e == 1) return launch_vr_ws_t<4, 1, false, 8, 256, 4, 16, true>(a, s);
-        if (a.e == 2) return launch_vr_ws_t<4, 2, false, 8, 256, 4, 16, true>(a, s);
+        if (a.e == 1) return launch_vr_ws_t<4, 1, false, 8, 1024, 4, 16, true>(a, s);
+        if (a.e == 2) return launch_vr_ws_t<4, 2, false, 8, 1024, 4, 16, true>(a, s);
+        if (a.e == 3) return launch_vr_ws_t<4, 3, false, 8, 1024, 4, 16, true>(a, s);
+        if (a.e == 4) return launch_vr_ws_t<4, 4, false, 8, 1024, 4, 16, true>(a, s);
         return false;
     }
     if (a.k == 16) {

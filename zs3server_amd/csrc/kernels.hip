@@ -58,6 +58,42 @@ __device__ __forceinline__ uint4 ld16(const uint8_t* p) {
     return v;
 }
 __device__ __forceinline__ void st16(uint8_t* p, const uint4& v) { __builtin_memcpy(p, &v, 16); }
+// Ragged columns of the unaligned-row kernels: nv = valid bytes of the row from the
+// column's start.  Shift = 0 (whole column valid), 16 (none: nothing is read) or the
+// bytes the 16-byte load must start early so that it ends at the row's valid end.
+__device__ __forceinline__ int tail_shift(int64_t nv) { return nv >= 16 ? 0 : (nv <= 0 ? 16 : (int)(16 - nv)); }
+// bytes [sh, 16) of v moved to [0, 16 - sh), zero above; sh in [1, 16]
+__device__ __forceinline__ uint4 shr_bytes_zero(const uint4& v, int sh) {
+    if (sh >= 16) return make_uint4(0, 0, 0, 0);
+    const uint32_t w[8] = {v.x, v.y, v.z, v.w, 0u, 0u, 0u, 0u};
+    const int q = sh >> 2;
+    const uint32_t r = (uint32_t)(sh & 3);
+    uint32_t t[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        const uint32_t a = q & 1 ? w[i + 1] : w[i];
+        const uint32_t b = q & 1 ? w[i + 3] : w[i + 2];
+        t[i] = q & 2 ? b : a;
+    }
+    return make_uint4(__builtin_amdgcn_alignbyte(t[1], t[0], r), __builtin_amdgcn_alignbyte(t[2], t[1], r),
+                      __builtin_amdgcn_alignbyte(t[3], t[2], r), __builtin_amdgcn_alignbyte(t[4], t[3], r));
+}
+// the first nv (< 16) bytes of v to p (any alignment): whole dwords, then bytes; fully
+// unrolled (a byte loop with a run-time trip count kept every parity row of the unrolled
+// K x M encode live across it: 343 VGPRs for RS(12+4))
+__device__ __forceinline__ void st16_part(uint8_t* p, const uint4& v, int64_t nv) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        if (4 * i + 4 <= nv) {
+            __builtin_memcpy(p + 4 * i, &w[i], 4);
+        } else {
+#pragma unroll
+            for (int b = 0; b < 3; ++b)
+                if (4 * i + b < nv) p[4 * i + b] = (uint8_t)(w[i] >> (8 * b));
+        }
+    }
+}
 // Non-temporal forms (bytes streamed once: nt cache policy).  p must be 16-byte aligned.
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint4 ld16_nt(const uint8_t* p) {
@@ -525,13 +561,21 @@ __global__ void __launch_bounds__(NT) k_encode_hash_pipe(EncArgs a) {
 // Encode only (no hash): one thread per 16-byte column, K loads -> M stores.
 // NTP: non-temporal data loads and parity stores (the encode-only call; not the
 // latency path, whose hash pass re-reads both from the cache).  Launch: 16-byte aligned.
-template <int K, int M, bool NTP = false>
+// UA (round 4): S need not be a multiple of 16 and the data may carry Split padding
+// (n < k*S; RS(12+4), RS(6+4), RS(10+4), ... on 1 MiB blocks): full columns use the same
+// 16-byte accesses at the rows' byte offsets (unaligned-access mode: 1-2 % below aligned
+// rows on the RS(12+4) streaming shape, profiles/r04/r04_mempat6.jsonl), the column that
+// crosses the last data row's valid length or the row end is read byte by byte (zero
+// past it) and only its parity bytes below S are stored.
+template <int K, int M, bool NTP = false, bool UA = false>
 __global__ void __launch_bounds__(256) k_encode_only(EncArgs a) {
+    static_assert(!(UA && NTP), "unaligned rows: plain accesses");
     __shared__ __attribute__((aligned(16))) uint32_t tabs[M * K * 8];
     for (int i = threadIdx.x; i < M * K * 8; i += 256) tabs[i] = a.tables[i];
     __syncthreads();
     const int64_t S = a.S, n = a.n;
     const int64_t cols = (S + 15) >> 4;
+    const int64_t vlast = n - (int64_t)(K - 1) * S;  // valid bytes of the last data row
     for (int64_t b = blockIdx.y; b < a.n_blocks; b += gridDim.y) {
         const uint8_t* blk = a.data + b * a.data_stride;
         uint8_t* pb = a.parity + b * a.parity_stride;
@@ -539,8 +583,25 @@ __global__ void __launch_bounds__(256) k_encode_only(EncArgs a) {
             const int64_t o = c * 16;
             const uint32_t* tb = tabs + opaque_zero();
             uint4 x[K];
+            if constexpr (UA) {
+                // A column crossing a row's valid end (S, or the last data row's Split
+                // padding) loads the 16 bytes ending at that end and shifts them down
+                // (zero fill); past the end nothing of the row is read (the block's first
+                // 16 bytes are loaded and discarded).  One 16-byte load per row on every
+                // path (a separate byte-wise path doubled the VGPRs).  Launch: S >= 16 and
+                // n >= 16, so every load lies inside [blk, blk + n).
+                const int shS = tail_shift(S - o);
+                const int shL = tail_shift((vlast < S ? vlast : S) - o);
 #pragma unroll
-            for (int j = 0; j < K; ++j) x[j] = NTP ? ld16_nt(blk + (int64_t)j * S + o) : ld16(blk + (int64_t)j * S + o);
+                for (int j = 0; j < K; ++j) {
+                    const int sh = j == K - 1 ? shL : shS;
+                    x[j] = ld16(sh == 16 ? blk : blk + (int64_t)j * S + o - sh);
+                    if (sh) x[j] = shr_bytes_zero(x[j], sh);
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < K; ++j) x[j] = NTP ? ld16_nt(blk + (int64_t)j * S + o) : ld16(blk + (int64_t)j * S + o);
+            }
             GfAcc acc[M][4];
 #pragma unroll
             for (int r = 0; r < M; ++r)
@@ -560,14 +621,22 @@ __global__ void __launch_bounds__(256) k_encode_only(EncArgs a) {
                     acc_add(acc[r][3], gf_lookup(n3, t));
                 }
             }
+            uint4 par[M];
 #pragma unroll
-            for (int r = 0; r < M; ++r) {
-                const uint4 p = make_uint4(acc_done(acc[r][0]), acc_done(acc[r][1]),
-                                           acc_done(acc[r][2]), acc_done(acc[r][3]));
-                if (NTP)
-                    st16_nt(pb + (int64_t)r * S + o, p);
-                else
-                    st16(pb + (int64_t)r * S + o, p);
+            for (int r = 0; r < M; ++r)
+                par[r] = make_uint4(acc_done(acc[r][0]), acc_done(acc[r][1]), acc_done(acc[r][2]), acc_done(acc[r][3]));
+            if (UA && o + 16 > S) {
+                // the ragged last column: only the parity bytes below S
+#pragma unroll
+                for (int r = 0; r < M; ++r) st16_part(pb + (int64_t)r * S + o, par[r], S - o);
+            } else {
+#pragma unroll
+                for (int r = 0; r < M; ++r) {
+                    if (NTP)
+                        st16_nt(pb + (int64_t)r * S + o, par[r]);
+                    else
+                        st16(pb + (int64_t)r * S + o, par[r]);
+                }
             }
         }
     }
@@ -1540,6 +1609,10 @@ static hipError_t run_encode_fast(const EncArgs& a, hipStream_t s, int* path) {
     X(2, 1) X(2, 2) X(3, 2) X(3, 3) X(4, 2) X(4, 3) X(4, 4) X(5, 3) X(6, 2) X(6, 3) X(6, 4) \
     X(8, 2) X(8, 3) X(8, 4) X(10, 4) X(12, 4) X(16, 4)
 
+// further geometries with an unaligned encode-only instance (the server defaults for
+// 9-, 11-, 13- and 15-drive sets)
+#define ZS3_UA_KM(X) X(5, 4) X(7, 4) X(9, 4) X(11, 4)
+
 bool has_fast_encode(int k, int m) {
 #define X(K, M) if (k == K && m == M) return true;
     ZS3_FAST_KM(X)
@@ -1578,6 +1651,25 @@ hipError_t launch_encode(const EncArgs& a, hipStream_t s, int* path) {
             if (path) *path = p;
             return hipGetLastError();
         }
+    }
+    // Encode only at shard sizes that are not a multiple of 16 or with Split padding
+    // (RS(12+4), RS(6+4), RS(10+4), ... on 1 MiB blocks): the specialised encode-only
+    // kernel in UA mode (diagnostics 96: the any-geometry kernel below)
+    // (a ragged column's 16-byte load ends at its row's valid end, so it starts at most 16
+    // bytes before that end: inside the block when S >= 16 and n >= 16)
+    if (!a.sums && a.S >= 16 && a.n >= 16 && !(ZS3_DIAG && (a.variant == 96 || a.variant == 97))) {
+        const int64_t cols = (a.S + 15) >> 4;
+        const unsigned gx = (unsigned)((cols + 255) / 256);
+        const unsigned gy = (unsigned)(a.n_blocks < 65535 ? a.n_blocks : 65535);
+#define X(K, M)                                                                               \
+    if (a.k == K && a.m == M) {                                                               \
+        hipLaunchKernelGGL((k_encode_only<K, M, false, true>), dim3(gx, gy), dim3(256), 0, s, a); \
+        if (path) *path = PATH_FIRSTGEN;                                                      \
+        return hipGetLastError();                                                             \
+    }
+        ZS3_FAST_KM(X)
+        ZS3_UA_KM(X)
+#undef X
     }
     if (path) *path = PATH_GENERIC;
     // any other geometry: encode (8-byte columns) + the batched hash in stripe mode;
@@ -1801,7 +1893,8 @@ static hipError_t run_vr_k(const VrArgs& a, hipStream_t s, int* path) {
     // diagnostics 231: the product dispatch without the latency path
     // diagnostics 240: the product dispatch without that path, batched scalar tables
     const int wv = (ZS3_DIAG && (a.variant == 231 || a.variant == 240 || a.variant == 241 || a.variant == 246)) ? 0 : a.variant;
-    if (wv == 0 || (ZS3_DIAG && ((wv >= 210 && wv <= 219) || wv == 232 || wv == 242 || (wv >= 250 && wv <= 263))))
+    if (wv == 0 || (ZS3_DIAG && ((wv >= 210 && wv <= 219) || wv == 232 || wv == 242 || (wv >= 250 && wv <= 263) ||
+                                    (wv >= 270 && wv <= 277))))
         if (launch_vr_ws(wv, a, s)) {
             if (path) *path = PATH_WS;
             return hipGetLastError();

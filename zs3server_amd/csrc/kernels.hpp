@@ -133,6 +133,8 @@ struct DigestArgs {
     const int64_t* lens;      // optional per-message lengths (device)
     int64_t n;
     uint8_t* out;
+    const int64_t* offs;      // optional per-message byte offsets from msgs (device; else i*stride)
+    int variant;              // diagnostics: 1 = the one-wave kernels (round 3)
 };
 
 // Launches return hipSuccess or the launch error; *path (may be null) receives the

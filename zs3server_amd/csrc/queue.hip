@@ -43,6 +43,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <memory>
@@ -53,6 +54,7 @@
 #include "../../include/zs3gpu.h"
 
 bool zs3i_pinned(const void* p, size_t n);  // zs3gpu.hip: inside a live zs3_host_alloc range
+bool zs3i_pinned_map(const void* p, size_t n, void** dev);  // ... and its device-side address
 
 namespace {
 
@@ -80,8 +82,9 @@ struct zs3_req {
     int32_t* h_bad = nullptr;
     uint8_t* h_sums_out = nullptr;
     int status = ZS3_OK;   // the block's status at launch (its pattern's reedsolomon error)
-    bool zc = false;       // zero-copy: the caller's buffer is pinned (zs3_host_alloc), so the
-                           // DMA engine moves its bytes to / from the device slot directly
+    bool zc = false;       // zero-copy: the caller's buffer is pinned (zs3_host_alloc), so its
+                           // bytes move to / from the device slot without host staging
+    uint8_t* d_map = nullptr;  // zc (copy-list mode): the caller's buffer as a kernel addresses it
     bool done = false;     // results copied out (completer)
     int64_t result = 0;    // zs3_req_wait's return value
 };
@@ -116,6 +119,19 @@ struct zs3_queue {
     int cap = 128;                // positions per slot
     int max_wait_us = 200;
     int nslots = 4;
+    // Pinned callers (round 4; ZS3_QUEUE_ZC=<mode> selects another for A/B measurements,
+    // profiles/r04/queue_ab*.jsonl):
+    //   0 staged like pageable callers (memcpy into the pinned slot, one DMA per batch);
+    //   1 (default) zero-copy only for the first block of a batch (a lone or leading
+    //     caller's block is DMA'd by its submitter while the slot is still empty), the
+    //     rest staged;
+    //   2 every block zero-copy by a DMA of its own (round 3): the per-block DMA calls of
+    //     many submitters serialise in the runtime (256 submitters 26.3 vs staged 32.8
+    //     GiB/s);
+    //   3 zero-copy by one copy-list kernel per batch and direction over the mapped
+    //     pinned pages: GPU-initiated PCIe reads are slower than the DMA engine (256
+    //     submitters 16.6 GiB/s).
+    int zc_mode = 1;
 
     std::mutex mu;
     std::condition_variable cv_space;   // a slot became free / open
@@ -192,6 +208,73 @@ int ensure_lane(zs3_queue* q, std::unique_lock<std::mutex>& lk, int lane) {
     return rc;
 }
 
+// ---- zero-copy transport: a copy-list kernel ---------------------------------------
+// Up to CL_MAX (src, dst, len) entries per launch, passed by value (kernel arguments);
+// grid.y = entry, grid.x strides the entry's bytes in W-byte words (W = the widest
+// alignment every entry allows).  Reads of the callers' mapped pinned pages and writes
+// to them cross PCIe as the GPU's own requests: one launch per batch and direction
+// instead of one DMA call per block (64 submitters each calling hipMemcpyAsync on the
+// slot's stream serialised in the runtime: pinned 17.7 vs pageable 20.8 GiB/s,
+// profiles/r03/queue_native_zero_copy_first.jsonl).
+constexpr int CL_MAX = 80;
+struct CopyList {
+    const uint8_t* src[CL_MAX];
+    uint8_t* dst[CL_MAX];
+    int64_t len[CL_MAX];
+    int n;
+};
+
+template <typename W>
+__global__ void __launch_bounds__(256) k_copy_list(CopyList L) {
+    const int e = blockIdx.y;
+    const W* src = reinterpret_cast<const W*>(L.src[e]);
+    W* dst = reinterpret_cast<W*>(L.dst[e]);
+    const int64_t nw = L.len[e] / (int64_t)sizeof(W);
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nw; i += (int64_t)gridDim.x * 256) dst[i] = src[i];
+    if (blockIdx.x == 0 && threadIdx.x < (int)(L.len[e] % (int64_t)sizeof(W))) {
+        const int64_t b = nw * (int64_t)sizeof(W) + threadIdx.x;
+        L.dst[e][b] = L.src[e][b];
+    }
+    __threadfence_system();  // host-visible before the batch's completion event
+}
+
+struct CopyEntry {
+    const uint8_t* src;
+    uint8_t* dst;
+    int64_t len;
+};
+
+int run_copy_list(const std::vector<CopyEntry>& v, hipStream_t st) {
+    for (size_t i0 = 0; i0 < v.size(); i0 += CL_MAX) {
+        CopyList L{};
+        L.n = (int)std::min<size_t>(CL_MAX, v.size() - i0);
+        uintptr_t al = 0;
+        int64_t mx = 0;
+        for (int j = 0; j < L.n; ++j) {
+            const CopyEntry& c = v[i0 + (size_t)j];
+            L.src[j] = c.src;
+            L.dst[j] = c.dst;
+            L.len[j] = c.len;
+            al |= (uintptr_t)c.src | (uintptr_t)c.dst;
+            mx = std::max(mx, c.len);
+        }
+        const int w = (al & 15) == 0 ? 16 : (al & 7) == 0 ? 8 : (al & 3) == 0 ? 4 : 1;
+        const int64_t words = mx / w;
+        const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(64, (words + 1023) / 1024));
+        const dim3 grid(gx, (unsigned)L.n);
+        if (w == 16)
+            hipLaunchKernelGGL(k_copy_list<uint4>, grid, dim3(256), 0, st, L);
+        else if (w == 8)
+            hipLaunchKernelGGL(k_copy_list<uint2>, grid, dim3(256), 0, st, L);
+        else if (w == 4)
+            hipLaunchKernelGGL(k_copy_list<uint32_t>, grid, dim3(256), 0, st, L);
+        else
+            hipLaunchKernelGGL(k_copy_list<uint8_t>, grid, dim3(256), 0, st, L);
+        if (hipGetLastError() != hipSuccess) return ZS3_ERR_DEVICE;
+    }
+    return ZS3_OK;
+}
+
 // Calls f(a, b) for every maximal run [a, b) of positions < n with skip[pos] == 0.
 template <class F>
 void for_runs(const std::vector<uint8_t>& skip, int n, F f) {
@@ -265,18 +348,27 @@ void launch_slot(zs3_queue* q, Slot* s) {
             // blocks were copied in by their submitter and get their parity rows
             // straight back into the caller's buffer
             std::vector<uint8_t> zc((size_t)nf, 0);
+            std::vector<CopyEntry> gin, gout;
             for (zs3_req* r : s->reqs)
-                if (r->pos < nf && r->zc) zc[(size_t)r->pos] = 1;
+                if (r->pos < nf && r->zc) {
+                    zc[(size_t)r->pos] = 1;
+                    if (r->d_map) {
+                        gin.push_back({r->d_map, s->d + r->pos * KS, r->len});
+                        gout.push_back({s->d + po + r->pos * MS, r->d_map + KS, (int64_t)MS});
+                    }
+                }
             for_runs(zc, nf, [&](int a, int b) {
                 chk(map_hip(hipMemcpyAsync(s->d + a * KS, s->h + a * KS, (size_t)(b - a) * KS, hipMemcpyHostToDevice, st)));
             });
+            if (!gin.empty()) chk(run_copy_list(gin, st));
             chk(zs3_encode_batch(q->c, s->d, (int64_t)KS, q->B, nf, s->d + po, (int64_t)MS, dsum, st));
             for_runs(zc, nf, [&](int a, int b) {
                 chk(map_hip(hipMemcpyAsync(s->h + po + a * MS, s->d + po + a * MS, (size_t)(b - a) * MS,
                                            hipMemcpyDeviceToHost, st)));
             });
+            if (!gout.empty()) chk(run_copy_list(gout, st));
             for (zs3_req* r : s->reqs)
-                if (r->pos < nf && r->zc)
+                if (r->pos < nf && r->zc && !r->d_map)
                     chk(map_hip(hipMemcpyAsync(r->h_buf + KS, s->d + po + r->pos * MS, MS, hipMemcpyDeviceToHost, st)));
             chk(map_hip(hipMemcpyAsync(hsum, dsum, (size_t)nf * R * 32, hipMemcpyDeviceToHost, st)));
         }
@@ -299,12 +391,25 @@ void launch_slot(zs3_queue* q, Slot* s) {
         std::vector<int32_t> status;
         if (nf > 0) {
             std::vector<uint8_t> zc((size_t)nf, 0);
+            std::vector<CopyEntry> gin;
             for (zs3_req* r : s->reqs)
-                if (r->pos < nf && r->zc) zc[(size_t)r->pos] = 1;
+                if (r->pos < nf && r->zc) {
+                    zc[(size_t)r->pos] = 1;
+                    if (r->d_map) {
+                        // the survivors, one entry per run of present rows
+                        std::vector<uint8_t> absent((size_t)R);
+                        for (int i = 0; i < R; ++i) absent[(size_t)i] = !r->present[i];
+                        for_runs(absent, R, [&](int a, int b) {
+                            gin.push_back({r->d_map + (size_t)a * S, s->d + (size_t)r->pos * E + (size_t)a * S,
+                                           (int64_t)(b - a) * S});
+                        });
+                    }
+                }
             for_runs(zc, nf, [&](int a, int b) {
                 chk(map_hip(hipMemcpyAsync(s->d + (size_t)a * E, s->h + (size_t)a * E, (size_t)(b - a) * E,
                                            hipMemcpyHostToDevice, st)));
             });
+            if (!gin.empty()) chk(run_copy_list(gin, st));
             chk(map_hip(hipMemcpyAsync(dsum, hsum, (size_t)nf * R * 32, hipMemcpyHostToDevice, st)));
             pres.assign((size_t)nf * R, 0);
             status.assign((size_t)nf, ZS3_OK);
@@ -334,16 +439,22 @@ void launch_slot(zs3_queue* q, Slot* s) {
             if (dout) chk(map_hip(hipMemcpyAsync(hout + so, dout + so, (size_t)R * 32, hipMemcpyDeviceToHost, st)));
         }
         // rebuilt rows back to the pinned slot (only those, per block), or straight into
-        // a zero-copy caller's shard rows
+        // a zero-copy caller's shard rows (copy-list mode: one launch for the batch)
+        std::vector<CopyEntry> gout;
         for (zs3_req* r : s->reqs) {
             if (r->status != ZS3_OK) continue;
             const size_t o = (size_t)r->pos * E;
             uint8_t* hdst = r->zc ? r->h_shards : s->h + o;
             for (int i = 0; i < R; ++i)
-                if (!r->present[i] && (i < k || !data_only))
-                    chk(map_hip(hipMemcpyAsync(hdst + (size_t)i * r->S, s->d + o + (size_t)i * r->S, (size_t)r->S,
-                                               hipMemcpyDeviceToHost, st)));
+                if (!r->present[i] && (i < k || !data_only)) {
+                    if (r->zc && r->d_map)
+                        gout.push_back({s->d + o + (size_t)i * r->S, r->d_map + (size_t)i * r->S, r->S});
+                    else
+                        chk(map_hip(hipMemcpyAsync(hdst + (size_t)i * r->S, s->d + o + (size_t)i * r->S,
+                                                   (size_t)r->S, hipMemcpyDeviceToHost, st)));
+                }
         }
+        if (!gout.empty()) chk(run_copy_list(gout, st));
     }
     chk(map_hip(hipEventRecord(s->done_ev, st)));
     s->launch_status = rc;
@@ -506,6 +617,7 @@ int zs3_queue_new(const zs3_codec* c, const zs3_queue_opts* opts, zs3_queue** ou
         if (opts->slots > 0) q->nslots = opts->slots;
     }
     if (q->nslots < 2) q->nslots = 2;
+    if (const char* e = std::getenv("ZS3_QUEUE_ZC")) q->zc_mode = std::max(0, std::min(3, std::atoi(e)));
     int prev = dev;
     if (hipSetDevice(q->device) != hipSuccess) {
         delete q;
@@ -570,10 +682,19 @@ int zs3_queue_submit_encode(zs3_queue* q, uint8_t* h_buf, int64_t len, int64_t c
     // Split (reedsolomon): data rows are the input bytes, zero-padded to k*S (the
     // kernel reads the pad of a full block as zero).  A full block in pinned memory is
     // DMA'd from the caller's buffer on the slot's stream, ahead of the batch's launch.
+    // Copy-list mode: the batch's launch moves it (run_copy_list).
     const size_t KS = (size_t)q->k * q->S;
-    if (len == q->B && zs3i_pinned(h_buf, (size_t)q->R * q->S))
-        r->zc = hipMemcpyAsync(s->d + (size_t)r->pos * KS, h_buf, (size_t)len, hipMemcpyHostToDevice, s->stream) ==
-                hipSuccess;
+    void* dmap = nullptr;
+    const bool zc_try = q->zc_mode == 2 || q->zc_mode == 3 || (q->zc_mode == 1 && r->pos == 0);
+    if (len == q->B && zc_try && zs3i_pinned_map(h_buf, (size_t)q->R * q->S, &dmap)) {
+        if (q->zc_mode == 3) {
+            r->zc = true;
+            r->d_map = (uint8_t*)dmap;
+        } else {
+            r->zc = hipMemcpyAsync(s->d + (size_t)r->pos * KS, h_buf, (size_t)len, hipMemcpyHostToDevice,
+                                   s->stream) == hipSuccess;
+        }
+    }
     if (r->zc) q->n_zc.fetch_add(1);
     if (!r->zc) {
         uint8_t* dst = s->h + (size_t)r->pos * KS;
@@ -613,7 +734,13 @@ int zs3_queue_submit_decode(zs3_queue* q, uint8_t* h_shards, int64_t shard_len, 
     }
     // survivors: DMA'd straight from a pinned caller buffer (runs of present rows, same
     // row layout as the slot), else copied into the pinned slot
-    if (shard_len == q->S && zs3i_pinned(h_shards, (size_t)q->E)) {
+    void* dmap = nullptr;
+    const bool zc_try = q->zc_mode == 2 || (q->zc_mode == 1 && r->pos == 0);
+    if (shard_len == q->S && q->zc_mode == 3 && zs3i_pinned_map(h_shards, (size_t)q->E, &dmap)) {
+        r->zc = true;  // gathered by the batch's copy-list launch
+        r->d_map = (uint8_t*)dmap;
+        q->n_zc.fetch_add(1);
+    } else if (shard_len == q->S && zc_try && zs3i_pinned(h_shards, (size_t)q->E)) {
         std::vector<uint8_t> absent((size_t)q->R);
         for (int i = 0; i < q->R; ++i) absent[(size_t)i] = !r->present[i];
         bool ok = true;

@@ -301,21 +301,30 @@ size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
 // Live zs3_host_alloc ranges (base -> bytes): the queue DMAs straight from / to a
 // caller buffer that lies in one of them (the pinned bpool, internal/bpool/bpool.go:29)
+struct PinnedRange {
+    size_t bytes;
+    uintptr_t dev;  // the allocation's device-side address (hipHostGetDevicePointer)
+};
 std::mutex g_pin_mu;
-std::map<uintptr_t, size_t> g_pinned;
+std::map<uintptr_t, PinnedRange> g_pinned;
 
 }  // namespace
 
-// [p, p+n) inside one live zs3_host_alloc allocation (queue.hip's zero-copy test)
-__attribute__((visibility("hidden"))) bool zs3i_pinned(const void* p, size_t n) {
+// [p, p+n) inside one live zs3_host_alloc allocation (queue.hip's zero-copy test); *dev
+// (optional) receives the address a kernel uses for p (the mapped pinned pages)
+__attribute__((visibility("hidden"))) bool zs3i_pinned_map(const void* p, size_t n, void** dev) {
     if (!p) return false;
     const uintptr_t a = (uintptr_t)p;
     std::lock_guard<std::mutex> g(g_pin_mu);
     auto it = g_pinned.upper_bound(a);
     if (it == g_pinned.begin()) return false;
     --it;
-    return a >= it->first && a - it->first <= it->second && n <= it->second - (a - it->first);
+    const size_t sz = it->second.bytes;
+    if (!(a >= it->first && a - it->first <= sz && n <= sz - (a - it->first))) return false;
+    if (dev) *dev = (void*)(it->second.dev + (a - it->first));
+    return true;
 }
+__attribute__((visibility("hidden"))) bool zs3i_pinned(const void* p, size_t n) { return zs3i_pinned_map(p, n, nullptr); }
 
 extern "C" {
 
@@ -351,10 +360,12 @@ int zs3_dev_alloc(void** d_ptr, size_t bytes) {
 int zs3_dev_free(void* d_ptr) { return map_hip(hipFree(d_ptr)); }
 int zs3_host_alloc(void** h_ptr, size_t bytes) {
     if (!h_ptr) return ZS3_ERR_INVALID_ARG;
-    const int rc = map_hip(hipHostMalloc(h_ptr, bytes, hipHostMallocDefault));
+    int rc = map_hip(hipHostMalloc(h_ptr, bytes, hipHostMallocMapped | hipHostMallocPortable));
     if (rc == ZS3_OK && *h_ptr) {
+        void* dev = nullptr;
+        if (hipHostGetDevicePointer(&dev, *h_ptr, 0) != hipSuccess || !dev) dev = *h_ptr;  // unified addressing
         std::lock_guard<std::mutex> g(g_pin_mu);
-        g_pinned[(uintptr_t)*h_ptr] = bytes;
+        g_pinned[(uintptr_t)*h_ptr] = PinnedRange{bytes, (uintptr_t)dev};
     }
     return rc;
 }
@@ -563,26 +574,42 @@ int zs3_verify_reconstruct_batch(const zs3_codec* cc, uint8_t* d_shards, int64_t
 }
 
 static int digest_batch(bool sha, const uint8_t* d_msgs, int64_t stride, int64_t len, const int64_t* d_lens,
-                        int64_t n, uint8_t* d_out, void* stream) {
+                        const int64_t* d_offs, int64_t n, uint8_t* d_out, void* stream) {
     if (n < 0 || (n > 0 && (!d_out || !d_msgs)) || (!d_lens && len < 0)) return ZS3_ERR_INVALID_ARG;
+    // one message's block count is kept in 32 bits by the kernels
+    if (!d_lens && len >= ((int64_t)1 << 36)) return ZS3_ERR_INVALID_ARG;
     zs3k::DigestArgs a{};
     a.msgs = d_msgs;
     a.stride = stride;
     a.len = len;
     a.lens = d_lens;
+    a.offs = d_offs;
     a.n = n;
     a.out = d_out;
+    a.variant = call_variant();
     return map_hip(sha ? zs3k::launch_sha256(a, (hipStream_t)stream) : zs3k::launch_md5(a, (hipStream_t)stream));
 }
 
 int zs3_md5_batch(const uint8_t* d_msgs, int64_t stride, int64_t len, const int64_t* d_lens, int64_t n,
                   uint8_t* d_out, void* stream) {
-    return digest_batch(false, d_msgs, stride, len, d_lens, n, d_out, stream);
+    return digest_batch(false, d_msgs, stride, len, d_lens, nullptr, n, d_out, stream);
 }
 
 int zs3_sha256_batch(const uint8_t* d_msgs, int64_t stride, int64_t len, const int64_t* d_lens, int64_t n,
                      uint8_t* d_out, void* stream) {
-    return digest_batch(true, d_msgs, stride, len, d_lens, n, d_out, stream);
+    return digest_batch(true, d_msgs, stride, len, d_lens, nullptr, n, d_out, stream);
+}
+
+int zs3_md5_parts(const uint8_t* d_base, const int64_t* d_offsets, const int64_t* d_lens, int64_t n,
+                  uint8_t* d_out, void* stream) {
+    if (n > 0 && (!d_offsets || !d_lens)) return ZS3_ERR_INVALID_ARG;
+    return digest_batch(false, d_base, 0, 0, d_lens, d_offsets, n, d_out, stream);
+}
+
+int zs3_sha256_parts(const uint8_t* d_base, const int64_t* d_offsets, const int64_t* d_lens, int64_t n,
+                     uint8_t* d_out, void* stream) {
+    if (n > 0 && (!d_offsets || !d_lens)) return ZS3_ERR_INVALID_ARG;
+    return digest_batch(true, d_base, 0, 0, d_lens, d_offsets, n, d_out, stream);
 }
 
 // etag.Multipart (internal/etag/etag.go:211-226): skip multipart ("-N") and encrypted

@@ -8,7 +8,7 @@
 //
 // Before round 4 these ran the any-geometry encode (8-byte columns) + a separate
 // stripe-mode hash launch: 23-26 % of 8 TB/s at 4096 x 1 MiB encode + sums
-// (profiles/r04/r04_geom.jsonl); RS(2+2) / (4+3) the first-generation fused kernel (44 / 51 %).
+// (profiles/r04/geom_before.jsonl); RS(2+2) / (4+3) the first-generation fused kernel (44 / 51 %).
 // Here the encode role multiplies every data row into every parity row (GEN: the general
 // M x K matrix, encode_general) with the coefficient tables in LDS; the rest is the
 // RS(12+4) unaligned-row recipe: buffer-addressed columns, non-temporal loads and stores,

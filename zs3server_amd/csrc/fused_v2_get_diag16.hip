@@ -6,38 +6,15 @@
 namespace zs3k {
 
 #if ZS3_DIAG
-// round 4: fewer barriers per hashed byte for the chain-latency-bound RS(16+4) rebuild /
-// heal of 3-4 rows (the RS(4+m) instances gained 20-30 % from 1 KiB tiles):
-//  273: 4 stripes, 768-byte tiles (LDS for 20 hashed rows), 8-byte columns
-//  274: 8 stripes, 512-byte tiles (rebuild, heal <= 2: LDS)
-//  275: quad-form hash waves beside the product's 384-byte tiles
-//  276: 16-byte rebuild columns of 384-byte tiles: 3 rebuild waves, so heal 4 is one
-//       8-wave workgroup with the 256-VGPR budget (the product's 11 waves get 168 and
-//       spill 44-58 VGPRs in the rebuild loop)
-//  277: 16-byte rebuild columns of 512-byte tiles (rebuild; heal 1-2)
-template <int EX, bool H>
-static bool vr16_r4(int v, const VrArgs& a, hipStream_t s) {
-    switch (v) {
-        case 276: return launch_vr_ws_t<16, EX, H, 8, 384, 1, 16, false, true, 4>(a, s);
-        case 277: return launch_vr_ws_t<16, EX, H, 8, 512, 1, 16, false, true, 4>(a, s);
-        case 273: return launch_vr_ws_t<16, EX, H, 4, 768, 1, 8, false, true, 4>(a, s);
-        case 274: return launch_vr_ws_t<16, EX, H, 8, 512, 1, 8, false, true, 4>(a, s);
-        case 275: return launch_vr_ws_t<16, EX, H, 8, 384, 1, 8, true, true, 4>(a, s);
-        default: return false;
-    }
-}
-
+// Round 4 candidates for the RS(16+4) rebuild / heal of 3-4 rows, measured and dropped
+// (profiles/r04/get_ab_k16.jsonl, 2048 x 1 MiB; their instances are no longer compiled):
+//  273: 4 stripes, 768-byte tiles          heal 4 0.88 vs 0.78 ms, rebuild 4 0.73 vs 0.76
+//  274: 8 stripes, 512-byte tiles          = the product rebuild shape; heal 1.05-1.35 ms
+//  275: quad-form hash waves               1.3-2.8 ms (spills 100-190 VGPRs)
+//  276 / 277: 16-byte rebuild columns      spill 100-570 VGPRs at compile time
+// The product RS(16+4) rebuild 3-4 / heal 2-4 instances spill 44-58 VGPRs at the 168-VGPR
+// budget of their 11-wave workgroups.
 bool launch_vr_ws_diag_k16(int v, const VrArgs& a, hipStream_t s) {
-    if (a.k == 16 && v >= 273 && v <= 277) {
-        const bool h = a.sums_out != nullptr;
-        switch (a.e) {
-            case 1: return h ? vr16_r4<1, true>(v, a, s) : vr16_r4<1, false>(v, a, s);
-            case 2: return h ? vr16_r4<2, true>(v, a, s) : vr16_r4<2, false>(v, a, s);
-            case 3: return h ? vr16_r4<3, true>(v, a, s) : vr16_r4<3, false>(v, a, s);
-            case 4: return h ? vr16_r4<4, true>(v, a, s) : vr16_r4<4, false>(v, a, s);
-            default: return false;
-        }
-    }
     // survivor prefetch depth / tile length / column width candidates (round 3); the
     // rejected ones (251-255, 257: 8-45 % slower, profiles/r03/get_ab_rs164_vr16.jsonl)
     // are no longer compiled; 250 / 256 / 259 became the product instances

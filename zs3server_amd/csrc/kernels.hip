@@ -748,7 +748,7 @@ __global__ void __launch_bounds__(64) k_vr_hash_lat(VrArgs a, int nr) {
     }
 }
 
-// Crossover of the split path against the fused kernels (sweep_sizes_small.txt,
+// Crossover of the split path against the fused kernels (profiles/r02/sweep_sizes_small_v49.txt,
 // sweep_cliffs.jsonl): RS(8+4) between 512 and 768 blocks (~1 GB of stripes), RS(16+4)
 // at 512 (448: 1516 vs 1463 GiB/s, 512: 1634 vs 1662).
 template <int K, int M>
@@ -1551,7 +1551,7 @@ static hipError_t run_encode_fast(const EncArgs& a, hipStream_t s, int* path) {
         constexpr int T = pick_T<G * R, NBUF>();
         // Small batches are bound by one hash chain's latency, not by bytes: the split
         // path (encode-only pass + k_hash_lat) halves that (RS(8+4) 1 block: 0.23 vs
-        // 0.53 ms; profiles/r02/sweep_sizes_small.txt).  Not for RS(4+2), whose
+        // 0.53 ms; profiles/r02/sweep_sizes_small_v49.txt).  Not for RS(4+2), whose
         // quad-form k_ehx_ws chains run faster than k_hash_lat's at every size.
         if (a.variant == 0 && small_batch<K, M>(a.n_blocks, a.S)) {
             launch_encode_lat<K, M>(a, s);
@@ -1870,7 +1870,7 @@ static hipError_t launch_vr_lat(const VrArgs& a, hipStream_t s) {
 }
 
 // Crossover of the GET / heal latency path against the fused kernels (NOBJ sweeps of
-// scripts/get_ab2.py, profiles/r02/get_lat.txt).  RS(4+2): the quad-form k_vr_ws
+// scripts/get_ab2.py, profiles/r02/get_lat_large_n.txt, get_small_batches.jsonl).  RS(4+2): the quad-form k_vr_ws
 // chains are faster at every size.
 static bool small_get(int k, int m, int e, bool heal, int64_t n, int64_t S) {
     if (k == 4 && m == 2) return false;
@@ -1894,7 +1894,7 @@ static hipError_t run_vr_k(const VrArgs& a, hipStream_t s, int* path) {
     // diagnostics 240: the product dispatch without that path, batched scalar tables
     const int wv = (ZS3_DIAG && (a.variant == 231 || a.variant == 240 || a.variant == 241 || a.variant == 246)) ? 0 : a.variant;
     if (wv == 0 || (ZS3_DIAG && ((wv >= 210 && wv <= 219) || wv == 232 || wv == 242 || (wv >= 250 && wv <= 263) ||
-                                    (wv >= 270 && wv <= 277))))
+                                    (wv >= 270 && wv <= 272))))
         if (launch_vr_ws(wv, a, s)) {
             if (path) *path = PATH_WS;
             return hipGetLastError();

@@ -1075,8 +1075,13 @@ constexpr int vr_nh() {
 // offsets (unaligned-access mode); the ragged tail tile is never prefetched: each lane
 // reads its columns of it byte by byte (zero past the row) and stores only the rebuilt
 // bytes below S.
+// BUF (round 4; aligned rows, no id list): survivor loads and rebuilt-row stores
+// buffer-addressed — one per-lane VGPR offset (the lane's stripe and column inside the
+// workgroup's span) and a wave-uniform SGPR offset per row — instead of one 64-bit VGPR
+// address per survivor row, which the RS(16+4) 3-4-row instances kept as 16 loop
+// invariants and spilled (scratch reloads in the steady loop).
 template <int K, int EX, bool HOUT, int G, int T, int PF, int CW = 16, bool HQ = false, bool ST = false,
-          int BT = 0, bool NTL = false, bool UA = false>
+          int BT = 0, bool NTL = false, bool UA = false, bool BUF = false>
 __global__ void __launch_bounds__((vr_nh<G, K + (HOUT ? EX : 0), HQ>() + G * (T / CW))) __attribute__((amdgpu_waves_per_eu(2)))
 k_vr_ws(VrArgs a) {
     constexpr int RH = K + (HOUT ? EX : 0);
@@ -1211,6 +1216,11 @@ k_vr_ws(VrArgs a) {
     const int64_t b = a.ids ? (int64_t)a.ids[bl] : bl;
     uint8_t* blk = a.shards + b * a.block_stride + o;
     const int col_off = g * RH * TS + o;
+    static_assert(!(BUF && UA), "buffer addressing: aligned rows");
+    // BUF: the launch guarantees no id list and a span of G stripes below 2^31 bytes
+    const __amdgpu_buffer_rsrc_t rs_s =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(a.shards + blk0 * a.block_stride), 0, 0x7FFFFFFF, 0x00020000);
+    const uint32_t vo_s = (uint32_t)((bl - blk0) * a.block_stride + o);
     lds_barrier2();  // tables / rows visible
     // row offsets in 32 bits (the launch requires (k + m) * S < 2^31): half the SGPRs
     uint32_t roff[K];
@@ -1221,18 +1231,42 @@ k_vr_ws(VrArgs a) {
     for (int r = 0; r < EX; ++r) ooff[r] = (uint32_t)__builtin_amdgcn_readfirstlane(srows[K + r]) * (uint32_t)S;
 
     VT x[PF][K];
-    auto load = [&](VT (&xs)[K], int64_t t0) {
+    // t0: wave-uniform tile offset; vx (BUF): a per-lane addition to it (the prefetch of
+    // the partial last tile: lanes past the row's tail re-read tile 0), carried in the
+    // VGPR offset — the SGPR offset is read from lane 0
+    auto load = [&](VT (&xs)[K], int64_t t0, uint32_t vx = 0) {
 #pragma unroll
         for (int j = 0; j < K; ++j) {
-            if constexpr (NTL)
+            if constexpr (BUF) {
+                static_assert(NWd == 2 || NWd == 4, "buffer loads: 8- or 16-byte columns");
+                const uint32_t vo = vo_s + vx;
+                // (the row offset may come out of a v_readfirstlane: an SGPR written by
+                // the VALU needs 5 wait states before a VMEM instruction reads it, which
+                // the compiler does not insert in front of inline asm — hence the s_nop)
+                const uint32_t so = __builtin_amdgcn_readfirstlane(roff[j] + (uint32_t)t0);
+                if constexpr (NWd == 4)
+                    asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, %2, %3 offen nt"
+                                 : "=v"(xs[j])
+                                 : "v"(vo), "s"(rs_s), "s"(so)
+                                 : "memory");
+                else
+                    asm volatile("s_nop 4\n\tbuffer_load_dwordx2 %0, %1, %2, %3 offen nt"
+                                 : "=v"(xs[j])
+                                 : "v"(vo), "s"(rs_s), "s"(so)
+                                 : "memory");
+            } else if constexpr (NTL) {
                 ld_async_nt<NWd>(xs[j], blk + roff[j] + t0);
-            else
+            } else {
                 ld_async<NWd>(xs[j], blk + roff[j] + t0);
+            }
         }
     };
     auto prefetch_any = [&](VT (&xs)[K], int64_t tn) {
         const bool ok = tn < nfull || (!UA && tn == nfull && o < tail);
-        load(xs, ok ? tn * T : 0);
+        if constexpr (BUF)
+            load(xs, 0, ok ? (uint32_t)(tn * T) : 0u);  // per-lane choice: VGPR offset
+        else
+            load(xs, ok ? tn * T : 0);
     };
     // UA tail tile: bytes [o, o + CW) of every survivor row, zero past the row
     auto tail_cols = [&](VT (&xs)[K]) {
@@ -1326,7 +1360,16 @@ k_vr_ws(VrArgs a) {
     auto store_rows = [&](const Col<NWd> (&y)[EX > 0 ? EX : 1], int64_t t0) {
 #pragma unroll
         for (int r = 0; r < EX; ++r) {
-            if constexpr (NTL)
+            if constexpr (BUF) {
+                const int so = (int)__builtin_amdgcn_readfirstlane(ooff[r] + (uint32_t)t0);
+                if constexpr (NWd == 4) {
+                    const VT v = {y[r].w[0], y[r].w[1], y[r].w[2], y[r].w[3]};
+                    __builtin_amdgcn_raw_buffer_store_b128(v, rs_s, (int)vo_s, so, 2);
+                } else {
+                    const VT v = {y[r].w[0], y[r].w[1]};
+                    __builtin_amdgcn_raw_buffer_store_b64(v, rs_s, (int)vo_s, so, 2);
+                }
+            } else if constexpr (NTL)
                 st_col_nt<NWd>(blk + ooff[r] + t0, y[r]);
             else
                 st_col<NWd>(blk + ooff[r] + t0, y[r]);
@@ -1387,12 +1430,21 @@ k_vr_ws(VrArgs a) {
 }
 
 template <int K, int EX, bool HOUT, int G, int T, int PF, int CW, bool HQ, bool ST, int BT, bool NTL = false,
-          bool UA = false>
+          bool UA = false, bool BUF = false>
 static bool launch_vr_ws_bt(const VrArgs& a, hipStream_t s);
 
 template <int K, int EX, bool HOUT, int G, int T, int PF, int CW = 16, bool HQ = false, bool ST = false,
-          int BT = 0, bool UA = false>
+          int BT = 0, bool UA = false, bool BUF = false>
 static bool launch_vr_ws_t(const VrArgs& a, hipStream_t s) {
+    if constexpr (BUF && !UA) {
+        // buffer addressing needs the G stripes of a workgroup in order (no id list) and
+        // their span below 2^31 bytes; otherwise the 64-bit-address instance (diagnostics
+        // 247: always that one)
+        if (!a.ids && (int64_t)G * a.block_stride < ((int64_t)1 << 31) && a.block_stride > 0 &&
+            !(ZS3_DIAG && a.variant == 247))
+            return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, BT, true, false, true>(a, s);
+        return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, BT, true>(a, s);
+    }
     if constexpr (UA) {
         // plain (temporal) survivor loads: with unaligned rows each tile's first and last
         // 128-byte lines are shared with the neighbouring tiles, and non-temporal loads
@@ -1416,7 +1468,7 @@ static bool launch_vr_ws_t(const VrArgs& a, hipStream_t s) {
     }
 }
 
-template <int K, int EX, bool HOUT, int G, int T, int PF, int CW, bool HQ, bool ST, int BT, bool NTL, bool UA>
+template <int K, int EX, bool HOUT, int G, int T, int PF, int CW, bool HQ, bool ST, int BT, bool NTL, bool UA, bool BUF>
 static bool launch_vr_ws_bt(const VrArgs& a, hipStream_t s) {
     constexpr int RH = K + (HOUT ? EX : 0);
     constexpr int NT = vr_nh<G, RH, HQ>() + G * (T / CW);
@@ -1429,7 +1481,7 @@ static bool launch_vr_ws_bt(const VrArgs& a, hipStream_t s) {
         if (a.e != EX || (!UA && (a.S % 16) != 0) || a.k != K || (HOUT != (a.sums_out != nullptr) && EX > 0))
             return false;
         if ((int64_t)(a.k + a.m) * a.S >= ((int64_t)1 << 31)) return false;  // 32-bit row offsets
-        auto kern = k_vr_ws<K, EX, HOUT, G, T, PF, CW, HQ, ST, BT, NTL, UA>;
+        auto kern = k_vr_ws<K, EX, HOUT, G, T, PF, CW, HQ, ST, BT, NTL, UA, BUF>;
         if (ensure_dyn_lds((const void*)kern, dyn) != hipSuccess) return false;
         const int64_t grid = (a.n_blocks + G - 1) / G;
         hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), dyn, s, a);

@@ -54,8 +54,8 @@ static bool launch_vr_ws_default(const VrArgs& a, hipStream_t s) {
             if (a.e == 0) return launch_vr_ws_t<16, 0, false, 8, 256, 2>(a, s);
             if (a.e == 1) return launch_vr_ws_t<16, 1, false, 8, 256, 2, 4, false, true, 0>(a, s);
             if (a.e == 2) return launch_vr_ws_t<16, 2, false, 8, 256, 2, 4, false, true, 0>(a, s);
-            if (a.e == 3) return launch_vr_ws_t<16, 3, false, 8, 512, 1, 8, false, true, 4>(a, s);
-            if (a.e == 4) return launch_vr_ws_t<16, 4, false, 8, 512, 1, 8, false, true, 4>(a, s);
+            if (a.e == 3) return launch_vr_ws_t<16, 3, false, 8, 512, 1, 8, false, true, 4, false, true>(a, s);
+            if (a.e == 4) return launch_vr_ws_t<16, 4, false, 8, 512, 1, 8, false, true, 4, false, true>(a, s);
             return false;
         }
         // heal 1-4: 8-byte rebuild columns of 384-byte tiles (6 rebuild waves beside 5
@@ -63,10 +63,10 @@ static bool launch_vr_ws_default(const VrArgs& a, hipStream_t s) {
         // 1 MiB: heal 1/2/3/4 0.501/0.573/0.652/0.759 ms vs 0.525/0.816/0.945/1.073 for
         // the round-2 instances (128-byte tiles, 4-byte columns; diagnostics 242)
         // (variant 259, profiles/r03/get_ab_rs164_vr16*.jsonl)
-        if (a.e == 1) return launch_vr_ws_t<16, 1, true, 8, 384, 1, 8, false, true, 4>(a, s);
-        if (a.e == 2) return launch_vr_ws_t<16, 2, true, 8, 384, 1, 8, false, true, 4>(a, s);
-        if (a.e == 3) return launch_vr_ws_t<16, 3, true, 8, 384, 1, 8, false, true, 4>(a, s);
-        if (a.e == 4) return launch_vr_ws_t<16, 4, true, 8, 384, 1, 8, false, true, 4>(a, s);
+        if (a.e == 1) return launch_vr_ws_t<16, 1, true, 8, 384, 1, 8, false, true, 4, false, true>(a, s);
+        if (a.e == 2) return launch_vr_ws_t<16, 2, true, 8, 384, 1, 8, false, true, 4, false, true>(a, s);
+        if (a.e == 3) return launch_vr_ws_t<16, 3, true, 8, 384, 1, 8, false, true, 4, false, true>(a, s);
+        if (a.e == 4) return launch_vr_ws_t<16, 4, true, 8, 384, 1, 8, false, true, 4, false, true>(a, s);
         return false;
     }
     if (a.k == 12 && (a.S % 16) != 0) {
@@ -107,8 +107,8 @@ static bool launch_vr_ws_default(const VrArgs& a, hipStream_t s) {
         // profiles/r03/get_ab_r03_84.jsonl)
         if (a.e == 1) return launch_vr_ws_t<8, 1, true, 16, 128, 2, 8, false, true, 4>(a, s);
         if (a.e == 2) return launch_vr_ws_t<8, 2, true, 16, 128, 2, 8, false, true, 4>(a, s);
-        if (a.e == 3) return launch_vr_ws_t<8, 3, true, 16, 256, 1, 16, false, true, 4>(a, s);
-        if (a.e == 4) return launch_vr_ws_t<8, 4, true, 16, 256, 1, 16, false, true, 4>(a, s);
+        if (a.e == 3) return launch_vr_ws_t<8, 3, true, 16, 256, 1, 16, false, true, 4, false, true>(a, s);
+        if (a.e == 4) return launch_vr_ws_t<8, 4, true, 16, 256, 1, 16, false, true, 4, false, true>(a, s);
         return false;
     }
     // RS(8+4) GET: 16 stripes, 256-byte tiles, verify-only or rebuild 1-2 with 16-byte
@@ -119,8 +119,8 @@ static bool launch_vr_ws_default(const VrArgs& a, hipStream_t s) {
     if (a.e == 0) return launch_vr_ws_t<8, 0, false, 16, 256, 2>(a, s);
     if (a.e == 1) return launch_vr_ws_t<8, 1, false, 16, 256, 2>(a, s);
     if (a.e == 2) return launch_vr_ws_t<8, 2, false, 16, 256, 2>(a, s);
-    if (a.e == 3) return launch_vr_ws_t<8, 3, false, 16, 256, 1, 8, false, true, 4>(a, s);
-    if (a.e == 4) return launch_vr_ws_t<8, 4, false, 16, 256, 1, 8, false, true, 4>(a, s);
+    if (a.e == 3) return launch_vr_ws_t<8, 3, false, 16, 256, 1, 8, false, true, 4, false, true>(a, s);
+    if (a.e == 4) return launch_vr_ws_t<8, 4, false, 16, 256, 1, 8, false, true, 4, false, true>(a, s);
     return false;
 }
 

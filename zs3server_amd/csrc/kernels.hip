@@ -1892,7 +1892,8 @@ static hipError_t run_vr_k(const VrArgs& a, hipStream_t s, int* path) {
     // force the first-generation kernel.
     // diagnostics 231: the product dispatch without the latency path
     // diagnostics 240: the product dispatch without that path, batched scalar tables
-    const int wv = (ZS3_DIAG && (a.variant == 231 || a.variant == 240 || a.variant == 241 || a.variant == 246)) ? 0 : a.variant;
+    const int wv = (ZS3_DIAG && (a.variant == 231 || a.variant == 240 || a.variant == 241 || a.variant == 246 ||
+                                  a.variant == 247)) ? 0 : a.variant;
     if (wv == 0 || (ZS3_DIAG && ((wv >= 210 && wv <= 219) || wv == 232 || wv == 242 || (wv >= 250 && wv <= 263) ||
                                     (wv >= 270 && wv <= 272))))
         if (launch_vr_ws(wv, a, s)) {

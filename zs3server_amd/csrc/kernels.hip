@@ -1645,7 +1645,7 @@ hipError_t launch_encode(const EncArgs& a, hipStream_t s, int* path) {
     // fused encode + sums at shard sizes that are not a multiple of 16 (RS(12+4) on
     // 1 MiB blocks: S = 87 382)
     // (diagnostics: the RS(12+4) UA variants of fused_v2_km124.hip, same guard)
-    if (a.sums && a.dyb && (a.variant == 0 || (ZS3_DIAG && a.variant >= 100 && a.variant < 200))) {
+    if (a.sums && a.dyb && (a.variant == 0 || (ZS3_DIAG && ((a.variant >= 100 && a.variant < 200) || a.variant >= 330)))) {
         const int p = a.variant == 0 ? launch_ehx_ua(a, s) : launch_ehx(a.variant, a, s);
         if (p != PATH_NONE) {
             if (path) *path = p;

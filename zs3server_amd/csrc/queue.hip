@@ -105,6 +105,7 @@ struct Slot {
     hipStream_t stream = nullptr;  // per slot: batches overlap each other's copies and kernels
     int launch_status = ZS3_OK;
     bool ready = false;                          // results are in the pinned slot
+    int nblocks = 0;                             // blocks at launch (inflight_blocks)
     std::unique_ptr<std::atomic<uint8_t>[]> claimed;  // [cap] block copied out by one thread
     std::atomic<int> pending{0};                 // blocks not yet finished (+1 completer)
 };
@@ -143,6 +144,9 @@ struct zs3_queue {
     int lane_state[NLANE] = {LANE_NONE, LANE_NONE, LANE_NONE};
     Slot* open[NLANE] = {nullptr, nullptr, nullptr};
     int inflight[NLANE] = {0, 0, 0};
+    int inflight_blocks[NLANE] = {0, 0, 0};  // blocks of the launched, unfinished slots
+    std::vector<Slot*> sealed[NLANE];         // closed to new blocks, waiting for copiers
+    int pipe_cap = 64;                        // ready_to_close: blocks per 64 MiB of input
     std::deque<Slot*> launched;
     bool flush = false;
     bool stop = false;       // dispatcher: drain the open slots and exit
@@ -290,6 +294,8 @@ void for_runs(const std::vector<uint8_t>& skip, int n, F f) {
     }
 }
 
+int pipe_size(const zs3_queue* q, const Slot* s, int lane);
+
 // Reserve a position for one block in the lane's open slot (caller holds lk).
 int reserve(zs3_queue* q, std::unique_lock<std::mutex>& lk, zs3_req* r, bool full) {
     int rc = ensure_lane(q, lk, r->lane);
@@ -302,7 +308,14 @@ int reserve(zs3_queue* q, std::unique_lock<std::mutex>& lk, zs3_req* r, bool ful
             r->pos = full ? s->front++ : q->cap - 1 - s->back++;
             s->copying++;
             s->reqs.push_back(r);
-            if (s->front + s->back == q->cap) q->cv_disp.notify_one();
+            if (s->front + s->back == q->cap || s->front + s->back >= pipe_size(q, s, r->lane)) {
+                // sealed: later submitters open the next slot at once instead of growing this
+                // one while its copiers are still busy (the dispatcher launches it when the
+                // last copier is done)
+                q->sealed[r->lane].push_back(s);
+                q->open[r->lane] = nullptr;
+                q->cv_disp.notify_one();
+            }
             return ZS3_OK;
         }
         if (!s) {
@@ -462,9 +475,22 @@ void launch_slot(zs3_queue* q, Slot* s) {
     q->n_blocks.fetch_add((int64_t)s->reqs.size());
 }
 
+// Blocks at which the open slot closes for pipelining (ready_to_close); caller holds mu.
+int pipe_size(const zs3_queue* q, const Slot* s, int lane) {
+    const int live = (int)s->reqs.size() + q->inflight_blocks[lane];
+    return std::max(8, std::min((live + 1) / 2, q->pipe_cap));
+}
+
 bool ready_to_close(zs3_queue* q, Slot* s, int lane, Clock::time_point now) {
     if (s->reqs.empty()) return false;
     if (s->front + s->back == q->cap || q->flush || q->stop) return true;
+    // Pipelining cap (round 4): T synchronous submitters keep about T blocks live (open
+    // slot + in flight); closing the slot at half of them keeps two batches alternating,
+    // one's H2D under the other's kernel and D2H, instead of one batch of all of them
+    // (1 MiB RS(8+4), 64 submitters: 29.9-30.5 GiB/s at batches of 32 vs 21-24 at 64-128;
+    // 256 submitters: 33-35 at 64; profiles/r04/queue_ab3.jsonl), at most 64 MiB of input
+    // per batch
+    if (s->front + s->back >= pipe_size(q, s, lane)) return true;
     // batch while busy: launch at once while fewer than slots-1 batches are in flight
     // (a small batch is bound by one hash chain's latency, ~0.5 ms for 128 KiB shards,
     // not by its bytes, so concurrent batches on their own streams overlap almost
@@ -480,7 +506,31 @@ void dispatcher(zs3_queue* q) {
         bool launched_any = false;
         auto now = Clock::now();
         Clock::time_point wake = now + std::chrono::milliseconds(50);
+        auto launch = [&](Slot* s, int lane) {
+            s->state = Slot::LAUNCHED;
+            q->inflight[lane]++;
+            s->nblocks = (int)s->reqs.size();
+            q->inflight_blocks[lane] += s->nblocks;
+            q->cv_space.notify_all();  // submitters may open the next slot
+            lk.unlock();
+            launch_slot(q, s);
+            lk.lock();
+            q->launched.push_back(s);
+            q->cv_comp.notify_one();
+            launched_any = true;
+        };
         for (int lane = 0; lane < NLANE; ++lane) {
+            // sealed slots whose copiers are done, oldest first
+            for (size_t i = 0; i < q->sealed[lane].size();) {
+                Slot* s = q->sealed[lane][i];
+                if (s->copying > 0) {
+                    ++i;
+                    continue;
+                }
+                q->sealed[lane].erase(q->sealed[lane].begin() + (std::ptrdiff_t)i);
+                launch(s, lane);
+                i = 0;  // the list may have changed while unlocked
+            }
             Slot* s = q->open[lane];
             if (!s) continue;
             if (!ready_to_close(q, s, lane, now)) {
@@ -492,18 +542,11 @@ void dispatcher(zs3_queue* q) {
             }
             if (s->copying > 0) continue;  // the last copier notifies
             q->open[lane] = nullptr;
-            s->state = Slot::LAUNCHED;
-            q->inflight[lane]++;
-            q->cv_space.notify_all();  // submitters may open the next slot
-            lk.unlock();
-            launch_slot(q, s);
-            lk.lock();
-            q->launched.push_back(s);
-            q->cv_comp.notify_one();
-            launched_any = true;
+            launch(s, lane);
         }
         bool pending = false;
-        for (int lane = 0; lane < NLANE; ++lane) pending |= q->open[lane] && !q->open[lane]->reqs.empty();
+        for (int lane = 0; lane < NLANE; ++lane)
+            pending |= (q->open[lane] && !q->open[lane]->reqs.empty()) || !q->sealed[lane].empty();
         if (!pending) q->flush = false;
         if (q->stop && !pending) break;
         if (!launched_any) q->cv_disp.wait_until(lk, wake);
@@ -549,6 +592,7 @@ void finish_one(zs3_queue* q, Slot* s) {
     s->reqs.clear();
     s->state = Slot::FREE;
     q->inflight[s->lane]--;
+    q->inflight_blocks[s->lane] -= s->nblocks;
     q->cv_space.notify_all();
     q->cv_disp.notify_one();  // batch-while-busy: the next open slot may go now
 }
@@ -617,6 +661,7 @@ int zs3_queue_new(const zs3_codec* c, const zs3_queue_opts* opts, zs3_queue** ou
         if (opts->slots > 0) q->nslots = opts->slots;
     }
     if (q->nslots < 2) q->nslots = 2;
+    q->pipe_cap = (int)std::max<int64_t>(4, std::min<int64_t>(q->cap, ((int64_t)64 << 20) / std::max<int64_t>(1, q->B)));
     if (const char* e = std::getenv("ZS3_QUEUE_ZC")) q->zc_mode = std::max(0, std::min(3, std::atoi(e)));
     int prev = dev;
     if (hipSetDevice(q->device) != hipSuccess) {

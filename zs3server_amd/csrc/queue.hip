@@ -147,6 +147,7 @@ struct zs3_queue {
     int inflight_blocks[NLANE] = {0, 0, 0};  // blocks of the launched, unfinished slots
     std::vector<Slot*> sealed[NLANE];         // closed to new blocks, waiting for copiers
     int pipe_cap = 64;                        // ready_to_close: blocks per 64 MiB of input
+    int pipe_pct = 50;                        // seal at this % of the live blocks (ZS3_QUEUE_PIPE_PCT)
     std::deque<Slot*> launched;
     bool flush = false;
     bool stop = false;       // dispatcher: drain the open slots and exit
@@ -478,7 +479,7 @@ void launch_slot(zs3_queue* q, Slot* s) {
 // Blocks at which the open slot closes for pipelining (ready_to_close); caller holds mu.
 int pipe_size(const zs3_queue* q, const Slot* s, int lane) {
     const int live = (int)s->reqs.size() + q->inflight_blocks[lane];
-    return std::max(8, std::min((live + 1) / 2, q->pipe_cap));
+    return std::max(8, std::min((live * q->pipe_pct + 99) / 100, q->pipe_cap));
 }
 
 bool ready_to_close(zs3_queue* q, Slot* s, int lane, Clock::time_point now) {
@@ -663,6 +664,7 @@ int zs3_queue_new(const zs3_codec* c, const zs3_queue_opts* opts, zs3_queue** ou
     if (q->nslots < 2) q->nslots = 2;
     q->pipe_cap = (int)std::max<int64_t>(4, std::min<int64_t>(q->cap, ((int64_t)64 << 20) / std::max<int64_t>(1, q->B)));
     if (const char* e = std::getenv("ZS3_QUEUE_ZC")) q->zc_mode = std::max(0, std::min(3, std::atoi(e)));
+    if (const char* e = std::getenv("ZS3_QUEUE_PIPE_PCT")) q->pipe_pct = std::max(10, std::min(100, std::atoi(e)));
     int prev = dev;
     if (hipSetDevice(q->device) != hipSuccess) {
         delete q;

@@ -48,7 +48,8 @@ def main():
     f = chunks(dispatches(sys.argv[1], "FETCH_SIZE"))
     w = chunks(dispatches(sys.argv[2], "WRITE_SIZE"))
     lines = [json.loads(l) for l in open(sys.argv[3]) if l.startswith("{")]
-    lines = [d for d in lines if "roofline" in d]
+    # the part-digest lines time 1 + 2 launches (long single-lane chains): not joined
+    lines = [d for d in lines if "roofline" in d and not d["path"].endswith("_parts")]
     if not (len(f) == len(w) == len(lines)):
         sys.exit(f"chunk count mismatch: fetch {len(f)}, write {len(w)}, lines {len(lines)}")
     with open(sys.argv[4], "w") as out:

@@ -19,7 +19,9 @@
 //  179 / 180 / 181: 196 + L2 prefetch by the hash waves, 2 / 3 / 1 tiles ahead
 //  178: 16 stripes, 16-byte columns of 256-byte tiles: 8 hash + 4 encode waves (2 + 1 per SIMD)
 //  330 / 331 (round 4): the product instance (179) with the conflict-free LDS row stride
-//  (TSP = 1), L2 prefetch 2 / 3 tiles ahead
+//  (TSP = 1), L2 prefetch 2 / 3 tiles ahead (no gain: profiles/r04/sweep_rs124_tsp.jsonl)
+//  332 / 333: the product instance with temporal data loads (nt stores only) / no nt at
+//  all: unaligned rows share each tile's edge lines with the neighbouring tiles
 #include "fused_v2.hpp"
 
 namespace zs3k {
@@ -43,6 +45,8 @@ bool launch_ehx_km_12_4(int v, const EncArgs& a, hipStream_t s) {
         case 166: return launch_ws_t<12, 4, 8, 512, 1, true, false, 0, false, 0, 16, false, 3, false, 0, 0, true, 2>(a, s);
         case 330: return launch_ws_t<12, 4, 8, 512, 1, true, false, 0, false, 0, 8, false, 3, false, 2, 2, true, 3, 1>(a, s);
         case 331: return launch_ws_t<12, 4, 8, 512, 1, true, false, 0, false, 0, 8, false, 3, false, 2, 3, true, 3, 1>(a, s);
+        case 332: return launch_ws_t<12, 4, 8, 512, 1, true, false, 0, false, 0, 8, false, 2, false, 2, 2, true>(a, s);
+        case 333: return launch_ws_t<12, 4, 8, 512, 1, true, false, 0, false, 0, 8, false, 0, false, 2, 2, true>(a, s);
         default: return false;
     }
 }

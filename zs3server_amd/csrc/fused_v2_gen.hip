@@ -14,17 +14,29 @@
 // RS(12+4) unaligned-row recipe: buffer-addressed columns, non-temporal loads and stores,
 // the hash waves touching the data lines two tiles ahead (PFD = 2), UA mode (S = ceil(B/k)
 // is not a multiple of 16 for any k here but 2 and 4), bank-conflict-free LDS rows (TSP 1).
-// Shapes: K+M <= 8: 16 stripes, 16-byte columns of 512-byte tiles (8 encode waves beside
-// 2-4 pair-form hash waves); K+M > 8: 8 stripes, 8-byte columns (K rows of 16-byte columns
-// do not fit the 168-VGPR budget beside the general encode's accumulators).
+// Shapes: k <= 3: 8 stripes, 16-byte columns of 1 KiB tiles (8 encode waves beside 1-2
+// pair-form hash waves); RS(4+3): 16 stripes, 16-byte columns of 512-byte tiles; K+M > 8:
+// 8 stripes, 8-byte columns of 512-byte tiles (K rows of
+// 16-byte columns do not fit the 168-VGPR budget beside the general encode's
+// accumulators).
 #include "fused_v2.hpp"
 
 namespace zs3k {
 
+// Round 4 shape sweep (diagnostics 340-344, profiles/r04/sweep_gen.jsonl, 4096 x 1 MiB):
+// k <= 3 gains from 8 stripes of 1 KiB tiles (each chain hashes 32 packets between
+// barriers; the rows are long: RS(3+3) S = 341 KiB): RS(3+2) 1.91 -> 1.75 ms, RS(3+3)
+// 2.79 -> 2.23, RS(2+2) 2.01 -> 1.90 (geom_r9.jsonl); RS(5+4) / RS(6+4) gain 2 % from temporal data loads without the L2
+// prefetch (2.09 -> 2.04, 1.93 -> 1.89); RS(10+4) keeps the first shape (1 KiB tiles:
+// 1.70 -> 2.90 ms at 8-byte columns).
 template <int K, int M>
 static bool launch_gen_t(const EncArgs& a, hipStream_t s) {
-    if constexpr (K + M <= 8)
+    if constexpr (K <= 3)
+        return launch_ws_t<K, M, 8, 1024, 1, true, false, 0, false, 0, 16, false, 3, false, 0, 2, true, 3, 1, 0, true>(a, s);
+    else if constexpr (K + M <= 8)  // RS(4+3): 1 KiB tiles measured 1.54 -> 1.64 ms (geom_r9.jsonl)
         return launch_ws_t<K, M, 16, 512, 1, true, false, 0, false, 0, 16, false, 3, false, 0, 2, true, 3, 1, 0, true>(a, s);
+    else if constexpr (K <= 6)
+        return launch_ws_t<K, M, 8, 512, 1, true, false, 0, false, 0, 8, false, 2, false, 0, 0, true, 3, 1, 0, true>(a, s);
     else
         return launch_ws_t<K, M, 8, 512, 1, true, false, 0, false, 0, 8, false, 3, false, 0, 2, true, 3, 1, 0, true>(a, s);
 }
@@ -38,8 +50,41 @@ bool has_gen_encode(int k, int m) {
     return false;
 }
 
+#if ZS3_DIAG
+// Diagnostics (round 4) shape candidates for the general-matrix encode + sums:
+//  340: no L2 prefetch by the hash waves (PFD = 0)
+//  341: 384-byte tiles
+//  342: quad-form hash waves (one HH lane per thread)
+//  343: temporal data loads (nt stores only), no L2 prefetch
+//  344: 8 stripes, 1 KiB tiles (fewer barriers per hashed byte)
+template <int K, int M>
+static bool launch_gen_diag(int v, const EncArgs& a, hipStream_t s) {
+    constexpr int G = K + M <= 8 ? 16 : 8;
+    constexpr int CW = K + M <= 8 ? 16 : 8;
+    switch (v) {
+        case 340: return launch_ws_t<K, M, G, 512, 1, true, false, 0, false, 0, CW, false, 3, false, 0, 0, true, 3, 1, 0, true>(a, s);
+        case 341: return launch_ws_t<K, M, G, 384, 1, true, false, 0, false, 0, CW, false, 3, false, 0, 2, true, 3, 1, 0, true>(a, s);
+        case 342: return launch_ws_t<K, M, G, 512, 1, true, true, 0, false, 0, CW, false, 3, false, 0, 0, true, 3, 1, 0, true>(a, s);
+        case 343: return launch_ws_t<K, M, G, 512, 1, true, false, 0, false, 0, CW, false, 2, false, 0, 0, true, 3, 1, 0, true>(a, s);
+        case 344: return launch_ws_t<K, M, 8, 1024, 1, true, false, 0, false, 0, CW, false, 3, false, 0, 2, true, 3, 1, 0, true>(a, s);
+        default: return false;
+    }
+}
+#endif
+
 int launch_ehx_gen(const EncArgs& a, hipStream_t s) {
     if (!a.sums) return PATH_NONE;
+#if ZS3_DIAG
+    if (a.variant >= 340 && a.variant <= 344) {
+        bool ok = false;
+        if (a.k == 3 && a.m == 3) ok = launch_gen_diag<3, 3>(a.variant, a, s);
+        if (a.k == 3 && a.m == 2) ok = launch_gen_diag<3, 2>(a.variant, a, s);
+        if (a.k == 5 && a.m == 4) ok = launch_gen_diag<5, 4>(a.variant, a, s);
+        if (a.k == 6 && a.m == 4) ok = launch_gen_diag<6, 4>(a.variant, a, s);
+        if (a.k == 10 && a.m == 4) ok = launch_gen_diag<10, 4>(a.variant, a, s);
+        return ok ? PATH_WS : PATH_NONE;
+    }
+#endif
 #define X(K, M) \
     if (a.k == K && a.m == M) return launch_gen_t<K, M>(a, s) ? PATH_WS : PATH_NONE;
     ZS3_GEN_KM(X)

@@ -1627,7 +1627,8 @@ hipError_t launch_encode(const EncArgs& a, hipStream_t s, int* path) {
     // RS(2+2) / RS(4+3)) on the warp-specialised kernel with a general matrix
     // (fused_v2_gen.hip) once the batch fills the chip (a workgroup takes 8-16 stripes);
     // smaller batches keep the latency-bound paths below.
-    if (a.sums && a.variant == 0 && a.n_blocks >= 1024 && has_gen_encode(a.k, a.m)) {
+    if (a.sums && (a.variant == 0 || (ZS3_DIAG && a.variant >= 340 && a.variant <= 344)) && a.n_blocks >= 1024 &&
+        has_gen_encode(a.k, a.m)) {
         const int p = launch_ehx_gen(a, s);
         if (p != PATH_NONE) {
             if (path) *path = p;
@@ -1927,7 +1928,8 @@ hipError_t launch_verify_reconstruct(const VrArgs& a, hipStream_t s, int* path) 
     // Server-default geometries whose k is not 4, 8, 12 or 16 (RS(2+2), (3+2), (5+4),
     // (6+4), ...; fused_v2_get_gen.hip): rebuild / heal on the warp-specialised kernel
     // in one launch (4096 x 1 MiB: see that file); small batches keep the launches below
-    if (a.variant == 0 && a.e >= 1 && a.e <= 4 && a.n_blocks >= 1024 && launch_vr_ws_gen(a, s)) {
+    if ((a.variant == 0 || (ZS3_DIAG && (a.variant == 350 || a.variant == 351))) && a.e >= 1 && a.e <= 4 &&
+        a.n_blocks >= 1024 && launch_vr_ws_gen(a, s)) {
         if (path) *path = PATH_WS;
         return hipGetLastError();
     }

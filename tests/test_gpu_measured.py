@@ -554,3 +554,50 @@ def test_default_geometries_encode_only(oracle, k, m):
     for b in (0, nb - 1):
         want = oracle.encode_data(k, m, oracle.fill(k * 17 + m, b, MiB), mat)
         assert np.array_equal(host[b, k * S:].reshape(m, S), want[k:]), b
+
+
+@pytest.mark.parametrize("erased,heal", [([0, 5], False), ([3, 13], True), ([1, 2, 14, 15], True)],
+                         ids=lambda v: str(v))
+def test_rs124_aligned_rows_get_heal(oracle, erased, heal):
+    """RS(12+4) at a 16-byte-aligned shard size (blocks of 12 x 65 536 bytes): GET / heal
+    on the warp-specialised kernel (round 4: the UA instances serve aligned rows too; the
+    first-generation kernel before), 1 401 stripes (past the small-batch latency path's
+    1 GiB, a last workgroup with dead stripes) of 61 distinct oracle stripes, one rotted
+    survivor flagged exactly."""
+    k, m, blen = 12, 4, 12 * 65536
+    R = k + m
+    nb = 1401
+    base, bsum, idx = _tiled_stripes(oracle, k, m, blen, nb, seed=97)
+    S = base.shape[2]
+    assert S % 16 == 0
+    codec = z.Codec(k, m, blen)
+    ref = torch.from_numpy(base).to(DEV)
+    refs = torch.from_numpy(bsum).to(DEV)
+    d = ref[idx].contiguous()
+    for e in erased:
+        d[:, e, :] = 0x5A
+    surv = [i for i in range(R) if i not in erased][:k]
+    bad_blk, bad_row = 500, surv[4]
+    d[bad_blk, bad_row, 777] ^= 0x40
+    exp = refs[idx].contiguous()
+    bad = torch.full((nb, R), 7, dtype=torch.int32, device=DEV)
+    out = torch.zeros((nb, R, 32), dtype=torch.uint8, device=DEV) if heal else None
+    codec.verify_reconstruct_batch(d, R * S, S, nb, [i not in erased for i in range(R)], not heal, exp, bad,
+                                   sums_out=out)
+    torch.cuda.synchronize()
+    assert z.last_path() == 2, z.last_path()
+    want_bad = np.zeros((nb, R), np.int32)
+    want_bad[bad_blk, bad_row] = 1
+    assert np.array_equal(bad.cpu().numpy(), want_bad)
+    ok = torch.ones(nb, dtype=torch.bool, device=DEV)
+    ok[bad_blk] = False
+    for i in erased:
+        if i < k or heal:
+            assert bool((d[:, i, :] == ref[idx, i, :]).all(dim=1)[ok].all()), f"rebuilt shard {i}"
+            if heal:
+                assert bool((out[:, i, :] == refs[idx, i, :]).all(dim=1)[ok].all()), f"heal sum {i}"
+        else:
+            assert bool((d[:, i, :] == 0x5A).all())
+    for i in range(R):
+        if i not in erased:
+            assert bool((d[:, i, :] == ref[idx, i, :]).all(dim=1)[ok].all()), f"survivor {i}"

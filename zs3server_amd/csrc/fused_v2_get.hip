@@ -69,7 +69,9 @@ static bool launch_vr_ws_default(const VrArgs& a, hipStream_t s) {
         if (a.e == 4) return launch_vr_ws_t<16, 4, true, 8, 384, 1, 8, false, true, 4, false, true>(a, s);
         return false;
     }
-    if (a.k == 12 && (a.S % 16) != 0) {
+    if (a.k == 12) {
+        // (UA instances serve 16-byte-aligned rows too: RS(12+4) blocks of 12 * 16 * j
+        // bytes, round 4; before, those fell back to the first-generation kernel)
         // RS(12+4) on 1 MiB blocks (the 16-drive default; S = 87 382, unaligned rows):
         // the RS(16+4) shapes in UA mode (round 3) instead of a survivor-verify hash launch
         // + the reconstruct kernel + a heal hash launch: 4096 x 1 MiB rebuild 2 1.77 ->

@@ -22,6 +22,8 @@
 //  (TSP = 1), L2 prefetch 2 / 3 tiles ahead (no gain: profiles/r04/sweep_rs124_tsp.jsonl)
 //  332 / 333: the product instance with temporal data loads (nt stores only) / no nt at
 //  all: unaligned rows share each tile's edge lines with the neighbouring tiles
+//  335: 4 stripes of 1 KiB tiles; 337: 16-byte columns (4 encode waves) with the
+//  256-VGPR budget, L2 prefetch, conflict-free LDS stride
 #include "fused_v2.hpp"
 
 namespace zs3k {
@@ -47,6 +49,8 @@ bool launch_ehx_km_12_4(int v, const EncArgs& a, hipStream_t s) {
         case 331: return launch_ws_t<12, 4, 8, 512, 1, true, false, 0, false, 0, 8, false, 3, false, 2, 3, true, 3, 1>(a, s);
         case 332: return launch_ws_t<12, 4, 8, 512, 1, true, false, 0, false, 0, 8, false, 2, false, 2, 2, true>(a, s);
         case 333: return launch_ws_t<12, 4, 8, 512, 1, true, false, 0, false, 0, 8, false, 0, false, 2, 2, true>(a, s);
+        case 335: return launch_ws_t<12, 4, 4, 1024, 1, true, false, 0, false, 0, 8, false, 3, false, 2, 2, true, 3, 1>(a, s);
+        case 337: return launch_ws_t<12, 4, 8, 512, 1, true, false, 0, false, 0, 16, false, 3, false, 2, 2, true, 2, 1>(a, s);
         default: return false;
     }
 }

@@ -283,11 +283,15 @@ void zs3_split_range(int64_t total, int world, int rank, int64_t* lo, int64_t* h
  * batches on pinned staging slots, each slot with its own stream:
  *   - a block is copied into the queue's pinned staging by its submitting thread, or,
  *     when the caller's buffer lies inside a zs3_host_alloc allocation (the pinned
- *     bpool) and holds a full-size block, DMA'd from it directly (zero-copy: no host
- *     memcpy either way; parity / rebuilt rows are DMA'd straight back into it);
+ *     bpool), holds a full-size block and opens its batch, DMA'd from it directly
+ *     (zero-copy: no host memcpy either way; parity / rebuilt rows are DMA'd straight
+ *     back into it; later blocks of a batch are staged, which measured faster under
+ *     concurrency);
  *   - a batch is launched when it is full, when fewer than slots-1 batches of its lane
  *     are in flight (batch while busy), when its oldest block has waited max_wait_us,
- *     or on flush;
+ *     or on flush; it is sealed — later blocks open the next batch — once it holds half
+ *     of its lane's live blocks (at least 8, at most 64 MiB of input), so that with T
+ *     synchronous callers two batches of ~T/2 alternate and overlap their copies;
  *   - when the batch is done, zs3_req_wait copies its own block's results back into
  *     the caller's buffers on the calling thread; blocks nobody is waiting for are
  *     copied back by the queue's completion thread.

@@ -1871,7 +1871,7 @@ static hipError_t launch_vr_lat(const VrArgs& a, hipStream_t s) {
 }
 
 // Crossover of the GET / heal latency path against the fused kernels (NOBJ sweeps of
-// scripts/get_ab2.py, profiles/r02/get_lat_large_n.txt, get_small_batches.jsonl).  RS(4+2): the quad-form k_vr_ws
+// profiles/r02/get_lat_large_n.txt, get_small_batches.jsonl).  RS(4+2): the quad-form k_vr_ws
 // chains are faster at every size.
 static bool small_get(int k, int m, int e, bool heal, int64_t n, int64_t S) {
     if (k == 4 && m == 2) return false;

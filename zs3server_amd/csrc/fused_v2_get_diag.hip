@@ -28,12 +28,16 @@ static bool vr12_ua(int v, const VrArgs& a, hipStream_t s) {
             else if constexpr (EX <= 2) return launch_vr_ws_t<12, EX, H, 8, 256, 2, 4, false, true, 0, true>(a, s);
             else return launch_vr_ws_t<12, EX, H, 8, 512, 1, 8, false, true, 4, true>(a, s);
         case 267: return launch_vr_ws_t<12, EX, H, 8, 256, 2, 8, false, true, 4, true>(a, s);
+        // round 4: 4 stripes of 1 KiB tiles (269); two tiles of survivor prefetch at 512
+        // bytes spill in-flight load registers (scripts/check_async_loads.py) and are not
+        // compiled
+        case 269: return launch_vr_ws_t<12, EX, H, 4, 1024, 1, 8, false, true, 4, true>(a, s);
         default: return false;
     }
 }
 
 bool launch_vr_ws_diag(int v, const VrArgs& a, hipStream_t s) {
-    if (a.k == 12 && (a.S % 16) != 0 && v >= 264 && v <= 267) {
+    if (a.k == 12 && v >= 264 && v <= 269) {
         const bool h = a.sums_out != nullptr;
         switch (a.e) {
             case 1: return h ? vr12_ua<1, true>(v, a, s) : vr12_ua<1, false>(v, a, s);

@@ -1948,7 +1948,7 @@ hipError_t launch_verify_reconstruct(const VrArgs& a, hipStream_t s, int* path) 
     // RS(12+4) on 1 MiB blocks (unaligned rows): the warp-specialised kernel in UA mode
     // (diagnostics 97: the any-geometry launches below)
     if (a.e <= 4 && a.k == 12 && !(ZS3_DIAG && a.variant == 97)) {
-        const int wv = (ZS3_DIAG && a.variant >= 264 && a.variant <= 267) ? a.variant : 0;  // diagnostics shapes
+        const int wv = (ZS3_DIAG && a.variant >= 264 && a.variant <= 269) ? a.variant : 0;  // diagnostics shapes
         if (launch_vr_ws(wv, a, s)) {
             if (path) *path = PATH_WS;
             return hipGetLastError();

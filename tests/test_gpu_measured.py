@@ -245,21 +245,24 @@ def test_masks_on_ws_kernel(oracle, k, m, blen, heal):
         assert bool(eq[ok][lost[ok]].all()), "heal sums of the rebuilt rows"
 
 
-@pytest.mark.parametrize("k,m,nb", [(12, 4, 4096), (12, 4, 2051), (12, 4, 1025), (12, 4, 1024), (12, 4, 5), (4, 4, 4096), (4, 4, 1024), (4, 4, 3)])
-def test_server_default_geometries(oracle, k, m, nb):
+@pytest.mark.parametrize("k,m,nb,blen", [(12, 4, 4096, MiB), (12, 4, 2051, MiB), (12, 4, 1025, MiB), (12, 4, 1024, MiB),
+                                         (12, 4, 5, MiB), (12, 4, 1031, 12 * 87392), (4, 4, 4096, MiB),
+                                         (4, 4, 1024, MiB), (4, 4, 3, MiB)])
+def test_server_default_geometries(oracle, k, m, nb, blen):
     """The server's default erasure geometries (getDefaultParityBlocks,
     cmd/format-erasure.go:870-881): RS(12+4) for 16-drive sets (1 MiB blocks: S = 87 382,
     rows 2-byte aligned, 8 bytes of Split padding, 22-byte HighwayHash remainder) and
-    RS(4+4) for 8-drive sets, through the default dispatch; every block vs cpu_ref."""
+    RS(4+4) for 8-drive sets, through the default dispatch; every block vs cpu_ref.  Blocks
+    of 12 x 87 392 bytes give RS(12+4) 16-byte-aligned rows (the aligned-row dispatch)."""
     R = k + m
-    S = -(-MiB // k)
-    codec = z.Codec(k, m, MiB)
+    S = -(-blen // k)
+    codec = z.Codec(k, m, blen)
     d = torch.zeros(nb * R * S, dtype=torch.uint8, device=DEV)
-    z.fill_batch(d, R * S, MiB, nb, seed=77, obj0=0)
-    if k * S > MiB:  # bytes past the object: Split must read them as zero
-        d.view(nb, R * S)[:, MiB:k * S] = 0xEE
+    z.fill_batch(d, R * S, blen, nb, seed=77, obj0=0)
+    if k * S > blen:  # bytes past the object: Split must read them as zero
+        d.view(nb, R * S)[:, blen:k * S] = 0xEE
     sums = torch.zeros(nb * R * 32, dtype=torch.uint8, device=DEV)
-    codec.encode_batch(d, R * S, MiB, nb, parity=d, parity_offset=k * S, parity_stride=R * S, sums=sums)
+    codec.encode_batch(d, R * S, blen, nb, parity=d, parity_offset=k * S, parity_stride=R * S, sums=sums)
     torch.cuda.synchronize()
     if nb >= 1024:
         assert z.last_path() == 2, "warp-specialised kernel"
@@ -271,10 +274,10 @@ def test_server_default_geometries(oracle, k, m, nb):
         par = np.empty(n * m * S, np.uint8)
         sref = np.empty(n * R * 32, np.uint8)
         blk = np.ascontiguousarray(host[b0:b0 + n])
-        cpuref.encode_hash(k, m, mat, blk, MiB, n, R * S, par, m * S, sref, KEY, cpuref.threads_available())
+        cpuref.encode_hash(k, m, mat, blk, blen, n, R * S, par, m * S, sref, KEY, cpuref.threads_available())
         assert np.array_equal(blk[:, k * S:], par.reshape(n, m * S)), f"parity, blocks {b0}.."
         assert np.array_equal(hs[b0 * R * 32:(b0 + n) * R * 32], sref), f"sums, blocks {b0}.."
-    want = oracle.encode_data(k, m, oracle.fill(77, nb - 1, MiB), mat)
+    want = oracle.encode_data(k, m, oracle.fill(77, nb - 1, blen), mat)
     assert np.array_equal(host[nb - 1, k * S:].reshape(m, S), want[k:])
 
 

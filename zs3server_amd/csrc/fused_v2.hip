@@ -76,11 +76,15 @@ static int launch_ehx_default(const EncArgs& a, hipStream_t s) {
         return launch_ws_t<K, M, 4, 512, 1, true, true, 0, false, 0, 0, false, 3>(a, s) ? PATH_WS : PATH_NONE;
     } else if constexpr (K == 12 && M == 4) {
         // RS(12+4), the 16-drive default (cmd/format-erasure.go:870-881), at shard sizes
-        // that are multiples of 16; 1 MiB blocks (S = 87 382) take launch_ehx_ua.  Same
-        // shapes as RS(16+4): 8 stripes of 8-byte buffer-addressed columns, data rows
-        // written to LDS before the encode; 4 stripes with quad-form hash waves up to 1024.
+        // that are multiples of 16; 1 MiB blocks (S = 87 382) take launch_ehx_ua.  Above
+        // 1024 stripes the unaligned-row product shape (8 stripes of 8-byte columns of
+        // 512-byte tiles, L2 prefetch two tiles ahead) with the conflict-free LDS stride
+        // (diagnostics 330): 4 096 x (12 x 87 392 bytes) 1.42-1.51 -> 1.23 ms over the
+        // RS(16+4) shape it had (profiles/r04/abl_rs124_al.jsonl); 4 stripes with
+        // quad-form hash waves up to 1024.
         if (n > 4 * 256)
-            return launch_ws_t<K, M, 8, 384, 1, true, false, 0, false, 0, 0, false, 3, false, 2>(a, s) ? PATH_WS : PATH_NONE;
+            return launch_ws_t<K, M, 8, 512, 1, true, false, 0, false, 0, 8, false, 3, false, 2, 2, true, 3, 1>(a, s)
+                       ? PATH_WS : PATH_NONE;
         return launch_ws_t<K, M, 4, 512, 1, true, true, 0, false, 0, 0, false, 3>(a, s) ? PATH_WS : PATH_NONE;
     } else if constexpr (K == 4 && M == 4) {
         // RS(4+4), the 8-drive default: the RS(8+4) shape (16 stripes, 16-byte columns,

@@ -24,6 +24,9 @@
 //  all: unaligned rows share each tile's edge lines with the neighbouring tiles
 //  335: 4 stripes of 1 KiB tiles; 337: 16-byte columns (4 encode waves) with the
 //  256-VGPR budget, L2 prefetch, conflict-free LDS stride
+//  334 / 336 / 338 (timing ablations of the product instance, output differs): no
+//  HighwayHash arithmetic or LDS reads in the hash waves / no GF arithmetic in the encode
+//  waves / neither (the memory pattern alone, L2 prefetch kept)
 #include "fused_v2.hpp"
 
 namespace zs3k {
@@ -51,6 +54,9 @@ bool launch_ehx_km_12_4(int v, const EncArgs& a, hipStream_t s) {
         case 333: return launch_ws_t<12, 4, 8, 512, 1, true, false, 0, false, 0, 8, false, 0, false, 2, 2, true>(a, s);
         case 335: return launch_ws_t<12, 4, 4, 1024, 1, true, false, 0, false, 0, 8, false, 3, false, 2, 2, true, 3, 1>(a, s);
         case 337: return launch_ws_t<12, 4, 8, 512, 1, true, false, 0, false, 0, 16, false, 3, false, 2, 2, true, 2, 1>(a, s);
+        case 334: return launch_ws_t<12, 4, 8, 512, 1, true, false, 0, false, 0, 8, false, 3, false, 2, 2, true, 3, 0, 3>(a, s);
+        case 336: return launch_ws_t<12, 4, 8, 512, 1, true, false, 0, false, 0, 8, false, 3, false, 9, 2, true>(a, s);
+        case 338: return launch_ws_t<12, 4, 8, 512, 1, true, false, 0, false, 0, 8, false, 3, false, 9, 2, true, 3, 0, 7>(a, s);
         default: return false;
     }
 }

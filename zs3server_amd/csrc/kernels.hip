@@ -1568,6 +1568,10 @@ static hipError_t run_encode_fast(const EncArgs& a, hipStream_t s, int* path) {
         if constexpr ((K == 8 && M == 4) || (K == 4 && M == 2) || (K == 16 && M == 4)) {
             if (fv > 0 && p == PATH_NONE) p = launch_variant<K, M>(fv, a, s);
         }
+        if constexpr (K == 12 && M == 4) {
+            // the RS(12+4) unaligned-row shapes at aligned rows (memory-pattern A/B)
+            if (fv >= 330 && p == PATH_NONE) p = launch_ehx(fv, a, s);
+        }
 #endif
         // Dyadic shapes (RS(4+2), RS(8+4), RS(16+4), ...): the second-generation
         // kernels of fused_v2.hip pick their launch shape from (k, m, n_blocks).

@@ -114,9 +114,14 @@ int launch_ehx_ua(const EncArgs& a, hipStream_t s) {
         // LDS before the encode, and the hash waves touching every line of the data rows
         // two tiles ahead (PFD = 2) so the unaligned row loads of the encode waves hit L2:
         // 4096 / 16384 x 1 MiB 1.72-1.79 / 6.72 -> 1.41 / 5.48 ms
-        // (profiles/r03/ab_rs124_pfd.jsonl; 196 = no prefetch 1.54-1.59 / 5.98-6.01)
+        // (profiles/r03/ab_rs124_pfd.jsonl; 196 = no prefetch 1.54-1.59 / 5.98-6.01).
+        // Round 4 (diagnostics 391): 4 stripes of 1 KiB tiles, whose memory pattern alone
+        // is 7 % faster (386 vs 338, profiles/r04/mem_rs124.jsonl), with 4 quad-form hash
+        // waves doing the L2 prefetch and 4 encode waves of 16-byte columns (256-VGPR
+        // budget): 1.41 -> 1.40 ms / 5.59 -> 5.56 ms at 4096 / 16384 x 1 MiB on the same
+        // box, 1-2 % over two boxes (sweep_rs124_1k.jsonl, sweep_rs124_1k_b.jsonl)
         if (a.n_blocks > 4 * 256)
-            return launch_ws_t<12, 4, 8, 512, 1, true, false, 0, false, 0, 8, false, 3, false, 2, 2, true>(a, s)
+            return launch_ws_t<12, 4, 4, 1024, 1, true, true, 0, false, 0, 16, false, 3, false, 2, 2, true, 2, 1>(a, s)
                        ? PATH_WS : PATH_NONE;
         return launch_ws_t<12, 4, 4, 512, 1, true, true, 0, false, 0, 0, false, 3, false, 0, 0, true>(a, s)
                    ? PATH_WS : PATH_NONE;

@@ -578,9 +578,30 @@ k_ehx_ws(EncArgs a) {
         const int row_off = crow * TS + 8 * lane;
         const uint32_t sel = zipper_sel(lane);
         HHLane st = hh_init(lane, a.key[0], a.key[1], a.key[2], a.key[3]);
+        // PFD: the same L2 prefetch of the data rows as the pair-form role below
+        constexpr int LPR = T / 128, NLN = G * K * LPR, NPL = PFD ? (NLN + NH - 1) / NH : 1;
+        const uint8_t* pfa[NPL];
+        uint32_t sink = 0;
+        if constexpr (PFD > 0) {
+            static_assert(T % 128 == 0, "prefetch whole 128-byte lines");
+#pragma unroll
+            for (int q = 0; q < NPL; ++q) {
+                const int li = tid + q * NH < NLN ? tid + q * NH : NLN - 1;
+                const int r = li / LPR, g = r / K, j = r % K;
+                const int64_t b = (blk0 + g) < a.n_blocks ? (blk0 + g) : (a.n_blocks - 1);
+                pfa[q] = a.data + b * a.data_stride + (int64_t)j * S + (li % LPR) * 128;
+            }
+        }
         bar();  // tables (matches the encode role)
         bar();  // step 0: tile 0 being encoded
         for (int64_t s = 1; s <= nfull; ++s) {
+            if constexpr (PFD > 0) {
+                if (s + PFD < nfull) {
+#pragma unroll
+                    for (int q = 0; q < NPL; ++q)
+                        asm volatile("global_load_dword %0, %1, off" : "+v"(sink) : "v"(pfa[q] + (s + PFD) * T));
+                }
+            }
             const uint64_t* p = reinterpret_cast<const uint64_t*>(tile[(s - 1) & 1] + row_off);
             uint64_t w[NPK];
 #pragma unroll
@@ -589,6 +610,7 @@ k_ehx_ws(EncArgs a) {
             for (int i = 0; i < NPK; ++i) hh_update(st, w[i], sel);
             bar();
         }
+        if constexpr (PFD > 0) asm volatile("s_waitcnt vmcnt(0)" : "+v"(sink)::"memory");
         if (tail) {
             const uint8_t* row = tile[nfull & 1] + crow * TS;
             hh_packets(st, row, tail >> 5, lane, sel);

@@ -27,6 +27,16 @@
 //  334 / 336 / 338 (timing ablations of the product instance, output differs): no
 //  HighwayHash arithmetic or LDS reads in the hash waves / no GF arithmetic in the encode
 //  waves / neither (the memory pattern alone, L2 prefetch kept)
+//  380-387: the memory pattern alone (ABL 7, no GF) of other shapes: 380 no L2 prefetch,
+//  381 16 stripes of 256-byte tiles, 382 4 stripes of 1 KiB tiles, 383 16-byte columns
+//  (256-VGPR budget), 384 temporal data loads, 385 L2 prefetch 4 tiles ahead, 386 4 stripes
+//  of 1 KiB tiles with 16-byte columns, 387 8 stripes of 256-byte tiles (two workgroups
+//  per CU, 128-VGPR budget)
+//  390-392: 4 stripes of 1 KiB tiles (the best memory pattern above, 386) with the L2
+//  prefetch two tiles ahead: 390 pair-form hash waves, 16-byte columns (256-VGPR budget);
+//  391 quad-form hash waves (4 instead of 2), 16-byte columns; 392 quad-form, 8-byte columns;
+//  391 with two tiles of register prefetch (393), without the early data write (394), with
+//  the L2 prefetch three tiles ahead (395)
 #include "fused_v2.hpp"
 
 namespace zs3k {
@@ -56,6 +66,20 @@ bool launch_ehx_km_12_4(int v, const EncArgs& a, hipStream_t s) {
         case 337: return launch_ws_t<12, 4, 8, 512, 1, true, false, 0, false, 0, 16, false, 3, false, 2, 2, true, 2, 1>(a, s);
         case 334: return launch_ws_t<12, 4, 8, 512, 1, true, false, 0, false, 0, 8, false, 3, false, 2, 2, true, 3, 0, 3>(a, s);
         case 336: return launch_ws_t<12, 4, 8, 512, 1, true, false, 0, false, 0, 8, false, 3, false, 9, 2, true>(a, s);
+        case 380: return launch_ws_t<12, 4, 8, 512, 1, true, false, 0, false, 0, 8, false, 3, false, 9, 0, true, 3, 0, 7>(a, s);
+        case 381: return launch_ws_t<12, 4, 16, 256, 1, true, false, 0, false, 0, 8, false, 3, false, 9, 2, true, 3, 1, 7>(a, s);
+        case 382: return launch_ws_t<12, 4, 4, 1024, 1, true, false, 0, false, 0, 8, false, 3, false, 9, 2, true, 3, 1, 7>(a, s);
+        case 383: return launch_ws_t<12, 4, 8, 512, 1, true, false, 0, false, 0, 16, false, 3, false, 9, 2, true, 2, 1, 7>(a, s);
+        case 384: return launch_ws_t<12, 4, 8, 512, 1, true, false, 0, false, 0, 8, false, 2, false, 9, 2, true, 3, 0, 7>(a, s);
+        case 385: return launch_ws_t<12, 4, 8, 512, 1, true, false, 0, false, 0, 8, false, 3, false, 9, 4, true, 3, 0, 7>(a, s);
+        case 386: return launch_ws_t<12, 4, 4, 1024, 1, true, false, 0, false, 0, 16, false, 3, false, 9, 2, true, 3, 1, 7>(a, s);
+        case 387: return launch_ws_t<12, 4, 8, 256, 1, true, false, 0, false, 0, 8, false, 3, false, 9, 2, true, 4, 1, 7>(a, s);
+        case 390: return launch_ws_t<12, 4, 4, 1024, 1, true, false, 0, false, 0, 16, false, 3, false, 2, 2, true, 2, 1>(a, s);
+        case 391: return launch_ws_t<12, 4, 4, 1024, 1, true, true, 0, false, 0, 16, false, 3, false, 2, 2, true, 2, 1>(a, s);
+        case 392: return launch_ws_t<12, 4, 4, 1024, 1, true, true, 0, false, 0, 8, false, 3, false, 2, 2, true, 3, 1>(a, s);
+        case 393: return launch_ws_t<12, 4, 4, 1024, 2, true, true, 0, false, 0, 16, false, 3, false, 2, 2, true, 2, 1>(a, s);
+        case 394: return launch_ws_t<12, 4, 4, 1024, 1, true, true, 0, false, 0, 16, false, 3, false, 0, 2, true, 2, 1>(a, s);
+        case 395: return launch_ws_t<12, 4, 4, 1024, 1, true, true, 0, false, 0, 16, false, 3, false, 2, 3, true, 2, 1>(a, s);
         case 338: return launch_ws_t<12, 4, 8, 512, 1, true, false, 0, false, 0, 8, false, 3, false, 9, 2, true, 3, 0, 7>(a, s);
         default: return false;
     }

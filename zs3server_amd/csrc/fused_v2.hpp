@@ -1102,8 +1102,11 @@ constexpr int vr_nh() {
 // workgroup's span) and a wave-uniform SGPR offset per row — instead of one 64-bit VGPR
 // address per survivor row, which the RS(16+4) 3-4-row instances kept as 16 loop
 // invariants and spilled (scratch reloads in the steady loop).
+// PFD (round 4): as in k_ehx_ws, the hash waves touch every 128-byte line of the survivor
+// rows of tile s+PFD while hashing tile s-1 (one untracked global_load_dword per line,
+// result discarded), so the rebuild waves' survivor loads hit L2.
 template <int K, int EX, bool HOUT, int G, int T, int PF, int CW = 16, bool HQ = false, bool ST = false,
-          int BT = 0, bool NTL = false, bool UA = false, bool BUF = false>
+          int BT = 0, bool NTL = false, bool UA = false, bool BUF = false, int PFD = 0>
 __global__ void __launch_bounds__((vr_nh<G, K + (HOUT ? EX : 0), HQ>() + G * (T / CW))) __attribute__((amdgpu_waves_per_eu(2)))
 k_vr_ws(VrArgs a) {
     constexpr int RH = K + (HOUT ? EX : 0);
@@ -1132,6 +1135,36 @@ k_vr_ws(VrArgs a) {
     int64_t iend = PF;
     if (nfull >= 3 * PF) iend = PF + ((nfull - 3 * PF) / PF + 1) * PF;
     const int64_t total = iend + 2 * PF + 1;
+    // PFD: this hash thread's prefetch lines (line li = tid + q*NH of the tile's survivor
+    // rows); set up after the first barrier (srows)
+    constexpr int LPR = T / 128, NLN = G * K * LPR, NPL = PFD ? (NLN + NH - 1) / NH : 1;
+    static_assert(PFD == 0 || T % 128 == 0, "prefetch whole 128-byte lines");
+    const uint8_t* pfa[NPL];
+    uint32_t sink = 0;
+    auto pf_setup = [&]() {
+        if constexpr (PFD > 0) {
+#pragma unroll
+            for (int q = 0; q < NPL; ++q) {
+                const int li = tid + q * NH < NLN ? tid + q * NH : NLN - 1;
+                const int r = li / LPR, gg = r / K, j = r % K;
+                const int64_t bl = (blk0 + gg) < a.n_blocks ? (blk0 + gg) : (a.n_blocks - 1);
+                const int64_t bb = a.ids ? (int64_t)a.ids[bl] : bl;
+                pfa[q] = a.shards + bb * a.block_stride + (int64_t)srows[j] * S + (li % LPR) * 128;
+            }
+        }
+    };
+    auto pf_issue = [&](int64_t s) {
+        if constexpr (PFD > 0) {
+            if (s + PFD < nfull) {
+#pragma unroll
+                for (int q = 0; q < NPL; ++q)
+                    asm volatile("global_load_dword %0, %1, off" : "+v"(sink) : "v"(pfa[q] + (s + PFD) * T));
+            }
+        }
+    };
+    auto pf_drain = [&]() {
+        if constexpr (PFD > 0) asm volatile("s_waitcnt vmcnt(0)" : "+v"(sink)::"memory");
+    };
 
     if (HQ && __builtin_amdgcn_readfirstlane(tid) < NH) {
         // ---- hash role (quad form): lane `lane` of hashed row cj of stripe g
@@ -1142,8 +1175,10 @@ k_vr_ws(VrArgs a) {
         const uint32_t sel = zipper_sel(lane);
         HHLane st = hh_init(lane, a.key[0], a.key[1], a.key[2], a.key[3]);
         lds_barrier2();  // tables / rows (matches the rebuild role)
+        pf_setup();
         lds_barrier2();  // step 0
         for (int64_t s = 1; s <= nfull; ++s) {
+            pf_issue(s);
             const uint64_t* p = reinterpret_cast<const uint64_t*>(tile[(s - 1) & 1] + row_off);
             uint64_t w[NPK];
 #pragma unroll
@@ -1152,6 +1187,7 @@ k_vr_ws(VrArgs a) {
             for (int i = 0; i < NPK; ++i) hh_update(st, w[i], sel);
             lds_barrier2();
         }
+        pf_drain();
         if (tail) {
             const uint8_t* row = tile[nfull & 1] + crow * TS;
             hh_packets(st, row, tail >> 5, lane, sel);
@@ -1187,8 +1223,10 @@ k_vr_ws(VrArgs a) {
         const int row_off = chain * TS;
         HHPair st = hh2_init(hh, a.key[0], a.key[1], a.key[2], a.key[3]);
         lds_barrier2();  // tables / rows (matches the rebuild role)
+        pf_setup();
         lds_barrier2();  // step 0
         for (int64_t s = 1; s <= nfull; ++s) {
+            pf_issue(s);
             const uint4* p = reinterpret_cast<const uint4*>(tile[(s - 1) & 1] + row_off) + hh;
             uint4 w[NPK];
 #pragma unroll
@@ -1198,6 +1236,7 @@ k_vr_ws(VrArgs a) {
                 hh2_update(st, ((uint64_t)w[i].y << 32) | w[i].x, ((uint64_t)w[i].w << 32) | w[i].z);
             lds_barrier2();
         }
+        pf_drain();
         if (tail) {
             const uint8_t* row = tile[nfull & 1] + row_off;
             hh2_packets(st, row, tail >> 5, hh);
@@ -1452,11 +1491,11 @@ k_vr_ws(VrArgs a) {
 }
 
 template <int K, int EX, bool HOUT, int G, int T, int PF, int CW, bool HQ, bool ST, int BT, bool NTL = false,
-          bool UA = false, bool BUF = false>
+          bool UA = false, bool BUF = false, int PFD = 0>
 static bool launch_vr_ws_bt(const VrArgs& a, hipStream_t s);
 
 template <int K, int EX, bool HOUT, int G, int T, int PF, int CW = 16, bool HQ = false, bool ST = false,
-          int BT = 0, bool UA = false, bool BUF = false>
+          int BT = 0, bool UA = false, bool BUF = false, int PFD = 0>
 static bool launch_vr_ws_t(const VrArgs& a, hipStream_t s) {
     if constexpr (BUF && !UA) {
         // buffer addressing needs the G stripes of a workgroup in order (no id list) and
@@ -1464,15 +1503,15 @@ static bool launch_vr_ws_t(const VrArgs& a, hipStream_t s) {
         // 247: always that one)
         if (!a.ids && (int64_t)G * a.block_stride < ((int64_t)1 << 31) && a.block_stride > 0 &&
             !(ZS3_DIAG && a.variant == 247))
-            return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, BT, true, false, true>(a, s);
-        return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, BT, true>(a, s);
+            return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, BT, true, false, true, PFD>(a, s);
+        return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, BT, true, false, false, PFD>(a, s);
     }
     if constexpr (UA) {
         // plain (temporal) survivor loads: with unaligned rows each tile's first and last
         // 128-byte lines are shared with the neighbouring tiles, and non-temporal loads
         // fetched them twice (RS(12+4) rebuild 2: HBM traffic 1.205 x algorithmic,
         // profiles/r03/final_session3/bench_paths_roofline.jsonl)
-        return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, BT, false, true>(a, s);
+        return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, BT, false, true, false, PFD>(a, s);
     } else {
         // diagnostics 240: the same launch with the scalar-table batching flipped (off <-> 4
         // coefficients per batch); 241: batches of 2
@@ -1486,11 +1525,12 @@ static bool launch_vr_ws_t(const VrArgs& a, hipStream_t s) {
         if constexpr (ZS3_DIAG) {
             if (a.variant == 246) return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, BT, false>(a, s);
         }
-        return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, BT, true>(a, s);
+        return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, BT, true, false, false, PFD>(a, s);
     }
 }
 
-template <int K, int EX, bool HOUT, int G, int T, int PF, int CW, bool HQ, bool ST, int BT, bool NTL, bool UA, bool BUF>
+template <int K, int EX, bool HOUT, int G, int T, int PF, int CW, bool HQ, bool ST, int BT, bool NTL, bool UA, bool BUF,
+          int PFD>
 static bool launch_vr_ws_bt(const VrArgs& a, hipStream_t s) {
     constexpr int RH = K + (HOUT ? EX : 0);
     constexpr int NT = vr_nh<G, RH, HQ>() + G * (T / CW);
@@ -1503,7 +1543,7 @@ static bool launch_vr_ws_bt(const VrArgs& a, hipStream_t s) {
         if (a.e != EX || (!UA && (a.S % 16) != 0) || a.k != K || (HOUT != (a.sums_out != nullptr) && EX > 0))
             return false;
         if ((int64_t)(a.k + a.m) * a.S >= ((int64_t)1 << 31)) return false;  // 32-bit row offsets
-        auto kern = k_vr_ws<K, EX, HOUT, G, T, PF, CW, HQ, ST, BT, NTL, UA, BUF>;
+        auto kern = k_vr_ws<K, EX, HOUT, G, T, PF, CW, HQ, ST, BT, NTL, UA, BUF, PFD>;
         if (ensure_dyn_lds((const void*)kern, dyn) != hipSuccess) return false;
         const int64_t grid = (a.n_blocks + G - 1) / G;
         hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), dyn, s, a);

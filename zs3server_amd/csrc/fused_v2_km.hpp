@@ -148,6 +148,17 @@ static bool launch_ehx_km(int v, const EncArgs& a, hipStream_t s) {
         case 327: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, true, false, 0, false, 1, 0, false, 3, false, 9, 0, false, 3, 1, 3>(a, s); else return false;
         case 328: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 1, true, false, 0, false, 1, 0, false, 3, false, 9, 0, false, 3, 1, 7>(a, s); else return false;
         case 329: if constexpr (deep) return launch_ws_t<K, M, 16, 384, 2, true, false, 0, false, 1, 0, false, 3, false, 9, 0, false, 3, 1, 7>(a, s); else return false;
+        // 1 KiB tiles (the RS(12+4) memory-pattern finding, profiles/r04/mem_rs124.jsonl):
+        // 360 / 361 / 362 the memory pattern alone of 4 stripes of 1 KiB tiles with / without
+        // the L2 prefetch, 2 stripes of 2 KiB tiles; 363 / 364 the real roles on 4 stripes of
+        // 1 KiB tiles with quad-form hash waves issuing the L2 prefetch, 16-byte columns, with /
+        // without encode priority; 365 = 363 with 8 stripes of 512-byte tiles
+        case 360: if constexpr (deep) return launch_ws_t<K, M, 4, 1024, 1, true, false, 0, false, 1, 16, false, 3, false, 9, 2, false, 3, 1, 7>(a, s); else return false;
+        case 361: if constexpr (deep) return launch_ws_t<K, M, 4, 1024, 1, true, false, 0, false, 1, 16, false, 3, false, 9, 0, false, 3, 1, 7>(a, s); else return false;
+        case 362: if constexpr (deep) return launch_ws_t<K, M, 2, 2048, 1, true, false, 0, false, 1, 16, false, 3, false, 9, 2, false, 3, 1, 7>(a, s); else return false;
+        case 363: if constexpr (deep) return launch_ws_t<K, M, 4, 1024, 1, true, true, 0, false, 1, 16, false, 3, false, 0, 2, false, 2, 1>(a, s); else return false;
+        case 364: if constexpr (deep) return launch_ws_t<K, M, 4, 1024, 1, true, true, 0, false, 0, 16, false, 3, false, 0, 2, false, 2, 1>(a, s); else return false;
+        case 365: if constexpr (deep) return launch_ws_t<K, M, 8, 512, 1, true, true, 0, false, 1, 16, false, 3, false, 0, 2, false, 2, 1>(a, s); else return false;
         default: return false;
     }
 }

@@ -28,15 +28,19 @@ namespace zs3k {
 // barriers; the rows are long: RS(3+3) S = 341 KiB): RS(3+2) 1.91 -> 1.75 ms, RS(3+3)
 // 2.79 -> 2.23, RS(2+2) 2.01 -> 1.90 (geom_r9.jsonl); RS(5+4) / RS(6+4) gain 2 % from temporal data loads without the L2
 // prefetch (2.09 -> 2.04, 1.93 -> 1.89); RS(10+4) keeps the first shape (1 KiB tiles:
-// 1.70 -> 2.90 ms at 8-byte columns).
+// 1.70 -> 2.90 ms at 8-byte columns).  Later in round 4 RS(5+4) / RS(6+4) moved to the
+// RS(12+4) product shape (4 stripes of 1 KiB tiles, quad-form hash waves issuing the L2
+// prefetch, 16-byte columns on the 256-VGPR budget; diagnostics 345): 2.04-2.05 -> 1.95-1.97
+// and 1.89-1.90 -> 1.88-1.89 ms (sweep_gen_1k.jsonl, one box, three runs); K >= 7 spills
+// there (RS(10+4): 231 VGPRs).
 template <int K, int M>
 static bool launch_gen_t(const EncArgs& a, hipStream_t s) {
     if constexpr (K <= 3)
         return launch_ws_t<K, M, 8, 1024, 1, true, false, 0, false, 0, 16, false, 3, false, 0, 2, true, 3, 1, 0, true>(a, s);
     else if constexpr (K + M <= 8)  // RS(4+3): 1 KiB tiles measured 1.54 -> 1.64 ms (geom_r9.jsonl)
         return launch_ws_t<K, M, 16, 512, 1, true, false, 0, false, 0, 16, false, 3, false, 0, 2, true, 3, 1, 0, true>(a, s);
-    else if constexpr (K <= 6)
-        return launch_ws_t<K, M, 8, 512, 1, true, false, 0, false, 0, 8, false, 2, false, 0, 0, true, 3, 1, 0, true>(a, s);
+    else if constexpr (K <= 6)  // RS(5+4) / (6+4): diagnostics 345 (profiles/r04/sweep_gen_1k.jsonl)
+        return launch_ws_t<K, M, 4, 1024, 1, true, true, 0, false, 0, 16, false, 3, false, 0, 2, true, 2, 1, 0, true>(a, s);
     else
         return launch_ws_t<K, M, 8, 512, 1, true, false, 0, false, 0, 8, false, 3, false, 0, 2, true, 3, 1, 0, true>(a, s);
 }
@@ -57,6 +61,8 @@ bool has_gen_encode(int k, int m) {
 //  342: quad-form hash waves (one HH lane per thread)
 //  343: temporal data loads (nt stores only), no L2 prefetch
 //  344: 8 stripes, 1 KiB tiles (fewer barriers per hashed byte)
+//  345 / 346: 4 stripes of 1 KiB tiles, quad-form hash waves issuing the L2 prefetch 2
+//  tiles ahead (the RS(12+4) product shape), 16-byte columns (256-VGPR budget) / 8-byte
 template <int K, int M>
 static bool launch_gen_diag(int v, const EncArgs& a, hipStream_t s) {
     constexpr int G = K + M <= 8 ? 16 : 8;
@@ -67,6 +73,8 @@ static bool launch_gen_diag(int v, const EncArgs& a, hipStream_t s) {
         case 342: return launch_ws_t<K, M, G, 512, 1, true, true, 0, false, 0, CW, false, 3, false, 0, 0, true, 3, 1, 0, true>(a, s);
         case 343: return launch_ws_t<K, M, G, 512, 1, true, false, 0, false, 0, CW, false, 2, false, 0, 0, true, 3, 1, 0, true>(a, s);
         case 344: return launch_ws_t<K, M, 8, 1024, 1, true, false, 0, false, 0, CW, false, 3, false, 0, 2, true, 3, 1, 0, true>(a, s);
+        case 345: return launch_ws_t<K, M, 4, 1024, 1, true, true, 0, false, 0, 16, false, 3, false, 0, 2, true, 2, 1, 0, true>(a, s);
+        case 346: return launch_ws_t<K, M, 4, 1024, 1, true, true, 0, false, 0, 8, false, 3, false, 0, 2, true, 3, 1, 0, true>(a, s);
         default: return false;
     }
 }
@@ -75,7 +83,7 @@ static bool launch_gen_diag(int v, const EncArgs& a, hipStream_t s) {
 int launch_ehx_gen(const EncArgs& a, hipStream_t s) {
     if (!a.sums) return PATH_NONE;
 #if ZS3_DIAG
-    if (a.variant >= 340 && a.variant <= 344) {
+    if (a.variant >= 340 && a.variant <= 346) {
         bool ok = false;
         if (a.k == 3 && a.m == 3) ok = launch_gen_diag<3, 3>(a.variant, a, s);
         if (a.k == 3 && a.m == 2) ok = launch_gen_diag<3, 2>(a.variant, a, s);

@@ -1631,7 +1631,7 @@ hipError_t launch_encode(const EncArgs& a, hipStream_t s, int* path) {
     // RS(2+2) / RS(4+3)) on the warp-specialised kernel with a general matrix
     // (fused_v2_gen.hip) once the batch fills the chip (a workgroup takes 8-16 stripes);
     // smaller batches keep the latency-bound paths below.
-    if (a.sums && (a.variant == 0 || (ZS3_DIAG && a.variant >= 340 && a.variant <= 344)) && a.n_blocks >= 1024 &&
+    if (a.sums && (a.variant == 0 || (ZS3_DIAG && a.variant >= 340 && a.variant <= 346)) && a.n_blocks >= 1024 &&
         has_gen_encode(a.k, a.m)) {
         const int p = launch_ehx_gen(a, s);
         if (p != PATH_NONE) {

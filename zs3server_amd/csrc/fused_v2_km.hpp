@@ -159,6 +159,12 @@ static bool launch_ehx_km(int v, const EncArgs& a, hipStream_t s) {
         case 363: if constexpr (deep) return launch_ws_t<K, M, 4, 1024, 1, true, true, 0, false, 1, 16, false, 3, false, 0, 2, false, 2, 1>(a, s); else return false;
         case 364: if constexpr (deep) return launch_ws_t<K, M, 4, 1024, 1, true, true, 0, false, 0, 16, false, 3, false, 0, 2, false, 2, 1>(a, s); else return false;
         case 365: if constexpr (deep) return launch_ws_t<K, M, 8, 512, 1, true, true, 0, false, 1, 16, false, 3, false, 0, 2, false, 2, 1>(a, s); else return false;
+        // RS(16+4) encode + sums with the RS(12+4) round-4 recipe: 4 stripes of 768-byte
+        // tiles (1 KiB does not fit the LDS), quad-form hash waves issuing the L2 prefetch,
+        // 16-byte (366) / 8-byte (367) columns; 368 the product + L2 prefetch + TSP 1
+        case 366: if constexpr (K == 16 && M == 4) return launch_ws_t<K, M, 4, 768, 1, true, true, 0, false, 0, 16, false, 3, false, 2, 2, false, 2, 1>(a, s); else return false;
+        case 367: if constexpr (K == 16 && M == 4) return launch_ws_t<K, M, 4, 768, 1, true, true, 0, false, 0, 8, false, 3, false, 2, 2, false, 3, 1>(a, s); else return false;
+        case 368: if constexpr (K == 16 && M == 4) return launch_ws_t<K, M, 8, 384, 1, true, false, 0, false, 0, 0, false, 3, false, 2, 2, false, 3, 1>(a, s); else return false;
         default: return false;
     }
 }

@@ -229,9 +229,9 @@ def test_queue_zero_copy_pinned_callers(oracle, k, m, bs, zc_mode, monkeypatch):
     padding (k*S > blockSize): a zero-copy block DMAs only its `len` data bytes, so the
     slot's padding bytes hold whatever the slot's previous batch left there, and every
     encode kernel must read them as zero.  Pinned-caller modes (queue.hip,
-    ZS3_QUEUE_ZC): 1 = zero-copy for the first block of a batch, the rest staged (the
-    default); 2 = every full block by a DMA of its own; 3 = copy-list kernels over the
-    mapped pinned pages."""
+    ZS3_QUEUE_ZC): 1 = zero-copy for a lone caller's block (first of its batch, no other
+    batch of the lane in flight), the rest staged (the default); 2 = every full block by a
+    DMA of its own; 3 = copy-list kernels over the mapped pinned pages."""
     monkeypatch.setenv("ZS3_QUEUE_ZC", str(zc_mode))
     codec = z.Codec(k, m, bs)
     q = z.Queue(codec, max_batch=16, max_wait_us=500)
@@ -283,7 +283,7 @@ def test_queue_zero_copy_pinned_callers(oracle, k, m, bs, zc_mode, monkeypatch):
     assert blocks == nthr * per * 2
     zc = q.zero_copy_blocks()
     # pinned threads: every full encode block and every decode block (modes 2, 3); mode 1
-    # only those that opened their batch
+    # only those that opened their batch with no other batch of the lane in flight
     n_short = sum(1 for t in range(0, nthr, 2) if t % 4 == 0)
     if zc_mode == 1:
         assert 0 <= zc <= (nthr // 2) * per * 2 - n_short, zc
@@ -292,3 +292,44 @@ def test_queue_zero_copy_pinned_callers(oracle, k, m, bs, zc_mode, monkeypatch):
     q.close()
     for p in pins + pins_dec:
         p.free()
+
+
+@pytest.mark.parametrize("k,m", [(12, 4), (8, 4)])
+def test_queue_lone_pinned_caller_zero_copy(oracle, k, m):
+    """Default pinned-caller mode (ZS3_QUEUE_ZC=1): a lone synchronous caller (each block
+    submitted and waited for before the next) takes the zero-copy path for every full
+    block, encode and decode (queue.hip zc_mode); results vs the oracle.  RS(12+4) on
+    1 MiB blocks has Split padding, which the zero-copy DMA does not write."""
+    bs = 1 << 20
+    codec = z.Codec(k, m, bs)
+    q = z.Queue(codec, max_batch=16, max_wait_us=500)
+    R = k + m
+    S = -(-bs // k)
+    mat = oracle.build_matrix(k, m)
+    pin = z.HostBuffer(R * S + 64)
+    try:
+        n = 3
+        for i in range(n):
+            data = oracle.fill(900 + k, i, bs)
+            buf = pin.array[:R * S + 64]
+            buf[:] = 0xEE
+            buf[:bs] = data
+            got_S, sums = q.encode_data(buf, bs)
+            want = oracle.encode_data(k, m, data, mat)
+            assert got_S == S
+            assert np.array_equal(buf[:R * S].reshape(R, S), want), i
+            assert np.array_equal(sums, oracle.hh256_rows(KEY, want)), i
+        sh, ssum = _stripe(oracle, k, m, bs, 950 + k, 0)
+        work = pin.array[:R * S].reshape(R, S)
+        work[:] = sh
+        present = np.ones(R, bool)
+        present[[1, k]] = False
+        work[~present] = 0x5A
+        bad = np.full(R, 9, np.int32)
+        assert q.decode(work, present, True, expect=ssum, bad=bad) == 0
+        assert not bad.any()
+        assert np.array_equal(work[1], sh[1])
+        assert q.zero_copy_blocks() == n + 1
+    finally:
+        q.close()
+        pin.free()

@@ -123,9 +123,11 @@ struct zs3_queue {
     // Pinned callers (round 4; ZS3_QUEUE_ZC=<mode> selects another for A/B measurements,
     // profiles/r04/queue_ab*.jsonl):
     //   0 staged like pageable callers (memcpy into the pinned slot, one DMA per batch);
-    //   1 (default) zero-copy only for the first block of a batch (a lone or leading
-    //     caller's block is DMA'd by its submitter while the slot is still empty), the
-    //     rest staged;
+    //   1 (default) zero-copy only for a lone caller: the first block of a batch while no
+    //     other batch of its lane is in flight is DMA'd by its submitter (the slot is still
+    //     empty), everything else staged — under concurrency the extra per-batch DMA call
+    //     cost more than the memcpy it saves (16 submitters 18-20 vs 20-22 GiB/s,
+    //     profiles/r04/queue_ab4.jsonl);
     //   2 every block zero-copy by a DMA of its own (round 3): the per-block DMA calls of
     //     many submitters serialise in the runtime (256 submitters 26.3 vs staged 32.8
     //     GiB/s);
@@ -717,6 +719,7 @@ int zs3_queue_submit_encode(zs3_queue* q, uint8_t* h_buf, int64_t len, int64_t c
     r->len = len;
     r->h_sums = h_sums;
     Slot* s;
+    bool lone = false;  // no other batch of the lane in flight (zc_mode 1)
     {
         std::unique_lock<std::mutex> lk(q->mu);
         const int rc = reserve(q, lk, r, len == q->B);
@@ -725,6 +728,7 @@ int zs3_queue_submit_encode(zs3_queue* q, uint8_t* h_buf, int64_t len, int64_t c
             return rc;
         }
         s = r->slot;
+        lone = q->inflight_blocks[ENC] == 0;
     }
     // Split (reedsolomon): data rows are the input bytes, zero-padded to k*S (the
     // kernel reads the pad of a full block as zero).  A full block in pinned memory is
@@ -732,7 +736,7 @@ int zs3_queue_submit_encode(zs3_queue* q, uint8_t* h_buf, int64_t len, int64_t c
     // Copy-list mode: the batch's launch moves it (run_copy_list).
     const size_t KS = (size_t)q->k * q->S;
     void* dmap = nullptr;
-    const bool zc_try = q->zc_mode == 2 || q->zc_mode == 3 || (q->zc_mode == 1 && r->pos == 0);
+    const bool zc_try = q->zc_mode == 2 || q->zc_mode == 3 || (q->zc_mode == 1 && r->pos == 0 && lone);
     if (len == q->B && zc_try && zs3i_pinned_map(h_buf, (size_t)q->R * q->S, &dmap)) {
         if (q->zc_mode == 3) {
             r->zc = true;
@@ -770,6 +774,7 @@ int zs3_queue_submit_decode(zs3_queue* q, uint8_t* h_shards, int64_t shard_len, 
     r->h_sums_out = h_sums_out;
     for (int i = 0; i < q->R; ++i) r->present[i] = h_present[i] ? 1 : 0;
     Slot* s;
+    bool lone = false;  // no other batch of the lane in flight (zc_mode 1)
     {
         std::unique_lock<std::mutex> lk(q->mu);
         const int rc = reserve(q, lk, r, shard_len == q->S);
@@ -778,11 +783,12 @@ int zs3_queue_submit_decode(zs3_queue* q, uint8_t* h_shards, int64_t shard_len, 
             return rc;
         }
         s = r->slot;
+        lone = q->inflight_blocks[r->lane] == 0;
     }
     // survivors: DMA'd straight from a pinned caller buffer (runs of present rows, same
     // row layout as the slot), else copied into the pinned slot
     void* dmap = nullptr;
-    const bool zc_try = q->zc_mode == 2 || (q->zc_mode == 1 && r->pos == 0);
+    const bool zc_try = q->zc_mode == 2 || (q->zc_mode == 1 && r->pos == 0 && lone);
     if (shard_len == q->S && q->zc_mode == 3 && zs3i_pinned_map(h_shards, (size_t)q->E, &dmap)) {
         r->zc = true;  // gathered by the batch's copy-list launch
         r->d_map = (uint8_t*)dmap;

@@ -283,10 +283,11 @@ void zs3_split_range(int64_t total, int world, int rank, int64_t* lo, int64_t* h
  * batches on pinned staging slots, each slot with its own stream:
  *   - a block is copied into the queue's pinned staging by its submitting thread, or,
  *     when the caller's buffer lies inside a zs3_host_alloc allocation (the pinned
- *     bpool), holds a full-size block and opens its batch, DMA'd from it directly
- *     (zero-copy: no host memcpy either way; parity / rebuilt rows are DMA'd straight
- *     back into it; later blocks of a batch are staged, which measured faster under
- *     concurrency);
+ *     bpool), holds a full-size block, opens its batch and no other batch of its lane
+ *     is in flight (a lone caller), DMA'd from it directly (zero-copy: no host memcpy
+ *     either way; parity / rebuilt rows are DMA'd straight back into it); under
+ *     concurrency pinned blocks are staged like any other, which measured at least as
+ *     fast;
  *   - a batch is launched when it is full, when fewer than slots-1 batches of its lane
  *     are in flight (batch while busy), when its oldest block has waited max_wait_us,
  *     or on flush; it is sealed — later blocks open the next batch — once it holds half

@@ -129,6 +129,22 @@ int launch_ehx_ua(const EncArgs& a, hipStream_t s) {
     return PATH_NONE;
 }
 
+#if ZS3_DIAG
+// RS(4+4) (the 8-drive default) encode + sums candidates above 2048 stripes (round 4):
+//  369: the RS(8+4) round-4 product recipe (buffer-addressed columns, conflict-free LDS
+//       stride TSP 1); 370: 4 stripes of 1 KiB tiles, quad-form hash waves issuing the L2
+//       prefetch, 16-byte columns (the RS(12+4) product shape); 371: 16 stripes of 512-byte
+//       tiles with the L2 prefetch (the RS(4+3) shape)
+static bool launch_ehx_km_4_4(int v, const EncArgs& a, hipStream_t s) {
+    switch (v) {
+        case 369: return launch_ws_t<4, 4, 16, 384, 1, true, false, 0, false, 1, 0, false, 3, false, 0, 0, false, 3, 1>(a, s);
+        case 370: return launch_ws_t<4, 4, 4, 1024, 1, true, true, 0, false, 0, 16, false, 3, false, 0, 2, false, 2, 1>(a, s);
+        case 371: return launch_ws_t<4, 4, 16, 512, 1, true, false, 0, false, 0, 16, false, 3, false, 0, 2, false, 3, 1>(a, s);
+        default: return false;
+    }
+}
+#endif
+
 int launch_ehx(int v, const EncArgs& a, hipStream_t s) {
     if (v == 0) {
         if (a.k == 8 && a.m == 4) return launch_ehx_default<8, 4>(a, s);
@@ -145,6 +161,7 @@ int launch_ehx(int v, const EncArgs& a, hipStream_t s) {
     if (a.k == 4 && a.m == 2) ok = launch_ehx_km_4_2(v, a, s);
     if (a.k == 16 && a.m == 4) ok = launch_ehx_km_16_4(v, a, s);
     if (a.k == 12 && a.m == 4) ok = launch_ehx_km_12_4(v, a, s);
+    if (a.k == 4 && a.m == 4) ok = launch_ehx_km_4_4(v, a, s);
     if (ok) return ((v >= 100 && v < 200) || v >= 300) ? PATH_WS : PATH_PIPE;
 #endif
     return PATH_NONE;

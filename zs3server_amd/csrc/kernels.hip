@@ -1568,8 +1568,9 @@ static hipError_t run_encode_fast(const EncArgs& a, hipStream_t s, int* path) {
         if constexpr ((K == 8 && M == 4) || (K == 4 && M == 2) || (K == 16 && M == 4)) {
             if (fv > 0 && p == PATH_NONE) p = launch_variant<K, M>(fv, a, s);
         }
-        if constexpr (K == 12 && M == 4) {
-            // the RS(12+4) unaligned-row shapes at aligned rows (memory-pattern A/B)
+        if constexpr ((K == 12 || K == 4) && M == 4) {
+            // the RS(12+4) unaligned-row shapes at aligned rows (memory-pattern A/B); the
+            // RS(4+4) candidates 369-371
             if (fv >= 330 && p == PATH_NONE) p = launch_ehx(fv, a, s);
         }
 #endif

@@ -32,11 +32,13 @@ static bool vr12_ua(int v, const VrArgs& a, hipStream_t s) {
         // bytes spill in-flight load registers (scripts/check_async_loads.py) and are not
         // compiled
         case 269: return launch_vr_ws_t<12, EX, H, 4, 1024, 1, 8, false, true, 4, true>(a, s);
-        // the L2 prefetch by the hash waves (PFD, as in the encode): product + prefetch 2 /
-        // 3 tiles ahead (265 / 266); 4 stripes of 1 KiB tiles, quad-form hash waves issuing
-        // it 2 tiles ahead (268)
+        // the L2 prefetch by the hash waves (PFD, as in the encode): product + prefetch 2
+        // tiles ahead (265; 3 tiles ahead measured slower still, profiles/r04/
+        // get_ab_k12_pfd.jsonl); 4 stripes of 1 KiB tiles, quad-form hash waves issuing it
+        // 2 tiles ahead (268); 266: 4 stripes of 1 KiB tiles, quad-form hash waves, 16-byte
+        // rebuild columns, no prefetch
         case 265: return launch_vr_ws_t<12, EX, H, 8, 512, 1, 8, false, true, 4, true, false, 2>(a, s);
-        case 266: return launch_vr_ws_t<12, EX, H, 8, 512, 1, 8, false, true, 4, true, false, 3>(a, s);
+        case 266: return launch_vr_ws_t<12, EX, H, 4, 1024, 1, 16, true, true, 4, true>(a, s);
         case 268: return launch_vr_ws_t<12, EX, H, 4, 1024, 1, 8, true, true, 4, true, false, 2>(a, s);
         default: return false;
     }

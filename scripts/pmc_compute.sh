@@ -21,7 +21,7 @@ for grp in "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY 
     i=$((i + 1))
     echo "pmc pass $i $(date +%T)"
     timeout -s KILL 240 rocprofv3 --pmc $grp -d $OUT/cpmc$i -o p --output-format csv -- \
-        python scripts/bench_paths.py > $OUT/cpmc$i.log 2>&1 || { tail -5 $OUT/cpmc$i.log; continue; }
+        python scripts/bench_paths.py > $OUT/cpmc$i.log 2>&1 || { tail -5 $OUT/cpmc$i.log; exit 5; }
     cp $(find $OUT/cpmc$i -name '*counter_collection.csv' | head -1) $P/pmc_compute_pass$i.csv
 done
 python scripts/pmc_compute_join.py $P/pmc_compute_kernel_stats.csv $P/pmc_compute_pass*.csv > $P/pmc_compute.json

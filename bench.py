@@ -13,14 +13,23 @@ Total work is fixed as N grows -> "scaling": "strong".  No data-path collective:
 carries only the timing barrier and the max-over-ranks reduction.  --objects N
 switches to weak scaling (N objects per GPU).
 
-Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
-torch.distributed.run (one rank per GPU).
+Launch: python bench.py [--gpus N --steps K --warmup W].  For N > 1 either under
+torch.distributed.run (one rank per GPU, WORLD_SIZE must equal N), or plain: the process
+then spawns the N ranks itself (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* per child,
+before any GPU call in the parent) and relays rank 0's line.  It exits non-zero when
+fewer than N devices are visible or WORLD_SIZE disagrees with --gpus: it never reports
+N GPUs it did not use.  Test-only switches (the JSON line says so): ZS3_BENCH_SAME_DEVICE=1
+puts every rank on device 0 (rehearsing N ranks on a 1-GPU box), ZS3_BENCH_DRY_RUN=1
+runs the launcher, rendezvous, barriers and max-over-ranks on CPU with no GPU work
+(value null).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -90,11 +99,28 @@ def cpu_baseline(k: int, m: int, blen: int, seconds: float) -> dict:
     }
 
 
+# The kernel instance each bench launch runs (fused_v2.hip launch_ehx_default: n > 2048
+# stripes of RS(8+4) at 1 MiB take the named shape Rs84Bulk).  committed_traffic matches
+# this full name, so counters of an older instance are never attached to the current one;
+# scripts/profile_round.sh checks that the traced kernel carries this name.
+HEADLINE_KERNEL = {(8, 4, 1 << 20): "void zs3k::k_ehx_ws<8, 4, zs3k::shape::Rs84Bulk>(zs3k::EncArgs)"}
+HEADLINE_MIN_OBJECTS = 2049
+
+
+def headline_kernel(k: int, m: int, blen: int, nobj: int):
+    if nobj < HEADLINE_MIN_OBJECTS:
+        return None
+    return HEADLINE_KERNEL.get((k, m, blen))
+
+
 def committed_traffic(k: int, m: int, nobj: int, blen: int):
     """Per-launch HBM bytes measured by scripts/profile_round.sh (two rocprofv3 PMC
-    passes, FETCH_SIZE doubled per the gfx950 correction) for this workload, if the
-    committed profile was taken on the same shape."""
+    passes, FETCH_SIZE doubled per the gfx950 correction) for exactly this kernel
+    instance (full name) and objects per launch; the newest round's entry wins."""
     import glob
+    want = headline_kernel(k, m, blen, nobj)
+    if want is None:
+        return None, None
     best = None
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json"))):
         try:
@@ -102,9 +128,46 @@ def committed_traffic(k: int, m: int, nobj: int, blen: int):
         except Exception:
             continue
         for name, v in d.items():
-            if f"<{k}, {m}," in name and v.get("workload", {}).get("objects") == nobj:
+            kname = name.split(" @ ")[0]
+            if kname == want and v.get("workload", {}).get("objects") == nobj:
                 best = (v["hbm_bytes_per_launch"], os.path.relpath(path, ROOT))
     return best if best else (None, None)
+
+
+def _free_port() -> int:
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(n: int, argv: list) -> int:
+    """Spawn the N ranks of `bench.py --gpus N` (the parent never touches a GPU: counting
+    devices does not initialise HIP on this image).  Rank 0's stdout is relayed; the
+    exit code is the worst of the children's."""
+    same = os.environ.get("ZS3_BENCH_SAME_DEVICE") == "1"
+    dry = os.environ.get("ZS3_BENCH_DRY_RUN") == "1"
+    if not (same or dry):
+        vis = torch.cuda.device_count()
+        if vis < n:
+            print(f"bench.py: --gpus {n} needs {n} visible devices, found {vis} "
+                  f"(set ZS3_BENCH_SAME_DEVICE=1 only to rehearse the ranks on one device)", file=sys.stderr)
+            return 2
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), ZS3_BENCH_CHILD="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    for p in procs:
+        c = p.wait()
+        if c != 0 and rc == 0:
+            rc = c
+            for q in procs:  # one rank failed: the others would wait at a barrier forever
+                if q.poll() is None:
+                    q.terminate()
+    return rc if rc >= 0 else 1
 
 
 def main() -> None:
@@ -129,9 +192,22 @@ def main() -> None:
 
     from zs3server_amd.dist import max_over_ranks, object_range, rank_env, split_range
 
+    if args.gpus < 1:
+        sys.exit(f"bench.py: --gpus must be >= 1, got {args.gpus}")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world, rank, local = rank_env()
+    if world != args.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: refusing to report a different N")
+    same_dev = os.environ.get("ZS3_BENCH_SAME_DEVICE") == "1"
+    dry = os.environ.get("ZS3_BENCH_DRY_RUN") == "1"
     if world > 1:
         dist.init_process_group("gloo")  # control only: barrier + max of timings
+    if dry:
+        return dry_run(args, world, rank)
+    if torch.cuda.device_count() < (1 if same_dev else world):
+        sys.exit(f"bench.py: rank {rank} needs device {local}, {torch.cuda.device_count()} visible")
+    local = 0 if same_dev else local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -208,13 +284,15 @@ def main() -> None:
             "data": "synthetic (splitmix64 counter stream per object id), device-resident in HBM",
             "config": {"workload": wl, "total_objects": total_objects, "objects_per_gpu": nobj,
                        "block_bytes": blen, "k": k, "m": m,
-                       "parallelism": f"objects partitioned over {world} GPU(s), no collectives",
+                       "parallelism": f"objects partitioned over {world} GPU(s), no collectives"
+                                      + (" (TEST: all ranks on device 0)" if same_dev else ""),
                        "kernel_path": {0: "generic", 1: "first-generation", 2: "warp-specialised",
                                        3: "mixed-wave", 4: "small-batch latency"}.get(path, str(path))},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
                          "traffic_source": traffic_src,
+                         "kernel": headline_kernel(k, m, blen, nobj),
                          "kernel_ms": round(kern_ms, 4),
                          "algo_bytes_per_launch": abytes},
         }
@@ -223,6 +301,26 @@ def main() -> None:
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def dry_run(args, world: int, rank: int) -> None:
+    """ZS3_BENCH_DRY_RUN=1 (tests only): the launcher, rendezvous, barriers and the
+    max-over-ranks reduction without any GPU work; value is null."""
+    from zs3server_amd.dist import max_over_ranks
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    time.sleep(0.01 * (rank + 1))
+    if world > 1:
+        dist.barrier()
+    elapsed, = max_over_ranks([time.perf_counter() - t0], world)
+    if rank == 0:
+        print(json.dumps({"metric": "dry run (launcher test, no GPU work)", "value": None, "unit": "GiB/s",
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(elapsed * 1e3, 3), "dry_run": True,
+                          "ranks_seen": world, "pid": os.getpid()}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

@@ -270,6 +270,30 @@ int64_t zs3_stream_encode(const zs3_codec* c, const uint8_t* h_src, int64_t tota
 int64_t zs3_stream_encode_multi(const zs3_codec* c, const int* devices, int n_devices, const uint8_t* h_src,
                                 int64_t total_len, uint8_t* h_parity, uint8_t* h_sums, int64_t batch_blocks);
 
+/* Streamed GET / heal of one object (SURVEY.md §8f.1 / §8f.3 over a whole part): the
+ * Erasure.Decode and Erasure.Heal block loops (erasure-decode.go:230-276, :287-332) in
+ * device batches of batch_blocks blocks, pipelined (H2D of the next batch's survivor
+ * rows || fused verify + rebuild (+ heal sums) || D2H of the previous batch's rebuilt
+ * rows), so a lone large GET or heal does not pay a device round trip per block.
+ *   h_stripes : the object's total_len bytes as ceil(total_len/blockSize) stripes, stripe b
+ *               at h_stripes + b*(k+m)*S (S = ShardSize), row i at + i*S_b (S_b = S, the
+ *               short last block its own ceil(len/k)); present rows hold the shard chunks
+ *               the readers returned, missing rows anything.  Missing data rows (GET,
+ *               data_only != 0) or all missing rows (heal) are rebuilt in place.
+ *   h_present : n_blocks x (k+m) flags (a reader may drop out mid-object)
+ *   h_expect  : n_blocks x (k+m) x 32 stored bitrot sums of the chunks (NULL: no verify);
+ *               h_bad (n_blocks x (k+m) int32, optional) flags every survivor whose sum
+ *               differs (errFileCorrupt: re-read that block with the shard dropped)
+ *   h_sums_out: heal only (optional): n_blocks x (k+m) x 32, HighwayHash-256 of the rebuilt rows
+ *   h_status  : optional n_blocks int32: each block's reedsolomon status
+ * Pinned (zs3_host_alloc / hipHostMalloc) stripes move by DMA; pageable ones are staged by
+ * helper threads.  Runs on the calling thread's device.  Returns the number of blocks, or
+ * the first block's error (ZS3_ERR_TOO_FEW_SHARDS, ...) after serving every other block
+ * (a failed block's missing rows are undefined). */
+int64_t zs3_stream_decode(const zs3_codec* c, uint8_t* h_stripes, int64_t total_len, const uint8_t* h_present,
+                          int data_only, const uint8_t* h_expect, int32_t* h_bad, uint8_t* h_sums_out,
+                          int32_t* h_status, int64_t batch_blocks);
+
 /* Range [lo, hi) of `total` units owned by `rank` of `world`: contiguous, near-equal,
  * the first total % world ranks one longer (the object / block split of the
  * multi-GPU paths). */
@@ -291,8 +315,13 @@ void zs3_split_range(int64_t total, int world, int rank, int64_t* lo, int64_t* h
  *   - a batch is launched when it is full, when fewer than slots-1 batches of its lane
  *     are in flight (batch while busy), when its oldest block has waited max_wait_us,
  *     or on flush; it is sealed — later blocks open the next batch — once it holds half
- *     of its lane's live blocks (at least 8, at most 64 MiB of input), so that with T
- *     synchronous callers two batches of ~T/2 alternate and overlap their copies;
+ *     of its lane's live blocks (at least 8), so that with T synchronous callers two
+ *     batches of ~T/2 alternate and overlap their copies.  A batch holds at most
+ *     max(8, 64 MiB / blockSize) blocks (at most 512, and at most max_batch when set):
+ *     the staging slots are sized to exactly that;
+ *   - several devices (opts.devices): every device has its own slots, streams and
+ *     threads; a block goes to the device with the fewest live blocks of its lane, and
+ *     each device batches its own blocks (a node's GPUs and PCIe links share the load);
  *   - when the batch is done, zs3_req_wait copies its own block's results back into
  *     the caller's buffers on the calling thread; blocks nobody is waiting for are
  *     copied back by the queue's completion thread.
@@ -308,14 +337,18 @@ void zs3_split_range(int64_t total, int world, int rank, int64_t* lo, int64_t* h
 typedef struct zs3_queue zs3_queue;
 typedef struct zs3_req zs3_req;
 typedef struct {
-    int device;       /* HIP device ordinal; -1 = the calling thread's current device */
-    int max_batch;    /* blocks per device batch (0 = 128).  Memory per lane in use:
-                         slots x max_batch x (k+m) x S of pinned host AND of device
-                         memory (+ sums); RS(8+4) 1 MiB, 4 slots, 128: 768 MiB each.
-                         The shim sizes it by bytes (384 MiB per slot: 256 at 1 MiB,
-                         25 at 10 MiB) */
+    int device;       /* HIP device ordinal; -1 = the calling thread's current device
+                         (ignored when n_devices > 0) */
+    int max_batch;    /* upper bound on blocks per device batch (0 = the default:
+                         max(8, 64 MiB / blockSize), at most 512).  Memory per lane in use,
+                         per device: slots x batch x (k+m) x S of pinned host AND of device
+                         memory (+ sums): RS(8+4) 1 MiB, 4 slots x 64 blocks = 384 MiB
+                         each; the encode, GET and heal lanes are allocated on first use */
     int max_wait_us;  /* longest a block waits for its batch to fill (0 = 200) */
     int slots;        /* pinned staging slots (+ streams) per lane (0 = 4; at least 2) */
+    const int* devices;  /* n_devices HIP ordinals to spread the blocks over (a node's
+                            GPUs; repeats allowed); NULL / 0 = the one `device` */
+    int n_devices;       /* 0..64 */
 } zs3_queue_opts;
 
 int zs3_queue_new(const zs3_codec* c, const zs3_queue_opts* opts /* NULL = defaults */, zs3_queue** out);
@@ -350,6 +383,8 @@ int64_t zs3_req_wait(zs3_req* req);
 int zs3_queue_flush(zs3_queue* q);   /* launch the open batches now */
 int zs3_queue_stats(const zs3_queue* q, int64_t* batches, int64_t* blocks);
 int64_t zs3_queue_zero_copy_blocks(const zs3_queue* q);  /* blocks DMA'd from / to pinned callers */
+/* Per-device counters of a multi-device queue: index = position in opts.devices. */
+int zs3_queue_device_stats(const zs3_queue* q, int index, int* device, int64_t* batches, int64_t* blocks);
 
 /* Synchronous conveniences (submit + wait): what the cgo shim calls per block. */
 int64_t zs3_queue_encode_data(zs3_queue* q, uint8_t* h_buf, int64_t len, int64_t cap, uint8_t* h_sums);

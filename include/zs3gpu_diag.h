@@ -22,6 +22,12 @@ int zs3_debug_set_variant(int variant);
 /* Device buffer receiving per-wave stamps from the stamped variants (NULL = off),
  * for the calling thread. */
 int zs3_debug_set_buffer(void* d_dbg);
+/* 1 if zs3_encode_batch accepts this batch layout (parity_bytes = m * ShardSize),
+ * 0 if it returns ZS3_ERR_INVALID_ARG for it.  Host-only: no device call, so the
+ * layout rules are testable without a GPU.  (The diagnostics build also accepts
+ * data_stride = parity_stride = 0, its timing-only aliased runs.) */
+int zs3_debug_encode_layout_ok(const void* d_data, int64_t data_stride, int64_t block_len, int64_t n_blocks,
+                               const void* d_parity, int64_t parity_stride, int64_t parity_bytes);
 
 #ifdef __cplusplus
 }

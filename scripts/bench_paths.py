@@ -3,7 +3,7 @@ BASELINE shapes, each as one JSON line with its roofline (algorithmic HBM bytes 
 launch / median launch time, against the 8 TB/s HBM3E spec), plus the batching queue
 and the end-to-end host stream.
 
-  PATHS=encode,geom,rec,get,hash,deep,digest,queue,e2e  python scripts/bench_paths.py
+  PATHS=encode,geom,rec,get,hash,deep,digest,queue,e2e,stream_get  python scripts/bench_paths.py
 (default: all).  Kernel-only sections (encode..digest) are what scripts/profile_paths.sh
 runs under rocprofv3; queue and e2e include host copies and PCIe.
 """
@@ -316,3 +316,104 @@ if "e2e" in PATHS:
                 for x in (src, par, sums):
                     x.free()
             del src, par, sums
+    # the same stream split over two device entries (zs3_stream_encode_multi; on a 1-GPU
+    # box both are device 0: the split, threads and slots of an N-device run, one HBM)
+    k, m, bs = 16, 4, MiB
+    total = int(gib * (1 << 30))
+    nblk = total // bs
+    S = bs // k
+    codec = z.Codec(k, m, bs)
+    src, par, sums = z.HostBuffer(total), z.HostBuffer(nblk * m * S), z.HostBuffer(nblk * (k + m) * 32)
+    src.array[:] = 7
+    devs = [int(x) for x in os.environ.get("E2E_DEVICES", "0,0").split(",")]
+    codec.stream_encode_multi(devs, src, 64 * bs, par, sums, batch_blocks=64)
+    t0 = time.perf_counter()
+    codec.stream_encode_multi(devs, src, total, par, sums, batch_blocks=512)
+    dt = time.perf_counter() - t0
+    print(json.dumps({"path": "stream_encode_multi_e2e", "what": f"RS({k}+{m}) {gib:g} GiB stream, 1 MiB blocks",
+                      "devices": devs, "host_buffers": "pinned", "seconds": round(dt, 3),
+                      "GiBps": round(total / dt / 2**30, 2),
+                      "pcie_GBps": round((total + nblk * (m * S + 32 * (k + m))) / dt / 1e9, 1)}), flush=True)
+    for x in (src, par, sums):
+        x.free()
+
+# ---- one large GET / heal (Erasure.Decode / Erasure.Heal block loops) streamed through
+# the device (zs3_stream_decode) vs the per-block queue path of a lone caller and the CPU
+if "stream_get" in PATHS:
+    from oracle import cpuref, oracle_c
+    gib = float(os.environ.get("SG_GIB", "1"))
+    for (k, m, lost) in ((12, 4, [1, 12]), (8, 4, [2, 9])):
+        R = k + m
+        S = -(-MiB // k)
+        E = R * S
+        nblk = int(gib * 1024)
+        codec = z.Codec(k, m, MiB)
+        for pinned in (True, False):
+            st_h = z.HostBuffer(nblk * E) if pinned else None
+            st = st_h.array if pinned else np.empty(nblk * E, np.uint8)
+            st[:] = 0
+            d = torch.empty(nblk * E, dtype=torch.uint8, device="cuda")
+            z.fill_batch(d, E, MiB, nblk, seed=17)
+            sums_d = torch.empty(nblk * R * 32, dtype=torch.uint8, device="cuda")
+            codec.encode_batch(d, E, MiB, nblk, parity=d, parity_offset=k * S, parity_stride=E, sums=sums_d)
+            st[:] = d.cpu().numpy()
+            sums = sums_d.cpu().numpy().reshape(nblk, R, 32)
+            del d, sums_d
+            present = np.ones((nblk, R), bool)
+            present[:, lost] = False
+            bad = np.zeros((nblk, R), np.int32)
+            for heal in (False, True):
+                outs = np.zeros((nblk, R, 32), np.uint8) if heal else None
+                arg = st_h if pinned else st
+                codec.stream_decode(arg, 64 * MiB, present[:64], not heal, expect=sums[:64], bad=bad[:64],
+                                    sums_out=outs[:64] if heal else None, batch_blocks=64)
+                ts = []
+                for _ in range(3):
+                    t0 = time.perf_counter()
+                    n = codec.stream_decode(arg, nblk * MiB, present, not heal, expect=sums, bad=bad, sums_out=outs,
+                                            batch_blocks=128)
+                    ts.append(time.perf_counter() - t0)
+                    assert n == nblk and not bad.any(), n
+                dt = sorted(ts)[1]
+                e = len(lost) if heal else len([i for i in lost if i < k])
+                pcie = nblk * ((k if not heal else k) * S + e * S + R * 32 * (2 if heal else 1))
+                print(json.dumps({"path": "stream_decode", "what": f"RS({k}+{m}) lone {'heal' if heal else 'GET'} of "
+                                  f"{nblk} x 1 MiB blocks, lost {lost}", "host_buffers": "pinned" if pinned else "pageable",
+                                  "seconds": round(dt, 4), "GiBps_object": round(nblk * MiB / dt / 2**30, 2),
+                                  "us_per_block": round(dt / nblk * 1e6, 1)}), flush=True)
+            if st_h is not None:
+                st_h.free()
+            del st
+        # CPU reference structure for the same heal (verify k survivors, rebuild e rows,
+        # hash them): cpu_ref's encode + hash with the e rebuild rows as the coding rows
+        # (GF cost is value-independent), 64 blocks repeated, T = 1 and T = all
+        e = len(lost)
+        mat = oracle_c.build_matrix(k, e)
+        nb = 64
+        data = np.concatenate([oracle_c.fill(0, b, MiB) for b in range(nb)])
+        par = np.zeros(nb * e * S, np.uint8)
+        sm = np.zeros(nb * (k + e) * 32, np.uint8)
+        for T in (1, cpuref.threads_available()):
+            reps, t0 = 0, time.perf_counter()
+            while time.perf_counter() - t0 < 3.0:
+                cpuref.encode_hash(k, e, mat, data, MiB, nb, MiB, par, e * S, sm, KEY, T)
+                reps += 1
+            dt = time.perf_counter() - t0
+            print(json.dumps({"path": "cpu_heal_ref", "what": f"RS({k}+{m}) heal {e} rows (verify {k} + rebuild {e} + "
+                              f"hash {e}) on the host, cpu_ref ({cpuref.isa()})", "threads": T,
+                              "GiBps_object": round(reps * nb * MiB / dt / 2**30, 2),
+                              "us_per_block": round(dt / (reps * nb) * 1e6, 1)}), flush=True)
+        # the per-block queue path of a lone synchronous caller (round 4: ~306 us per block)
+        q = z.Queue(codec, max_wait_us=200)
+        sh_ = np.zeros((R, S), np.uint8)
+        pres = np.ones(R, bool)
+        pres[lost] = False
+        t0 = time.perf_counter()
+        nq = 200
+        for _ in range(nq):
+            q.decode(sh_, pres, False, sums_out=np.zeros((R, 32), np.uint8))
+        dt = time.perf_counter() - t0
+        print(json.dumps({"path": "queue_lone_heal", "what": f"RS({k}+{m}) heal {len(lost)}, one block per call",
+                          "GiBps_object": round(nq * MiB / dt / 2**30, 2), "us_per_block": round(dt / nq * 1e6, 1)}),
+              flush=True)
+        q.close()

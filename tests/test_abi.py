@@ -150,6 +150,33 @@ def test_encode_batch_rejects_bad_layouts(case):
     assert rc == -8, (case, rc)
 
 
+@pytest.mark.parametrize("k,m", [(2, 2), (3, 3), (4, 4), (8, 4), (8, 8), (12, 4)])
+def test_encode_batch_layouts_accepted(k, m):
+    """separate data / parity regions are accepted whatever the strides.
+    The queue's encode slots put [n][k*S] data then [n][m*S] parity, so for k == m (RS(2+2),
+    RS(3+3), RS(4+4): the 4-, 6- and 8-drive defaults) both strides are equal; the layout
+    check runs on the host only (zs3_debug_encode_layout_ok, no device call)."""
+    import ctypes as C
+    L = z.diag_lib()
+    B = 1 << 20
+    S = -(-B // k)
+    KS, MS = k * S, m * S
+    ok = lambda d, ds, n, p, ps: L.zs3_debug_encode_layout_ok(C.c_void_p(d), ds, B, n, C.c_void_p(p), ps, MS)
+    for n in (1, 2, 5, 256):
+        cap = n
+        # the queue slot: data region then parity region right after it
+        assert ok(BASE, KS, n, BASE + cap * KS, MS) == 1, (k, m, n, "queue slot")
+        # separately allocated regions with equal strides, either order, any address gap
+        assert ok(BASE, KS, n, BASE + (1 << 34) + 17, KS) == 1, (k, m, n, "separate, equal strides")
+        assert ok(BASE + (1 << 34), KS, n, BASE, KS) == 1, (k, m, n, "parity below data")
+        # the reference's in-place Split layout
+        assert ok(BASE, (k + m) * S, n, BASE + KS, (k + m) * S) == 1, (k, m, n, "in place")
+    # equal strides whose spans interleave without landing in each block's gap: rejected
+    assert ok(BASE, KS + MS, 4, BASE + KS - 16, KS + MS) == 0
+    # separate spans that overlap with different strides: rejected
+    assert ok(BASE, KS, 4, BASE + 2 * KS, MS) == 0
+
+
 @pytest.mark.parametrize("fn", ["reconstruct", "verify", "reconstruct_masks", "verify_masks"])
 @pytest.mark.parametrize("stride_delta", [-1, -(1 << 30)])
 def test_stripe_batches_reject_short_strides(fn, stride_delta):

@@ -69,12 +69,12 @@ def test_concurrent_first_callers_share_one_codec():
     assert len(FakeQueue.made) == 2
 
 
-@pytest.mark.parametrize("k,m,bs,want", [(8, 4, MiB, 256), (12, 4, MiB, 287), (4, 2, MiB, 256), (16, 4, MiB, 307),
-                                         (8, 4, 10 * MiB, 25), (12, 4, 10 * MiB, 28), (2, 2, 64 * MiB, 4),
+@pytest.mark.parametrize("k,m,bs,want", [(8, 4, MiB, 64), (12, 4, MiB, 64), (4, 2, MiB, 64), (16, 4, MiB, 64),
+                                         (8, 4, 10 * MiB, 8), (12, 4, 10 * MiB, 8), (2, 2, 64 * MiB, 8),
                                          (8, 4, 64 << 10, 512)])
 def test_queue_batch_sized_by_bytes(k, m, bs, want):
-    """Blocks per batch from the slot byte budget: RS(8+4) 1 MiB closes batches of 256
-    stripes (above the 128-stripe small-batch latency path), legacy 10 MiB blocks 25."""
+    """Blocks per batch by input bytes, the library's rule (queue_policy.hpp slot_blocks):
+    64 MiB of input, 8..512 blocks — RS(8+4) 1 MiB 64, legacy 10 MiB blocks 8."""
     c = ze.get_gpu_codec(k, m, bs, FakeQueue)
     assert c.max_batch == want == ze.queue_max_batch(k, m, bs)
     assert FakeQueue.made[-1].max_batch == want

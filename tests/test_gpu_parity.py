@@ -106,12 +106,8 @@ RECON_PATTERNS = [
 
 @pytest.mark.parametrize("k,m,erased", RECON_PATTERNS)
 @pytest.mark.parametrize("data_only", [True, False])
-@pytest.mark.parametrize("variant", [0, 220, 221, 222])
-def test_reconstruct_batch(oracle, k, m, erased, data_only, variant):
-    """variant 220/221: the reconstruct kernel with 2/4 columns per thread (e <= 2); 222:
-    non-temporal loads and stores."""
-    with variant_ctx(variant):
-        run_reconstruct_case(oracle, k, m, erased, data_only)
+def test_reconstruct_batch(oracle, k, m, erased, data_only):
+    run_reconstruct_case(oracle, k, m, erased, data_only)
 
 
 def run_reconstruct_case(oracle, k, m, erased, data_only):

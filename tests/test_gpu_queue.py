@@ -185,15 +185,18 @@ def test_queue_mixed_encode_and_decode_concurrently(oracle):
     q.close()
 
 
-def test_queue_batches_concurrent_blocks(oracle):
+@pytest.mark.parametrize("k,m,bs", [(8, 4, 1 << 16), (4, 4, 1 << 20), (2, 2, 1 << 20), (3, 3, 1 << 16)])
+def test_queue_batches_concurrent_blocks(oracle, k, m, bs):
     """Under concurrency the queue forms multi-block batches (fewer launches than
-    blocks): 16 threads x 8 blocks, async submits, then waits."""
-    k, m, bs = 8, 4, 1 << 16
+    blocks): 16 threads x 8 blocks, async submits, then waits.  k == m (RS(2+2), RS(3+3),
+    RS(4+4): the 4-, 6- and 8-drive defaults) gives the slot's data and parity regions
+    equal strides, which the encode layout check once rejected for every batch of two or
+    more full blocks."""
     codec = z.Codec(k, m, bs)
     q = z.Queue(codec, max_batch=64, max_wait_us=2000)
     R = k + m
     mat = oracle.build_matrix(k, m)
-    S = bs // k
+    S = -(-bs // k)
 
     def worker(t):
         bufs, reqs, sums = [], [], []
@@ -229,18 +232,23 @@ def test_queue_zero_copy_pinned_callers(oracle, k, m, bs, zc_mode, monkeypatch):
     padding (k*S > blockSize): a zero-copy block DMAs only its `len` data bytes, so the
     slot's padding bytes hold whatever the slot's previous batch left there, and every
     encode kernel must read them as zero.  Pinned-caller modes (queue.hip,
-    ZS3_QUEUE_ZC): 1 = zero-copy for a lone caller's block (first of its batch, no other
-    batch of the lane in flight), the rest staged (the default); 2 = every full block by a
-    DMA of its own; 3 = copy-list kernels over the mapped pinned pages."""
+    ZS3_QUEUE_ZC, diagnostics build only): 1 = zero-copy for a lone caller's block (first
+    of its batch, no other batch of the lane in flight), the rest staged (the default and
+    the product library's only mode); 2 = every full block by a DMA of its own; 3 =
+    copy-list kernels over the mapped pinned pages."""
+    # the ZS3_QUEUE_ZC switch is read by the diagnostics build only (the product library
+    # always runs mode 1); a codec and its queue belong to the library that made them
     monkeypatch.setenv("ZS3_QUEUE_ZC", str(zc_mode))
-    codec = z.Codec(k, m, bs)
-    q = z.Queue(codec, max_batch=16, max_wait_us=500)
     R = k + m
     S = -(-bs // k)
     mat = oracle.build_matrix(k, m)
     nthr, per = 8, 4
-    pins = [z.HostBuffer(R * S + 64) for _ in range(nthr)]
-    pins_dec = [z.HostBuffer(R * S) for _ in range(nthr)]
+    with z.diag(0):
+        codec = z.Codec(k, m, bs)
+        q = z.Queue(codec, max_batch=16, max_wait_us=500)
+        # pinned ranges are registered per library: allocate from the queue's library
+        pins = [z.HostBuffer(R * S + 64) for _ in range(nthr)]
+        pins_dec = [z.HostBuffer(R * S) for _ in range(nthr)]
 
     def worker(t):
         pinned = t % 2 == 0
@@ -333,3 +341,55 @@ def test_queue_lone_pinned_caller_zero_copy(oracle, k, m):
     finally:
         q.close()
         pin.free()
+
+
+@pytest.mark.parametrize("k,m,bs", [(8, 4, 1 << 20), (12, 4, 1 << 20), (4, 4, 1 << 16)])
+def test_queue_multi_device_16_threads(oracle, k, m, bs):
+    """A multi-device queue (zs3_queue_opts.devices; here both entries are device 0, the
+    box has one GPU): 16 submitter threads encode and decode / heal through it, every
+    result vs the oracle, and both device parts received blocks and launched batches of
+    their own (the assignment policy itself is checked on the CPU, tests/test_queue_policy.py)."""
+    codec = z.Codec(k, m, bs)
+    q = z.Queue(codec, max_wait_us=300, devices=[0, 0])
+    R = k + m
+    S = -(-bs // k)
+    mat = oracle.build_matrix(k, m)
+
+    def worker(t):
+        for i in range(6):
+            data = oracle.fill(1100 + t, i, bs)
+            buf = np.zeros(R * S + 32, np.uint8)
+            buf[:bs] = data
+            got_S, sums = q.encode_data(buf, bs)
+            want = oracle.encode_data(k, m, data, mat)
+            assert got_S == S
+            assert np.array_equal(buf[:R * S].reshape(R, S), want), (t, i)
+            assert np.array_equal(sums, oracle.hh256_rows(KEY, want)), (t, i)
+            if i % 2:
+                sh, ssum = want, oracle.hh256_rows(KEY, want)
+                work = sh.copy()
+                present = np.ones(R, bool)
+                present[[(i + t) % k, k + (t % m)]] = False
+                work[~present] = 0x5A
+                heal = t % 2 == 1
+                out = np.zeros((R, 32), np.uint8) if heal else None
+                bad = np.full(R, 9, np.int32)
+                assert q.decode(work, present, not heal, expect=ssum, bad=bad, sums_out=out) == 0, (t, i)
+                assert not bad.any()
+                for r in range(R):
+                    if present[r] or r < k or heal:
+                        assert np.array_equal(work[r], sh[r]), (t, i, r)
+                if heal:
+                    for r in np.nonzero(~present)[0]:
+                        assert np.array_equal(out[r], ssum[r]), (t, i, r)
+
+    run_threads(16, worker)
+    batches, blocks = q.stats()
+    assert blocks == 16 * 6 + 16 * 3
+    per = [q.device_stats(i) for i in range(2)]
+    assert [d for d, _, _ in per] == [0, 0]
+    assert sum(n for _, _, n in per) == blocks and sum(b for _, b, _ in per) == batches
+    assert all(n > 0 and b > 0 for _, b, n in per), per
+    # the assignment keeps the two parts within a few blocks of each other
+    assert abs(per[0][2] - per[1][2]) <= 16, per
+    q.close()

@@ -76,25 +76,15 @@ WS_CASES = [(8, 4, 1 << 16, []), (8, 4, 1 << 16, [0, 5]), (8, 4, 1 << 16, [3, 9]
 @pytest.mark.parametrize("k,m,blen,erased", WS_CASES)
 @pytest.mark.parametrize("data_only", [True, False])
 @pytest.mark.parametrize("heal", [False, True])
-@pytest.mark.parametrize("variant", [0, 210, 211, 212, 213, 214, 216, 218, 230, 231, 232, 240, 241, 246,
-                                     260, 261, 262, 263])
+@pytest.mark.parametrize("variant", [0, 230, 231, 246, 247, 420, 421])
 def test_verify_reconstruct_ws(oracle, k, m, blen, erased, data_only, heal, variant):
     """Variant 0: the product dispatch; at 17 blocks it takes the small-batch latency
-    path (k_reconstruct + one chain per quad).  231 = the product dispatch without that
-    path, asserted to run k_vr_ws for every RS(8+4) GET and heal with 0-4 rebuilt rows
-    (zs3_last_path).  218 = split heal (GET rebuild + hash kernel)."""
-    e = len(erased) if heal else len([i for i in erased if i < k or not data_only])
-    want = None
-    if variant == 0:
-        want = 4
-    if variant in (231, 240, 241, 246):  # 240 / 241: scalar-table batching flipped / pairs; 246: plain loads
-        want = 2
-    if variant == 232 and heal and e >= 3:  # heal 3-4 on k_vr_ws (padded pair form)
-        want = 2
-    if variant in (260, 261, 262) and heal and e >= 1:  # r03 longer-tile heal instances
-        want = 2
-    if variant == 263 and not heal and e >= 1:  # r03 8-stripe rebuild, 384-byte tiles
-        want = 2
+    path (k_reconstruct + one chain per quad; 230 forces it).  231 = the product dispatch
+    without that path, asserted to run k_vr_ws for every RS(8+4) GET and heal with 0-4
+    rebuilt rows (zs3_last_path); 246 / 247 / 420 / 421 = the product shapes with plain
+    survivor loads / 64-bit addresses / the conflict-free LDS row stride / the
+    region-interleaved workgroup order (fused_v2.hpp launch_vr_ws_t)."""
+    want = {0: 4, 230: 4}.get(variant, 2)
     with variant_ctx(variant):
         run_verify_case(oracle, k, m, blen, erased, data_only, heal, nb=17, want_path=want)
 
@@ -106,12 +96,12 @@ WS4_CASES = [(4, 2, 1 << 16, []), (4, 2, 1 << 16, [1]), (4, 2, 1 << 16, [0, 5]),
 @pytest.mark.parametrize("k,m,blen,erased", WS4_CASES)
 @pytest.mark.parametrize("data_only", [True, False])
 @pytest.mark.parametrize("heal", [False, True])
-@pytest.mark.parametrize("variant", [0, 210])
+@pytest.mark.parametrize("variant", [0, 231])
 def test_verify_reconstruct_ws_rs42(oracle, k, m, blen, erased, data_only, heal, variant):
-    """RS(4+2)-shaped GET / heal on k_vr_ws: quad-form (default) and pair-form (210)
-    hash waves, tile edges and dead stripes."""
+    """RS(4+2)-shaped GET / heal on k_vr_ws (quad-form hash waves): tile edges and dead
+    stripes; 231 = the product dispatch asserted to run the warp-specialised kernel."""
     with variant_ctx(variant):
-        run_verify_case(oracle, k, m, blen, erased, data_only, heal, nb=11)
+        run_verify_case(oracle, k, m, blen, erased, data_only, heal, nb=11, want_path=2 if variant == 231 else None)
 
 
 WS16_HEAL_CASES = [(16, 4, 1 << 16, [0, 5]), (16, 4, 1 << 16, [3, 17]), (16, 4, 16 * 48, [2, 19]),
@@ -123,18 +113,15 @@ WS16_HEAL_CASES = [(16, 4, 1 << 16, [0, 5]), (16, 4, 1 << 16, [3, 17]), (16, 4, 
 
 
 @pytest.mark.parametrize("k,m,blen,erased", WS16_HEAL_CASES)
-@pytest.mark.parametrize("variant", [0, 215, 216, 218, 231, 232, 240, 241, 242, 246, 250, 256, 259])
+@pytest.mark.parametrize("variant", [0, 231, 246, 247, 420, 421])
 def test_heal_ws_rs164(oracle, k, m, blen, erased, variant):
-    """RS(16+4) heal (rebuild 1-4 shards and hash them) on k_vr_ws: the defaults (231 =
-    the product dispatch without the small-batch latency path that variant 0 takes at 11
-    blocks): padded pair-form hash waves, 8-byte rebuild columns for one lost shard and
-    4-byte columns of 128-byte tiles for 2-4 (232 forces the latter); 215 (quad-form
-    hash waves, e = 2 / 4), 216 (pair form, 8-byte columns, e = 1..4) and 218 (split:
-    GET rebuild + hash kernel).  The launched family is asserted: tile edges, ragged
-    tails and dead stripes of the 8-stripe workgroup."""
-    e = len(erased)
-    want = {0: 4, 231: 2, 215: 2 if e in (2, 4) else None, 216: 2, 218: 2,
-            232: 2, 240: 2, 241: 2, 242: 2, 246: 2, 250: None, 256: None, 259: 2}[variant]
+    """RS(16+4) heal (rebuild 1-4 shards and hash them) on k_vr_ws: the product shapes
+    (231 = the product dispatch without the small-batch latency path that variant 0 takes
+    at 11 blocks) and their memory-policy / layout variants (246 plain loads, 247 64-bit
+    addresses, 420 conflict-free LDS stride, 421 region-interleaved workgroups).  The
+    launched family is asserted: tile edges, ragged tails and dead stripes of the
+    8-stripe workgroup."""
+    want = 4 if variant == 0 else 2
     with variant_ctx(variant):
         run_verify_case(oracle, k, m, blen, erased, False, True, nb=11, want_path=want)
 
@@ -149,7 +136,7 @@ WS16_GET_CASES = [(16, 4, blen, erased, data_only)
 
 
 @pytest.mark.parametrize("k,m,blen,erased,data_only", WS16_GET_CASES)
-@pytest.mark.parametrize("variant", [0, 216, 217, 219, 231, 240, 241, 242, 246, 250, 256, 259])
+@pytest.mark.parametrize("variant", [0, 231, 246, 247, 420, 421])
 def test_verify_reconstruct_ws_rs164(oracle, k, m, blen, erased, data_only, variant):
     """The RS(16+4) rebuild-1..4 defaults (231: without the small-batch latency path
     that variant 0 takes at 11 blocks) run the warp-specialised kernel (asserted through
@@ -260,12 +247,13 @@ def test_fused_kernel_selected():
                                                   (8, 4, 8 * 640, [2, 10], True), (4, 2, 4 * 512, [1], True),
                                                   (16, 4, 16 * 256, [3, 17], False),
                                                   (16, 4, 16 * 256, [3, 17], True)])
-@pytest.mark.parametrize("variant", [0, 200, 201, 210, 211, 212])
+@pytest.mark.parametrize("variant", [0, 200, 420, 421])
 def test_verify_reconstruct_large_batch(oracle, k, m, blen, erased, heal, variant):
     """4096 stripes through the default launch (k_vr_ws where it applies), the
-    first-generation kernel (200), its one-workgroup-per-CU launch (201) and k_vr_ws
-    with one tile of prefetch (211); every stripe checked against the oracle, one
-    corrupt survivor flagged."""
+    first-generation kernel (200, any variant the product GET dispatch does not serve) and
+    the product shapes with the conflict-free LDS row stride (420) / the region-interleaved
+    workgroup order (421); every stripe checked against the oracle, one corrupt survivor
+    flagged."""
     nb = 4096
     R = k + m
     S = -(-blen // k)

@@ -2,7 +2,7 @@
 compiler does not track (inline asm, exact s_waitcnt vmcnt(N) by hand), so no
 instruction may touch a load's destination VGPRs before a wait retires it.  Compiles
 the device code to assembly and runs scripts/check_async_loads.py's dataflow check on
-every compiled k_ehx instance; a compiler change that copies or re-uses an in-flight
+every compiled k_ehx_ws / k_vr_ws instance; a compiler change that copies or re-uses an in-flight
 register fails here, before any GPU run."""
 import os
 import shutil
@@ -30,12 +30,8 @@ def test_untracked_loads_never_touched_in_flight(tmp_path, diag):
     import check_async_loads as cal
 
     # every translation unit that instantiates fused_v2.hpp's kernels, compiled in parallel
-    # fused_dma.hip (product and diagnostics) issues its loads with global_load_lds_*: the data
-    # goes straight to LDS, no VGPR is a load destination, so the VGPR dataflow check does not
-    # apply; it is compiled here for the SGPR-hazard check all the same.
-    units = ["fused_v2.hip", "fused_v2_gen.hip", "fused_v2_get.hip", "fused_v2_get_gen.hip", "fused_dma.hip"] + (
-        ["fused_v2_get_diag.hip", "fused_v2_get_diag4.hip", "fused_v2_get_diag8.hip", "fused_v2_get_diag16.hip",
-         "fused_v2_km84.hip", "fused_v2_km42.hip", "fused_v2_km164.hip", "fused_v2_km124.hip"] if diag else [])
+    units = ["fused_v2.hip", "fused_v2_gen.hip", "fused_v2_get.hip", "fused_v2_get_gen.hip"] + (
+        ["fused_v2_diag.hip"] if diag else [])
     procs = []
     for u in units:
         asm = tmp_path / (u + ".s")

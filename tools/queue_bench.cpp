@@ -4,7 +4,8 @@
 // synchronously (submit + wait per block, as EncodeData returns before the next block
 // is read).  Prints one JSON line per T: aggregate GiB/s of object bytes, per-block
 // latency p50 / p99, blocks per device batch.
-//   tools/queue_bench [T,T,...] [per] [k] [m] [max_batch] [slots] [pinned]
+//   tools/queue_bench [T,T,...] [per] [k] [m] [max_batch] [slots] [pinned] [devices]
+// devices: a comma list of HIP ordinals for a multi-device queue (e.g. 0,0 on one GPU).
 // pinned = 1: every caller's block buffer comes from zs3_host_alloc (the pinned bpool),
 // so the queue DMAs it zero-copy; 0 (default): pageable buffers, staged by memcpy.
 #include <algorithm>
@@ -35,7 +36,19 @@ int main(int argc, char** argv) {
     }
     const int per = argc > 2 ? std::atoi(argv[2]) : 32;
     const int k = argc > 3 ? std::atoi(argv[3]) : 8, m = argc > 4 ? std::atoi(argv[4]) : 4;
-    zs3_queue_opts o = {-1, argc > 5 ? std::atoi(argv[5]) : 0, 0, argc > 6 ? std::atoi(argv[6]) : 0};
+    zs3_queue_opts o = {-1, argc > 5 ? std::atoi(argv[5]) : 0, 0, argc > 6 ? std::atoi(argv[6]) : 0, nullptr, 0};
+    std::vector<int> devs;
+    if (argc > 8) {
+        std::string d = argv[8];
+        size_t p = 0;
+        while (p < d.size()) {
+            size_t q2 = d.find(',', p);
+            devs.push_back(std::atoi(d.substr(p, q2 - p).c_str()));
+            p = q2 == std::string::npos ? d.size() : q2 + 1;
+        }
+        o.devices = devs.data();
+        o.n_devices = (int)devs.size();
+    }
     const int64_t B = 1 << 20, S = (B + k - 1) / k, R = k + m;
     zs3_codec* c = nullptr;
     if (zs3_codec_new(k, m, B, &c) != ZS3_OK) return 2;
@@ -80,10 +93,10 @@ int main(int argc, char** argv) {
             for (auto& v : lat) all.insert(all.end(), v.begin(), v.end());
             std::sort(all.begin(), all.end());
             if (rep == 1)
-                std::printf("{\"path\": \"queue_encode_native\", \"pinned\": %s, \"k\": %d, \"m\": %d, \"threads\": %d, \"blocks\": %d, "
+                std::printf("{\"path\": \"queue_encode_native\", \"devices\": %d, \"pinned\": %s, \"k\": %d, \"m\": %d, \"threads\": %d, \"blocks\": %d, "
                             "\"GiBps\": %.2f, \"block_latency_us_p50\": %.1f, \"block_latency_us_p99\": %.1f, "
                             "\"blocks_per_batch\": %.1f, \"errors\": %d}\n",
-                            pinned ? "true" : "false", k, m, T, T * per, (double)T * per * B / dt / (1 << 30), all[all.size() / 2],
+                            std::max(1, o.n_devices), pinned ? "true" : "false", k, m, T, T * per, (double)T * per * B / dt / (1 << 30), all[all.size() / 2],
                             all[(size_t)(all.size() * 0.99)], (double)(n1 - n0) / std::max<int64_t>(1, b1 - b0),
                             errs.load());
             std::fflush(stdout);

@@ -55,9 +55,10 @@ EXPORTS = [
     "zs3_queue_new", "zs3_queue_free", "zs3_queue_submit_encode", "zs3_queue_submit_decode", "zs3_req_wait",
     "zs3_queue_flush", "zs3_queue_stats", "zs3_queue_zero_copy_blocks", "zs3_queue_encode_data", "zs3_queue_decode_data_blocks",
     "zs3_stream_encode_multi", "zs3_split_range", "zs3_md5_parts", "zs3_sha256_parts",
+    "zs3_queue_device_stats", "zs3_stream_decode",
 ]
 # include/zs3gpu_diag.h: exported by the diagnostics build only
-DIAG_EXPORTS = ["zs3_debug_set_variant", "zs3_debug_set_buffer"]
+DIAG_EXPORTS = ["zs3_debug_set_variant", "zs3_debug_set_buffer", "zs3_debug_encode_layout_ok"]
 
 
 class ZS3Error(Exception):
@@ -93,6 +94,8 @@ def diag_lib():
         _LD = _load(DIAG_LIB_PATH)
         _LD.zs3_debug_set_variant.argtypes = [C.c_int]
         _LD.zs3_debug_set_buffer.argtypes = [C.c_void_p]
+        i64 = C.c_int64
+        _LD.zs3_debug_encode_layout_ok.argtypes = [C.c_void_p, i64, i64, i64, C.c_void_p, i64, i64]
     return _LD
 
 
@@ -168,11 +171,14 @@ def _load(path):
     L.zs3_queue_stats.argtypes = [vp, C.POINTER(i64), C.POINTER(i64)]
     L.zs3_queue_zero_copy_blocks.argtypes = [vp]
     L.zs3_queue_zero_copy_blocks.restype = i64
+    L.zs3_queue_device_stats.argtypes = [vp, C.c_int, C.POINTER(C.c_int), C.POINTER(i64), C.POINTER(i64)]
     L.zs3_queue_encode_data.argtypes = [vp, vp, i64, i64, vp]
     L.zs3_queue_encode_data.restype = i64
     L.zs3_queue_decode_data_blocks.argtypes = [vp, vp, i64, vp, C.c_int, vp, vp]
     L.zs3_stream_encode_multi.argtypes = [vp, vp, C.c_int, vp, i64, vp, vp, i64]
     L.zs3_stream_encode_multi.restype = i64
+    L.zs3_stream_decode.argtypes = [vp, vp, i64, vp, C.c_int, vp, vp, vp, vp, i64]
+    L.zs3_stream_decode.restype = i64
     L.zs3_split_range.argtypes = [i64, C.c_int, C.c_int, C.POINTER(i64), C.POINTER(i64)]
     L.zs3_split_range.restype = None
     return L
@@ -180,7 +186,8 @@ def _load(path):
 
 class QueueOpts(C.Structure):
     """zs3_queue_opts (include/zs3gpu.h)."""
-    _fields_ = [("device", C.c_int), ("max_batch", C.c_int), ("max_wait_us", C.c_int), ("slots", C.c_int)]
+    _fields_ = [("device", C.c_int), ("max_batch", C.c_int), ("max_wait_us", C.c_int), ("slots", C.c_int),
+                ("devices", C.POINTER(C.c_int)), ("n_devices", C.c_int)]
 
 
 def _check(rc: int, what: str = "") -> int:
@@ -329,6 +336,24 @@ class Codec:
                                             addr(sums), batch_blocks)
         return _check(n, "stream_encode_multi")
 
+    def stream_decode(self, stripes, total_len: int, present, data_only: bool, expect=None, bad=None,
+                      sums_out=None, status=None, batch_blocks: int = 128) -> int:
+        """zs3_stream_decode: GET (data_only) / heal of a whole object's stripes in host
+        memory (numpy uint8 or HostBuffer), pipelined through the device.  `present` is an
+        (n_blocks, k+m) array; expect (n_blocks, k+m, 32) uint8, bad (n_blocks, k+m) int32,
+        sums_out (n_blocks, k+m, 32) uint8 and status (n_blocks,) int32 are optional numpy
+        arrays.  Returns the number of blocks or the first block's status (< 0)."""
+        import numpy as np
+
+        def addr(x):
+            if x is None:
+                return None
+            return x.ptr if isinstance(x, HostBuffer) else x.ctypes.data
+        pres = np.ascontiguousarray(np.asarray(present, dtype=bool).astype(np.uint8))
+        return int(self._L.zs3_stream_decode(self._h, addr(stripes), total_len, pres.ctypes.data,
+                                             1 if data_only else 0, addr(expect), addr(bad), addr(sums_out),
+                                             addr(status), batch_blocks))
+
     def decode_data_blocks(self, shards, present, data_only: bool) -> None:
         """Reconstruct in place on a (k+m, S) C-contiguous numpy uint8 array."""
         pres = (C.c_uint8 * (self.k + self.m))(*[1 if p else 0 for p in present])
@@ -341,11 +366,14 @@ class Queue:
     gathered into device batches.  Each call below blocks the calling thread only
     (ctypes releases the GIL), so N Python threads behave like N goroutines in cgo."""
 
-    def __init__(self, codec: Codec, device: int = -1, max_batch: int = 0, max_wait_us: int = 0, slots: int = 0):
+    def __init__(self, codec: Codec, device: int = -1, max_batch: int = 0, max_wait_us: int = 0, slots: int = 0,
+                 devices=None):
         self._L = codec._L
         self.codec = codec
         self.k, self.m = codec.k, codec.m
-        opts = QueueOpts(device, max_batch, max_wait_us, slots)
+        devs = list(devices) if devices else []
+        self._devs = (C.c_int * max(1, len(devs)))(*devs)
+        opts = QueueOpts(device, max_batch, max_wait_us, slots, self._devs if devs else None, len(devs))
         h = C.c_void_p()
         _check(self._L.zs3_queue_new(codec._h, C.byref(opts), C.byref(h)), "queue_new")
         self._h = h
@@ -405,6 +433,12 @@ class Queue:
         _check(self._L.zs3_queue_stats(self._h, C.byref(b), C.byref(n)))
         return b.value, n.value
 
+    def device_stats(self, index: int) -> tuple[int, int, int]:
+        """(device, batches, blocks) of the index-th listed device."""
+        d, b, n = C.c_int(0), C.c_int64(0), C.c_int64(0)
+        _check(self._L.zs3_queue_device_stats(self._h, index, C.byref(d), C.byref(b), C.byref(n)))
+        return d.value, b.value, n.value
+
     def zero_copy_blocks(self) -> int:
         """Blocks whose bytes were DMA'd straight from / to a pinned caller buffer."""
         return int(self._L.zs3_queue_zero_copy_blocks(self._h))
@@ -416,14 +450,15 @@ class HostBuffer:
     def __init__(self, nbytes: int):
         import numpy as np
         p = C.c_void_p()
-        _check(lib().zs3_host_alloc(C.byref(p), nbytes), "host_alloc")
+        self._L = lib()  # the library whose queues see this buffer as pinned
+        _check(self._L.zs3_host_alloc(C.byref(p), nbytes), "host_alloc")
         self.ptr = p.value
         self.nbytes = nbytes
         self.array = np.ctypeslib.as_array((C.c_uint8 * nbytes).from_address(self.ptr))
 
     def free(self):
         if self.ptr:
-            lib().zs3_host_free(self.ptr)
+            self._L.zs3_host_free(self.ptr)
             self.ptr = None
 
 

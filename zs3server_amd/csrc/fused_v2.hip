@@ -59,8 +59,7 @@ static int launch_ehx_default(const EncArgs& a, hipStream_t s) {
         // stride (TSP = 1: SQ_LDS_BANK_CONFLICT 20 % -> 0 % of LDS cycles), diagnostics 302:
         // 4.98 / 4.84 -> 4.79 ms on 16384 x 1 MiB pairs of runs (profiles/r04/r04_ab1.jsonl)
         if (n > 2048)
-            return launch_ws_t<K, M, 16, 384, 1, true, false, 0, false, 1, 0, false, 3, false, 0, 0, false, 3, 1>(a, s)
-                       ? PATH_WS : PATH_NONE;
+            return launch_ws<K, M, shape::Rs84Bulk>(a, s) ? PATH_WS : PATH_NONE;
         // up to 2048 stripes (round 3, variant 199): 4 stripes per workgroup, quad-form
         // hash waves (3) beside 4 encode waves, 1 KiB tiles, two tiles of prefetch, and
         // the 2-waves-per-SIMD register budget (7-wave workgroups: no spills, where the
@@ -68,12 +67,11 @@ static int launch_ehx_default(const EncArgs& a, hipStream_t s) {
         // 0.275 / 0.285 / 0.281 / 0.336 / 0.611 / 0.676 ms vs 0.32 / 0.42 / 0.47 / 0.555 /
         // 0.684 / 0.73-0.78 for the latency path, first-generation and 8-stripe kernels
         // (profiles/r03/ab_rs84_mid_batches.jsonl, sweep_rs84_sizes199.jsonl)
-        return launch_ws_t<K, M, 4, 1024, 2, false, true, 83968, false, 0, 0, false, 3, false, 0, 0, false, 2>(a, s)
-                   ? PATH_WS : PATH_NONE;
+        return launch_ws<K, M, shape::Rs84Mid>(a, s) ? PATH_WS : PATH_NONE;
     } else if constexpr (K == 16 && M == 4) {
         if (n > 4 * 256)
-            return launch_ws_t<K, M, 8, 384, 1, true, false, 0, false, 0, 0, false, 3, false, 2>(a, s) ? PATH_WS : PATH_NONE;
-        return launch_ws_t<K, M, 4, 512, 1, true, true, 0, false, 0, 0, false, 3>(a, s) ? PATH_WS : PATH_NONE;
+            return launch_ws<K, M, shape::Rs164Bulk>(a, s) ? PATH_WS : PATH_NONE;
+        return launch_ws<K, M, shape::Quad512>(a, s) ? PATH_WS : PATH_NONE;
     } else if constexpr (K == 12 && M == 4) {
         // RS(12+4), the 16-drive default (cmd/format-erasure.go:870-881), at shard sizes
         // that are multiples of 16; 1 MiB blocks (S = 87 382) take launch_ehx_ua.  Above
@@ -83,25 +81,24 @@ static int launch_ehx_default(const EncArgs& a, hipStream_t s) {
         // RS(16+4) shape it had (profiles/r04/abl_rs124_al.jsonl); 4 stripes with
         // quad-form hash waves up to 1024.
         if (n > 4 * 256)
-            return launch_ws_t<K, M, 8, 512, 1, true, false, 0, false, 0, 8, false, 3, false, 2, 2, true, 3, 1>(a, s)
-                       ? PATH_WS : PATH_NONE;
-        return launch_ws_t<K, M, 4, 512, 1, true, true, 0, false, 0, 0, false, 3>(a, s) ? PATH_WS : PATH_NONE;
+            return launch_ws<K, M, shape::Rs124AlignedBulk>(a, s) ? PATH_WS : PATH_NONE;
+        return launch_ws<K, M, shape::Quad512>(a, s) ? PATH_WS : PATH_NONE;
     } else if constexpr (K == 4 && M == 4) {
         // RS(4+4), the 8-drive default: the RS(8+4) shape (16 stripes, 16-byte columns,
         // pair-form hash waves) for large batches, the RS(4+2) config-2 shape (4 stripes,
         // quad-form hash waves, 4 tiles of prefetch) below.
         if (n > 8 * 256)
-            return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3>(a, s) ? PATH_WS : PATH_NONE;
-        return launch_ws_t<K, M, 4, 512, 4, false, true, 83968, false, 0, 0, false, 3>(a, s) ? PATH_WS : PATH_NONE;
+            return launch_ws<K, M, shape::PairG16>(a, s) ? PATH_WS : PATH_NONE;
+        return launch_ws<K, M, shape::QuadSmall<3>>(a, s) ? PATH_WS : PATH_NONE;
     } else if constexpr (K == 4 && M == 2) {
         // config 2 (1024 objects, 6 144 chains: the chain latency sets the pace): 2 KiB
         // tiles, so each chain runs 64 packets between barriers (0.397 -> 0.364 ms over
         // 512-byte tiles, profiles/r03/ab_config2_tiles.jsonl)
         if (n >= 1024 && n <= 8 * 256)
-            return launch_ws_t<K, M, 4, 2048, 2, false, true, 83968, false, 0, 0, false, 3>(a, s) ? PATH_WS : PATH_NONE;
+            return launch_ws<K, M, shape::Config2>(a, s) ? PATH_WS : PATH_NONE;
         if (n <= 8 * 256)
-            return launch_ws_t<K, M, 4, 512, 4, false, true, 83968, false, 0, 0, false, 2>(a, s) ? PATH_WS : PATH_NONE;
-        return launch_ws_t<K, M, 16, 384, 1, false, false, 0, false, 1, 0, false, 3>(a, s) ? PATH_WS : PATH_NONE;
+            return launch_ws<K, M, shape::QuadSmall<2>>(a, s) ? PATH_WS : PATH_NONE;
+        return launch_ws<K, M, shape::PairG16>(a, s) ? PATH_WS : PATH_NONE;
     }
     return PATH_NONE;
 }
@@ -121,29 +118,11 @@ int launch_ehx_ua(const EncArgs& a, hipStream_t s) {
         // budget): 1.41 -> 1.40 ms / 5.59 -> 5.56 ms at 4096 / 16384 x 1 MiB on the same
         // box, 1-2 % over two boxes (sweep_rs124_1k.jsonl, sweep_rs124_1k_b.jsonl)
         if (a.n_blocks > 4 * 256)
-            return launch_ws_t<12, 4, 4, 1024, 1, true, true, 0, false, 0, 16, false, 3, false, 2, 2, true, 2, 1>(a, s)
-                       ? PATH_WS : PATH_NONE;
-        return launch_ws_t<12, 4, 4, 512, 1, true, true, 0, false, 0, 0, false, 3, false, 0, 0, true>(a, s)
-                   ? PATH_WS : PATH_NONE;
+            return launch_ws<12, 4, shape::Rs124Ua1K>(a, s) ? PATH_WS : PATH_NONE;
+        return launch_ws<12, 4, shape::Rs124UaSmall>(a, s) ? PATH_WS : PATH_NONE;
     }
     return PATH_NONE;
 }
-
-#if ZS3_DIAG
-// RS(4+4) (the 8-drive default) encode + sums candidates above 2048 stripes (round 4):
-//  369: the RS(8+4) round-4 product recipe (buffer-addressed columns, conflict-free LDS
-//       stride TSP 1); 370: 4 stripes of 1 KiB tiles, quad-form hash waves issuing the L2
-//       prefetch, 16-byte columns (the RS(12+4) product shape); 371: 16 stripes of 512-byte
-//       tiles with the L2 prefetch (the RS(4+3) shape)
-static bool launch_ehx_km_4_4(int v, const EncArgs& a, hipStream_t s) {
-    switch (v) {
-        case 369: return launch_ws_t<4, 4, 16, 384, 1, true, false, 0, false, 1, 0, false, 3, false, 0, 0, false, 3, 1>(a, s);
-        case 370: return launch_ws_t<4, 4, 4, 1024, 1, true, true, 0, false, 0, 16, false, 3, false, 0, 2, false, 2, 1>(a, s);
-        case 371: return launch_ws_t<4, 4, 16, 512, 1, true, false, 0, false, 0, 16, false, 3, false, 0, 2, false, 3, 1>(a, s);
-        default: return false;
-    }
-}
-#endif
 
 int launch_ehx(int v, const EncArgs& a, hipStream_t s) {
     if (v == 0) {
@@ -155,14 +134,7 @@ int launch_ehx(int v, const EncArgs& a, hipStream_t s) {
         return PATH_NONE;
     }
 #if ZS3_DIAG
-    if (v == 190) return launch_ehx_dma(v, a, s);
-    bool ok = false;
-    if (a.k == 8 && a.m == 4) ok = launch_ehx_km_8_4(v, a, s);
-    if (a.k == 4 && a.m == 2) ok = launch_ehx_km_4_2(v, a, s);
-    if (a.k == 16 && a.m == 4) ok = launch_ehx_km_16_4(v, a, s);
-    if (a.k == 12 && a.m == 4) ok = launch_ehx_km_12_4(v, a, s);
-    if (a.k == 4 && a.m == 4) ok = launch_ehx_km_4_4(v, a, s);
-    if (ok) return ((v >= 100 && v < 200) || v >= 300) ? PATH_WS : PATH_PIPE;
+    if (launch_ehx_diag(v, a, s)) return PATH_WS;
 #endif
     return PATH_NONE;
 }

@@ -139,288 +139,6 @@ __device__ __forceinline__ Col<NWd> to_col(const typename VecOf<NWd>::type& v) {
 
 }  // namespace
 
-// K data rows, M parity rows (dyadic), G stripes per workgroup, CW-byte columns,
-// PF tiles of register prefetch, NBUF LDS tiles, NTS = non-temporal parity stores.
-// ABL (timing-only diagnostics): 1 = no hash, 2 = no GF arithmetic (parity = data
-// rows 0..M-1), 3 = neither.
-// PIPE: software-pipelined body, one basic block per step holding encode(tile i)
-// AND hash(tile i-1), so the scheduler fills the HighwayHash chain's dependent
-// latency with independent GF work (requires NBUF = 2).
-// PRIO: rotate s_setprio by (tile + workgroup) so co-resident workgroups of a CU
-// progress at equal rates (oldest-first issue otherwise lets the first workgroup of a
-// CU finish far ahead and leaves the CU under-occupied for the rest of the launch).
-template <int K, int M, int G, int CW, int PF, int NBUF, bool NTS, int ABL = 0, bool PIPE = false, bool PRIO = false>
-__global__ void __launch_bounds__(4 * G * (K + M)) __attribute__((amdgpu_waves_per_eu(3))) k_ehx(EncArgs a) {
-    constexpr int R = K + M;
-    constexpr int NT = 4 * G * R;
-    constexpr int NWd = CW / 4;
-    constexpr int CPB = NT / G;        // columns per stripe = threads per stripe
-    constexpr int T = CPB * CW;        // tile bytes per shard row
-    constexpr int TS = T + 32;         // +8 banks per row: conflict-free b64 row reads
-    constexpr int NPK = T / 32;
-    constexpr int NTAB = K * 8;
-    static_assert(M == 2 || M == 4, "dyadic shapes only");
-    // tile buffers in dynamic LDS (one workgroup may take up to 160 KiB)
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem_dyn[];
-    uint8_t(*tile)[G * R * TS] = reinterpret_cast<uint8_t(*)[G * R * TS]>(smem_dyn);
-    __shared__ __attribute__((aligned(16))) uint32_t tabs[NTAB];
-    auto set_prio = [&](int64_t ti) {
-        if constexpr (PRIO) {
-            const int q = (int)((ti + blockIdx.x) & 3);
-            if (q == 0) __builtin_amdgcn_s_setprio(0);
-            else if (q == 1) __builtin_amdgcn_s_setprio(1);
-            else if (q == 2) __builtin_amdgcn_s_setprio(2);
-            else __builtin_amdgcn_s_setprio(3);
-        }
-    };
-
-    const int tid = threadIdx.x;
-    const int64_t blk0 = (int64_t)blockIdx.x * G;
-    const int64_t S = a.S;
-    for (int i = tid; i < NTAB; i += NT) tabs[i] = a.dtables[i];
-
-    // hash role: lane `lane` of shard row `chain` (stripe chain / R)
-    const int chain = tid >> 2, lane = tid & 3;
-    const bool chain_live = blk0 + chain / R < a.n_blocks;
-    const uint32_t sel = zipper_sel(lane);
-    HHLane st = hh_init(lane, a.key[0], a.key[1], a.key[2], a.key[3]);
-
-    // encode role: column o of stripe g (dead stripes of the last workgroup alias
-    // the last live block and store byte-identical parity)
-    const int g = tid / CPB, o = (tid % CPB) * CW;
-    const int64_t b = (blk0 + g) < a.n_blocks ? (blk0 + g) : (a.n_blocks - 1);
-    const uint8_t* src = a.data + b * a.data_stride + o;
-    uint8_t* pdst = a.parity + b * a.parity_stride + o;
-    const int col_off = g * R * TS + o;
-    const int row_off = chain * TS + 8 * lane;
-
-    const int64_t nfull = S / T;
-    const int tail = (int)(S - nfull * T);
-
-    // Diagnostics (a.dbg set): per-wave start/end real time, shader clocks, HW_ID and
-    // XCC_ID, to see load balance across CUs/XCDs and the in-kernel clock.
-    uint64_t rt0 = 0, ct0 = 0;
-    if (a.dbg) {
-        rt0 = __builtin_amdgcn_s_memrealtime();
-        ct0 = __builtin_amdgcn_s_memtime();
-    }
-
-    typedef typename VecOf<NWd>::type VT;
-    VT x[PF][K];
-    auto load = [&](VT (&xs)[K], int64_t t0) {
-#pragma unroll
-        for (int j = 0; j < K; ++j) ld_async<NWd>(xs[j], src + (int64_t)j * S + t0);
-    };
-    auto load_tail = [&](VT (&xs)[K], int64_t t0) {
-        if (o < tail) {
-#pragma unroll
-            for (int j = 0; j < K; ++j) ld_async<NWd>(xs[j], src + (int64_t)j * S + t0);
-        } else {
-#pragma unroll
-            for (int j = 0; j < K; ++j) xs[j] = VT{};
-        }
-    };
-    // encode tile into LDS buffer `tl`, then issue the loads of tile `t_next`
-    // into the same registers, then store parity of tile t0.
-    auto encode = [&](VT (&xr)[K], uint8_t* tl, Col<NWd> (&par)[M]) {
-        Col<NWd> xs[K];
-#pragma unroll
-        for (int j = 0; j < K; ++j) xs[j] = to_col<NWd>(xr[j]);
-        if constexpr (ABL & 2) {
-#pragma unroll
-            for (int r = 0; r < M; ++r)
-#pragma unroll
-                for (int w = 0; w < NWd; ++w) par[r].w[w] = xs[r].w[w] ^ xs[r + M].w[w];
-        } else {
-            encode_dyadic<NWd, K, M, !PIPE>(xs, par, tabs);
-        }
-#pragma unroll
-        for (int j = 0; j < K; ++j) st_col<NWd>(tl + col_off + j * TS, xs[j]);
-#pragma unroll
-        for (int r = 0; r < M; ++r) st_col<NWd>(tl + col_off + (K + r) * TS, par[r]);
-    };
-    auto store_par = [&](const Col<NWd> (&par)[M], int64_t t0) {
-#pragma unroll
-        for (int r = 0; r < M; ++r) {
-            if (NTS)
-                st_col_nt<NWd>(pdst + (int64_t)r * S + t0, par[r]);
-            else
-                st_col<NWd>(pdst + (int64_t)r * S + t0, par[r]);
-        }
-    };
-    auto hash_full = [&](const uint8_t* tl) {
-        const uint64_t* p = reinterpret_cast<const uint64_t*>(tl + row_off);
-        uint64_t w[NPK];
-#pragma unroll
-        for (int i = 0; i < NPK; ++i) w[i] = p[4 * i];
-#pragma unroll
-        for (int i = 0; i < NPK; ++i) {
-            if constexpr (ABL & 1)
-                st.v0 ^= w[i];
-            else
-                hh_update(st, w[i], sel);
-        }
-    };
-    // Branch-free prefetch for the edge steps: a tile past the end (or a tail column
-    // past the tail) re-reads tile 0 of its own row, so x is defined on every path (no
-    // phi copies of in-flight registers) and the value is unused.
-    auto prefetch_any = [&](VT (&xs)[K], int64_t tn) {
-        const bool ok = tn < nfull || (tn == nfull && o < tail);
-        load(xs, ok ? tn * T : 0);
-    };
-    // Steady-state step on full tile ti held in xs (tile ti+PF known full): encode
-    // into LDS, issue the loads of tile ti+PF into the freed registers, then the
-    // parity stores, barrier, hash.
-    // Before encode(ti) the wave's pending vector-memory ops are, oldest first:
-    // loads(ti), stores(ti-PF), loads(ti+1), stores(ti-PF+1), ..., loads(ti+PF-1),
-    // stores(ti-1).  Steady state waits for loads(ti) only: vmcnt(M + (PF-1)*(K+M)).
-    // Edge steps (below) wait for everything.
-    auto step = [&](VT (&xs)[K], int64_t ti) {
-        set_prio(ti);
-        uint8_t* tl = tile[NBUF == 1 ? 0 : (ti & 1)];
-        Col<NWd> par[M];
-        vm_wait<M + (PF - 1) * (K + M)>(xs);
-        encode(xs, tl, par);
-        load(xs, (ti + PF) * T);
-        store_par(par, ti * T);
-        lds_barrier2();
-        hash_full(tl);
-        if (NBUF == 1) lds_barrier2();
-    };
-
-    if constexpr (PIPE) {
-        static_assert(NBUF == 2, "pipelined body double-buffers the LDS tile");
-        // Step ti: hash tile ti-1 (buffer (ti-1)&1, written before the last barrier)
-        // and encode tile ti into buffer ti&1 (last read by hash(ti-2), which every
-        // wave finished before the last barrier); one barrier per step.
-        auto hash_words = [&](const uint8_t* tl, uint64_t (&w)[NPK]) {
-            const uint64_t* p = reinterpret_cast<const uint64_t*>(tl + row_off);
-#pragma unroll
-            for (int i2 = 0; i2 < NPK; ++i2) w[i2] = p[4 * i2];
-        };
-        auto hash_apply = [&](const uint64_t (&w)[NPK]) {
-#pragma unroll
-            for (int i2 = 0; i2 < NPK; ++i2) {
-                if constexpr (ABL & 1)
-                    st.v0 ^= w[i2];
-                else
-                    hh_update(st, w[i2], sel);
-            }
-        };
-        // steady state: full tile ti (>= 1) encoded, tile ti+PF known full
-        auto steady = [&](VT (&xs)[K], int64_t ti) {
-            set_prio(ti);
-            uint64_t w[NPK];
-            hash_words(tile[(ti - 1) & 1], w);
-            vm_wait<M + (PF - 1) * (K + M)>(xs);
-            Col<NWd> par[M];
-            encode(xs, tile[ti & 1], par);
-            load(xs, (ti + PF) * T);
-            store_par(par, ti * T);
-            hash_apply(w);
-            lds_barrier2();
-        };
-        // any step ti >= 0: hash tile ti-1 if it is a full tile, encode tile ti if it
-        // exists (full or tail); always prefetch tile ti+PF and hit the barrier.
-        auto edge = [&](VT (&xs)[K], int64_t ti) {
-            uint64_t w[NPK];
-            const bool do_hash = ti >= 1 && ti <= nfull;
-            if (do_hash) hash_words(tile[(ti - 1) & 1], w);
-            vm_wait<0>(xs);
-            if (ti < nfull || (ti == nfull && tail)) {
-                Col<NWd> par[M];
-                encode(xs, tile[ti & 1], par);
-                if (ti < nfull || o < tail) store_par(par, ti * T);
-            }
-            prefetch_any(xs, ti + PF);
-            if (do_hash) hash_apply(w);
-            lds_barrier2();
-        };
-        lds_barrier2();  // tables visible
-#pragma unroll
-        for (int p = 0; p < PF; ++p) prefetch_any(x[p], p);
-#pragma unroll
-        for (int p = 0; p < PF; ++p) edge(x[p], p);
-        int64_t i = PF;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        for (; i + 2 * PF <= nfull; i += PF) {
-#pragma unroll
-            for (int p = 0; p < PF; ++p) steady(x[p], i + p);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-        for (int p = 0; p < 2 * PF; ++p) edge(x[p % PF], i + p);
-        if (tail) {
-            const uint8_t* row = tile[nfull & 1] + chain * TS;
-            hh_packets(st, row, tail >> 5, lane, sel);
-            if (tail & 31) hh_remainder(st, row + (tail & ~31), (uint32_t)(tail & 31), lane, sel);
-        }
-    } else {
-        // Any step ti >= 0 outside the steady state: encode tile ti if it exists (full
-        // or tail), always prefetch tile ti+PF (branch-free), barrier, hash what was
-        // encoded.  Every wave runs every edge step, so barriers stay matched.
-        auto edge = [&](VT (&xs)[K], int64_t ti) {
-            uint8_t* tl = tile[NBUF == 1 ? 0 : (ti & 1)];
-            const bool full = ti < nfull, part = ti == nfull && tail;
-            vm_wait<0>(xs);
-            Col<NWd> par[M];
-            if (full || part) encode(xs, tl, par);
-            prefetch_any(xs, ti + PF);
-            if (full || (part && o < tail)) store_par(par, ti * T);
-            lds_barrier2();
-            if (full) {
-                hash_full(tl);
-            } else if (part) {
-                const uint8_t* row = tl + chain * TS;
-                hh_packets(st, row, tail >> 5, lane, sel);
-                if (tail & 31) hh_remainder(st, row + (tail & ~31), (uint32_t)(tail & 31), lane, sel);
-            }
-            if (NBUF == 1) lds_barrier2();
-        };
-        lds_barrier2();  // tables visible
-    #pragma unroll
-        for (int p = 0; p < PF; ++p) prefetch_any(x[p], p);
-    #pragma unroll
-        for (int p = 0; p < PF; ++p) edge(x[p], p);
-        int64_t i = PF;
-        // Drain once before the steady state and once after it: the in-loop vmcnt counts
-        // then only have to hold for the loop's own issue order (and
-        // scripts/check_async_loads.py can prove it without path-sensitive reasoning).
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        for (; i + 2 * PF <= nfull; i += PF) {
-    #pragma unroll
-            for (int p = 0; p < PF; ++p) step(x[p], i + p);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    #pragma unroll
-        for (int p = 0; p < 2 * PF; ++p) edge(x[p % PF], i + p);
-
-    }
-
-    // Keep every prefetch register allocated until all loads have retired: a load
-    // whose value turns out unused must not have its destination handed to other code
-    // while it is still in flight.
-#pragma unroll
-    for (int p = 0; p < PF; ++p) vm_wait<0>(x[p]);
-
-    const uint64_t h = hh_finalize256(st, lane, sel);
-    if (chain_live) {
-        const int64_t bb = blk0 + chain / R;
-        const int s = chain % R;
-        *reinterpret_cast<uint64_t*>(a.sums + (bb * R + s) * 32 + 8 * lane) = h;
-    }
-    if (a.dbg && (tid & 63) == 0) {
-        const uint64_t rt1 = __builtin_amdgcn_s_memrealtime();
-        const uint64_t ct1 = __builtin_amdgcn_s_memtime();
-        uint64_t* d = a.dbg + ((int64_t)blockIdx.x * (NT / 64) + (tid >> 6)) * 5;
-        d[0] = rt0;
-        d[1] = rt1;
-        d[2] = ct1 - ct0;
-        d[3] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
-        d[4] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
-    }
-}
-
 // Warp-specialised form (one workgroup per CU, G stripes): the first NH = 2*G*R threads
 // only hash, one HighwayHash chain per thread PAIR (hh256_dev.hpp pair form: no DPP and
 // a shared zipper v_perm, 16 instead of 19 VALU per lane-packet); the other NE threads
@@ -460,6 +178,46 @@ constexpr int ws_cwe() {
 template <int T, bool HQ, int TSP>
 constexpr int ws_ts() {
     return TSP ? T + (T % 64 == 0 ? 32 : 0) : (HQ ? T + 32 : T + 16);
+}
+
+// ---- Named kernel shapes ------------------------------------------------------------
+// Every compile-time knob of k_ehx_ws with its default.  A shape derives from EncShape
+// and overrides what it changes, so a launch site names its shape
+// (launch_ws<8, 4, shape::Rs84Bulk>) instead of passing 19 positional template
+// arguments, and rocprof reports the kernel by that name.  The knobs are described below.
+struct EncShape {
+    static constexpr int G = 0;          // stripes per workgroup (every shape sets it)
+    static constexpr int T = 0;          // tile: bytes of each shard row per step (every shape sets it)
+    static constexpr int PF = 1;         // tiles of register prefetch in the encode role
+    static constexpr bool BUF = false;   // buffer-resource addressing of the encode columns
+    static constexpr bool HQ = false;    // quad-form hash waves (else pair form)
+    static constexpr int LDSMIN = 0;     // dynamic-LDS floor (bounds workgroups per CU)
+    static constexpr bool WT = false;    // diagnostics: barrier / load-wait cycle stamps
+    static constexpr int PM = 0;         // issue-priority scheme
+    static constexpr int CWX = 0;        // encode column width (0 = ws_cwe's default)
+    static constexpr bool RING = false;  // LDS counters instead of the per-step barrier
+    static constexpr int NTM = 0;        // non-temporal policy: bit 0 data loads, bit 1 parity stores
+    static constexpr bool STB = false;   // scalar coefficient tables in the encode role
+    static constexpr int EP = 0;         // encode-role order (2 = data rows to LDS first)
+    static constexpr int PFD = 0;        // L2 prefetch distance of the hash waves, in tiles
+    static constexpr bool UA = false;    // unaligned shard sizes
+    static constexpr int WPE = 3;        // waves per SIMD the register budget is sized for
+    static constexpr int TSP = 0;        // LDS row stride rule (ws_ts)
+    static constexpr int ABL = 0;        // diagnostics timing ablations (output differs)
+    static constexpr bool GEN = false;   // general M x K coding matrix (not dyadic)
+    static constexpr int XMAP = 0;       // workgroup -> stripe-group order (ws_group)
+};
+
+// workgroup -> stripe group (XMAP above k_ehx_ws); a bijection on [0, gridDim.x)
+template <int P>
+__device__ __forceinline__ int64_t ws_group() {
+    if constexpr (P <= 1) {
+        return blockIdx.x;
+    } else {
+        const uint32_t w = blockIdx.x, q = gridDim.x / P;
+        if (w >= q * P) return w;  // the last gridDim.x % P workgroups keep their place
+        return (int64_t)(w % P) * q + w / P;
+    }
 }
 
 // WT (diagnostic): per-wave shader cycles spent waiting at barriers, into the dbg stamps.
@@ -502,11 +260,17 @@ constexpr int ws_ts() {
 // TSP: LDS row stride rule (ws_ts).  ABL (timing-only diagnostics, output differs):
 // bit 0 = the pair-form hash waves XOR the words instead of running HighwayHash; bit 1 =
 // they skip their LDS reads; bit 2 = the encode waves skip their LDS writes.
-template <int K, int M, int G, int T, int PF, bool BUF = false, bool HQ = false, bool WT = false, int PM = 0,
-          int CWX = 0, bool RING = false, int NTM = 0, bool STB = false, int EP = 0, int PFD = 0, bool UA = false,
-          int WPE = 3, int TSP = 0, int ABL = 0, bool GEN = false>
-__global__ void __launch_bounds__((ws_nh<K, M, G, T, HQ>() + G * (T / ws_cwe<K, CWX>()))) __attribute__((amdgpu_waves_per_eu(WPE)))
-k_ehx_ws(EncArgs a) {
+// XMAP (round 5): workgroup -> stripe-group order.  0: workgroup w encodes stripes
+// [w*G, w*G+G).  P > 1: the grid is cut into P equal regions and consecutive workgroups
+// alternate between them (w -> region w % P, position w / P), so the workgroups resident
+// at one time stream from P places of the batch at once instead of one contiguous window
+// (with P = 8 = XCDs and the round-robin dispatch, each XCD walks its own eighth).
+template <int K, int M, class C>
+__global__ void __launch_bounds__((ws_nh<K, M, C::G, C::T, C::HQ>() + C::G * (C::T / ws_cwe<K, C::CWX>())))
+__attribute__((amdgpu_waves_per_eu(C::WPE))) k_ehx_ws(EncArgs a) {
+    constexpr int G = C::G, T = C::T, PF = C::PF, PM = C::PM, CWX = C::CWX, NTM = C::NTM, EP = C::EP, PFD = C::PFD,
+                  TSP = C::TSP, ABL = C::ABL;
+    constexpr bool BUF = C::BUF, HQ = C::HQ, WT = C::WT, RING = C::RING, STB = C::STB, UA = C::UA, GEN = C::GEN;
     constexpr int R = K + M;
     constexpr int NH = ws_nh<K, M, G, T, HQ>();  // hash threads
     constexpr int CWE = ws_cwe<K, CWX>();
@@ -527,7 +291,7 @@ k_ehx_ws(EncArgs a) {
     constexpr uint32_t NEW = (uint32_t)(NT - NH) / 64, NHW = (uint32_t)NH / 64;
 
     const int tid = threadIdx.x;
-    const int64_t blk0 = (int64_t)blockIdx.x * G;
+    const int64_t blk0 = (int64_t)ws_group<C::XMAP>() * G;
     const int64_t S = a.S;
     for (int i = tid; i < NTAB; i += NT) tabs[i] = GEN ? a.tables[i] : a.dtables[i];
     if (RING && tid < 4) ring[tid] = 0;
@@ -1009,56 +773,30 @@ k_ehx_ws(EncArgs a) {
     stamp();
 }
 
-template <int K, int M, int G, int T, int PF, bool BUF = false, bool HQ = false, int LDSMIN = 0, bool WT = false,
-          int PM = 0, int CWX = 0, bool RING = false, int NTM = 0, bool STB = false, int EP = 0, int PFD = 0,
-          bool UA = false, int WPE = 3, int TSP = 0, int ABL = 0, bool GEN = false>
-static bool launch_ws_t(const EncArgs& a, hipStream_t s) {
+template <int K, int M, class C>
+static bool launch_ws(const EncArgs& a, hipStream_t s) {
+    constexpr int G = C::G, T = C::T;
     constexpr int R = K + M;
-    constexpr int NT = ws_nh<K, M, G, T, HQ>() + G * (T / ws_cwe<K, CWX>());
-    constexpr size_t tiles = (size_t)2 * G * R * ws_ts<T, HQ, TSP>();
-    constexpr size_t dyn = tiles > (size_t)LDSMIN ? tiles : (size_t)LDSMIN;
-    if constexpr (dyn + (GEN ? M * K : K) * 32 > 163840 || NT > 1024) {
+    constexpr int NT = ws_nh<K, M, G, T, C::HQ>() + G * (T / ws_cwe<K, C::CWX>());
+    constexpr size_t tiles = (size_t)2 * G * R * ws_ts<T, C::HQ, C::TSP>();
+    constexpr size_t dyn = tiles > (size_t)C::LDSMIN ? tiles : (size_t)C::LDSMIN;
+    static_assert(G > 0 && T > 0, "a shape names its stripes per workgroup and tile length");
+    if constexpr (dyn + (C::GEN ? M * K : K) * 32 > 163840 || NT > 1024) {
         return false;
     } else {
-        if (!GEN && a.dyb != M) return false;
+        if (!C::GEN && a.dyb != M) return false;
         if (a.k != K || a.m != M) return false;
-        if constexpr (UA) {
+        if constexpr (C::UA) {
             // the Split padding (n .. k*S) must lie in the last data row's tail tile
             const int64_t tail = a.S % T;
             if ((int64_t)K * a.S - a.n > tail || a.n <= (int64_t)(K - 1) * a.S) return false;
         } else {
             if ((a.S % 16) != 0 || a.n != (int64_t)K * a.S) return false;
         }
-        if (BUF && ((G - 1) * a.data_stride + K * a.S > 0x7FFFFFFF ||
-                    (G - 1) * a.parity_stride + M * a.S > 0x7FFFFFFF || a.data_stride < 0 || a.parity_stride < 0))
+        if (C::BUF && ((G - 1) * a.data_stride + K * a.S > 0x7FFFFFFF ||
+                       (G - 1) * a.parity_stride + M * a.S > 0x7FFFFFFF || a.data_stride < 0 || a.parity_stride < 0))
             return false;
-        auto kern = k_ehx_ws<K, M, G, T, PF, BUF, HQ, WT, PM, CWX, RING, NTM, STB, EP, PFD, UA, WPE, TSP, ABL, GEN>;
-        if (ensure_dyn_lds((const void*)kern, dyn) != hipSuccess) return false;
-        const int64_t grid = (a.n_blocks + G - 1) / G;
-        hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), dyn, s, a);
-        return true;
-    }
-}
-
-// GM multiplies the minimal stripe count per workgroup (GM = 4 on RS(8+4): 16 stripes,
-// 12 waves, one workgroup per CU, all of a CU's waves in one barrier domain).
-// LDSMIN pads the dynamic LDS so that at most 163840 / LDSMIN workgroups share a CU.
-template <int K, int M, int CW, int PF, int NBUF, bool NTS = false, int ABL = 0, bool PIPE = false,
-          int GM = 1, bool PRIO = false, int LDSMIN = 0>
-static bool launch_ehx_t(const EncArgs& a, hipStream_t s) {
-    constexpr int R = K + M;
-    // G: smallest number of stripes making 4*G*R a multiple of 64 (whole wavefronts)
-    constexpr int G0 = (R % 16 == 0) ? 1 : (R % 8 == 0) ? 2 : (R % 4 == 0) ? 4 : (R % 2 == 0) ? 8 : 16;
-    constexpr int G = G0 * GM;
-    constexpr int NT = 4 * G * R;
-    constexpr int T = (NT / G) * CW;
-    constexpr size_t tiles = (size_t)NBUF * G * R * (T + 32);
-    constexpr size_t dyn = tiles > (size_t)LDSMIN ? tiles : (size_t)LDSMIN;
-    if constexpr (dyn + K * 32 > 163840 || NT > 1024) {
-        return false;
-    } else {
-        if (a.dyb != M) return false;
-        auto kern = k_ehx<K, M, G, CW, PF, NBUF, NTS, ABL, PIPE, PRIO>;
+        auto kern = k_ehx_ws<K, M, C>;
         if (ensure_dyn_lds((const void*)kern, dyn) != hipSuccess) return false;
         const int64_t grid = (a.n_blocks + G - 1) / G;
         hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), dyn, s, a);
@@ -1105,16 +843,42 @@ constexpr int vr_nh() {
 // PFD (round 4): as in k_ehx_ws, the hash waves touch every 128-byte line of the survivor
 // rows of tile s+PFD while hashing tile s-1 (one untracked global_load_dword per line,
 // result discarded), so the rebuild waves' survivor loads hit L2.
-template <int K, int EX, bool HOUT, int G, int T, int PF, int CW = 16, bool HQ = false, bool ST = false,
-          int BT = 0, bool NTL = false, bool UA = false, bool BUF = false, int PFD = 0>
-__global__ void __launch_bounds__((vr_nh<G, K + (HOUT ? EX : 0), HQ>() + G * (T / CW))) __attribute__((amdgpu_waves_per_eu(2)))
-k_vr_ws(VrArgs a) {
+// TSP (round 5): LDS row stride rule, as k_ehx_ws (ws_ts; 0 = the round-1 padding).
+// XMAP (round 5): workgroup -> stripe-group order, as k_ehx_ws (ws_group).
+struct GetShape {
+    static constexpr int G = 0;          // stripes per workgroup (every shape sets it)
+    static constexpr int T = 0;          // tile: bytes of each row per step (every shape sets it)
+    static constexpr int PF = 1;         // tiles of survivor prefetch in the rebuild role
+    static constexpr int CW = 16;        // rebuild column width, bytes
+    static constexpr bool HQ = false;    // quad-form hash waves
+    static constexpr bool ST = false;    // scalar coefficient tables
+    static constexpr int BT = 0;         // scalar tables per batch (0 = one per wait)
+    static constexpr bool NTL = false;   // non-temporal survivor loads / rebuilt stores (set by the launch)
+    static constexpr bool UA = false;    // unaligned shard sizes allowed
+    static constexpr bool BUF = false;   // buffer addressing (requested; the launch decides)
+    static constexpr int PFD = 0;        // L2 prefetch distance of the hash waves
+    static constexpr int TSP = 0;        // LDS row stride rule
+    static constexpr int XMAP = 0;       // workgroup -> stripe-group order
+};
+// The instance a launch picks for a requested shape: its memory policy (non-temporal,
+// buffer-addressed) fixed by the batch (launch_vr_ws_t).
+template <class C, bool NTL_, bool BUF_>
+struct VrMem : C {
+    static constexpr bool NTL = NTL_;
+    static constexpr bool BUF = BUF_;
+};
+
+template <int K, int EX, bool HOUT, class C>
+__global__ void __launch_bounds__((vr_nh<C::G, K + (HOUT ? EX : 0), C::HQ>() + C::G * (C::T / C::CW)))
+__attribute__((amdgpu_waves_per_eu(2))) k_vr_ws(VrArgs a) {
+    constexpr int G = C::G, T = C::T, PF = C::PF, CW = C::CW, BT = C::BT, PFD = C::PFD;
+    constexpr bool HQ = C::HQ, ST = C::ST, NTL = C::NTL, UA = C::UA, BUF = C::BUF;
     constexpr int RH = K + (HOUT ? EX : 0);
     constexpr int NH = vr_nh<G, RH, HQ>();
     constexpr int CPS = T / CW;
     constexpr int NE = G * CPS;
     constexpr int NT = NH + NE;
-    constexpr int TS = HQ ? T + 32 : T + 16;
+    constexpr int TS = ws_ts<T, HQ, C::TSP>();
     constexpr int NPK = T / 32;
     constexpr int NTAB = (EX > 0 ? EX : 1) * K * 8;
     static_assert(NH % 64 == 0 && NE % 64 == 0 && T % 32 == 0, "whole wavefronts per role");
@@ -1124,7 +888,7 @@ k_vr_ws(VrArgs a) {
     __shared__ int32_t srows[K + EX];
 
     const int tid = threadIdx.x;
-    const int64_t blk0 = (int64_t)blockIdx.x * G;
+    const int64_t blk0 = (int64_t)ws_group<C::XMAP>() * G;
     const int64_t S = a.S;
     const int R = a.k + a.m;
     if (EX > 0)
@@ -1490,60 +1254,81 @@ k_vr_ws(VrArgs a) {
     for (int p = 0; p < PF; ++p) vm_wait<0>(x[p]);
 }
 
-template <int K, int EX, bool HOUT, int G, int T, int PF, int CW, bool HQ, bool ST, int BT, bool NTL = false,
-          bool UA = false, bool BUF = false, int PFD = 0>
-static bool launch_vr_ws_bt(const VrArgs& a, hipStream_t s);
+template <int K, int EX, bool HOUT, class C>
+static bool launch_vr_inst(const VrArgs& a, hipStream_t s);
 
-template <int K, int EX, bool HOUT, int G, int T, int PF, int CW = 16, bool HQ = false, bool ST = false,
-          int BT = 0, bool UA = false, bool BUF = false, int PFD = 0>
+// Shape modifiers (diagnostics A/B of a product shape): the conflict-free LDS row stride,
+// the region-interleaved workgroup order.
+template <class C>
+struct Tsp1 : C {
+    static constexpr int TSP = 1;
+};
+template <class C, int P>
+struct XMap : C {
+    static constexpr int XMAP = P;
+};
+// C itself when P == 0 (product instances keep their shape's name)
+template <class C, int P>
+using WithXMap = std::conditional_t<P == 0, C, XMap<C, P>>;
+
+// Launch a requested GET shape: the instance's memory policy follows the batch.
+template <int K, int EX, bool HOUT, class C>
 static bool launch_vr_ws_t(const VrArgs& a, hipStream_t s) {
-    if constexpr (BUF && !UA) {
+#if ZS3_DIAG
+    // diagnostics 420: the same shape with the conflict-free LDS row stride (ws_ts TSP 1;
+    // pair-form shapes of k = 8 / 12 / 16: for the quad form at T % 64 == 0 both rules
+    // give T + 32); 421: with the region-interleaved workgroup order (ws_group, 8 regions;
+    // k = 8 / 16).  Instantiated for those k only: every modifier multiplies the
+    // diagnostics library by the product GET instances.
+    if constexpr (C::TSP == 0 && !C::HQ && (K == 8 || K == 12 || K == 16)) {
+        if (a.variant == 420) return launch_vr_ws_t<K, EX, HOUT, Tsp1<C>>(a, s);
+    }
+    if constexpr (C::XMAP == 0 && C::TSP == 0 && (K == 8 || K == 16)) {
+        if (a.variant == 421) return launch_vr_ws_t<K, EX, HOUT, XMap<C, 8>>(a, s);
+    }
+#endif
+    if constexpr (C::BUF && !C::UA) {
         // buffer addressing needs the G stripes of a workgroup in order (no id list) and
         // their span below 2^31 bytes; otherwise the 64-bit-address instance (diagnostics
         // 247: always that one)
-        if (!a.ids && (int64_t)G * a.block_stride < ((int64_t)1 << 31) && a.block_stride > 0 &&
-            !(ZS3_DIAG && a.variant == 247))
-            return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, BT, true, false, true, PFD>(a, s);
-        return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, BT, true, false, false, PFD>(a, s);
+        if (!a.ids && (int64_t)C::G * a.block_stride < ((int64_t)1 << 31) && a.block_stride > 0 &&
+            !(ZS3_DIAG && a.variant == 247 && C::TSP == 0 && C::XMAP == 0))
+            return launch_vr_inst<K, EX, HOUT, VrMem<C, true, true>>(a, s);
+        return launch_vr_inst<K, EX, HOUT, VrMem<C, true, false>>(a, s);
     }
-    if constexpr (UA) {
+    if constexpr (C::UA) {
         // plain (temporal) survivor loads: with unaligned rows each tile's first and last
         // 128-byte lines are shared with the neighbouring tiles, and non-temporal loads
         // fetched them twice (RS(12+4) rebuild 2: HBM traffic 1.205 x algorithmic,
         // profiles/r03/final_session3/bench_paths_roofline.jsonl)
-        return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, BT, false, true, false, PFD>(a, s);
+        return launch_vr_inst<K, EX, HOUT, VrMem<C, false, false>>(a, s);
     } else {
-        // diagnostics 240: the same launch with the scalar-table batching flipped (off <-> 4
-        // coefficients per batch); 241: batches of 2
-        if constexpr (ZS3_DIAG && ST) {
-            if (a.variant == 240) return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, (BT ? 0 : 4), true>(a, s);
-            if (a.variant == 241) return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, 2, true>(a, s);
-        }
         // Survivor loads and rebuilt-row stores are non-temporal (each byte is touched once):
         // RS(8+4) verify 0.706 -> 0.627 ms, RS(16+4) verify 0.386 -> 0.351, rebuild 1-4 and
         // heals 1-5 % faster (profiles/r02/ab_get_nt.jsonl).  Diagnostics 246: plain loads.
-        if constexpr (ZS3_DIAG) {
-            if (a.variant == 246) return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, BT, false>(a, s);
+        if constexpr (ZS3_DIAG && (K == 8 || K == 16) && C::TSP == 0 && C::XMAP == 0) {
+            if (a.variant == 246) return launch_vr_inst<K, EX, HOUT, VrMem<C, false, false>>(a, s);
         }
-        return launch_vr_ws_bt<K, EX, HOUT, G, T, PF, CW, HQ, ST, BT, true, false, false, PFD>(a, s);
+        return launch_vr_inst<K, EX, HOUT, VrMem<C, true, false>>(a, s);
     }
 }
 
-template <int K, int EX, bool HOUT, int G, int T, int PF, int CW, bool HQ, bool ST, int BT, bool NTL, bool UA, bool BUF,
-          int PFD>
-static bool launch_vr_ws_bt(const VrArgs& a, hipStream_t s) {
+template <int K, int EX, bool HOUT, class C>
+static bool launch_vr_inst(const VrArgs& a, hipStream_t s) {
+    constexpr int G = C::G, T = C::T, CW = C::CW;
     constexpr int RH = K + (HOUT ? EX : 0);
-    constexpr int NT = vr_nh<G, RH, HQ>() + G * (T / CW);
-    constexpr size_t tiles = (size_t)2 * G * RH * (HQ ? T + 32 : T + 16);
+    constexpr int NT = vr_nh<G, RH, C::HQ>() + G * (T / CW);
+    constexpr size_t tiles = (size_t)2 * G * RH * ws_ts<T, C::HQ, C::TSP>();
     constexpr size_t dyn = tiles > 83968 ? tiles : 83968;  // one workgroup per CU
+    static_assert(G > 0 && T > 0, "a shape names its stripes per workgroup and tile length");
     if constexpr (dyn + (size_t)(EX > 0 ? EX : 1) * K * 32 + 4 * (K + EX) > 163840 || NT > 1024 ||
-                  vr_nh<G, RH, HQ>() % 64 != 0 || (G * (T / CW)) % 64 != 0) {
+                  vr_nh<G, RH, C::HQ>() % 64 != 0 || (G * (T / CW)) % 64 != 0) {
         return false;
     } else {
-        if (a.e != EX || (!UA && (a.S % 16) != 0) || a.k != K || (HOUT != (a.sums_out != nullptr) && EX > 0))
+        if (a.e != EX || (!C::UA && (a.S % 16) != 0) || a.k != K || (HOUT != (a.sums_out != nullptr) && EX > 0))
             return false;
         if ((int64_t)(a.k + a.m) * a.S >= ((int64_t)1 << 31)) return false;  // 32-bit row offsets
-        auto kern = k_vr_ws<K, EX, HOUT, G, T, PF, CW, HQ, ST, BT, NTL, UA, BUF, PFD>;
+        auto kern = k_vr_ws<K, EX, HOUT, C>;
         if (ensure_dyn_lds((const void*)kern, dyn) != hipSuccess) return false;
         const int64_t grid = (a.n_blocks + G - 1) / G;
         hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), dyn, s, a);
@@ -1551,29 +1336,161 @@ static bool launch_vr_ws_bt(const VrArgs& a, hipStream_t s) {
     }
 }
 
-#if ZS3_DIAG
-// RS(16+4) rebuild / heal with the survivor prefetch depth and tile length as
-// parameters (diagnostics 250-259, round 3; PF = 2 with 8-byte columns spills
-// in-flight load registers, scripts/check_async_loads.py, so no such instance): e = 1..4 rebuilt rows.
-template <int T, int PF, bool HOUT, int BT, int CW = 4>
-static bool vr16(const VrArgs& a, hipStream_t s) {
-    switch (a.e) {
-        case 1: return launch_vr_ws_t<16, 1, HOUT, 8, T, PF, CW, false, true, BT>(a, s);
-        case 2: return launch_vr_ws_t<16, 2, HOUT, 8, T, PF, CW, false, true, BT>(a, s);
-        case 3: return launch_vr_ws_t<16, 3, HOUT, 8, T, PF, CW, false, true, BT>(a, s);
-        case 4: return launch_vr_ws_t<16, 4, HOUT, 8, T, PF, CW, false, true, BT>(a, s);
-        default: return false;
-    }
-}
-#endif
+// ---- The product shapes (named; the dispatch in fused_v2.hip, fused_v2_gen.hip,
+// fused_v2_get.hip and fused_v2_get_gen.hip says which batch takes which, and why) --------
+namespace shape {
+
+// Encode + sums (k_ehx_ws).
+// Pair-form hash waves, 16 stripes of 384-byte tiles, non-temporal loads and stores,
+// encode waves at priority 1: the large-batch shape of the dyadic geometries.
+struct PairG16 : EncShape {
+    static constexpr int G = 16, T = 384, PM = 1, NTM = 3;
+};
+// RS(8+4) above 2048 stripes (the BASELINE config-4 bench): PairG16 with buffer-addressed
+// columns and the conflict-free LDS row stride (round 4), and the region-interleaved
+// workgroup order over 8 regions (round 5: each XCD walks its own eighth of the batch;
+// 65 536 x 1 MiB 19.52 -> 18.77 ms, profiles/r05/xmap84.jsonl).
+struct Rs84Bulk : PairG16 {
+    static constexpr bool BUF = true;
+    static constexpr int TSP = 1, XMAP = 8;
+};
+// RS(8+4) up to 2048 stripes: 4 stripes of 1 KiB tiles, quad-form hash waves, two tiles
+// of prefetch, one workgroup per CU (LDSMIN), the 256-VGPR budget.
+struct Rs84Mid : EncShape {
+    static constexpr int G = 4, T = 1024, PF = 2, LDSMIN = 83968, NTM = 3, WPE = 2;
+    static constexpr bool HQ = true;
+};
+// RS(16+4) above 1024 stripes: 8 stripes of 384-byte tiles, 8-byte buffer-addressed
+// columns, data rows to LDS before the encode.
+struct Rs164Bulk : EncShape {
+    static constexpr int G = 8, T = 384, NTM = 3, EP = 2;
+    static constexpr bool BUF = true;
+};
+// Quad-form hash waves on 4 stripes of 512-byte tiles (RS(16+4) / RS(12+4) small batches).
+struct Quad512 : EncShape {
+    static constexpr int G = 4, T = 512, NTM = 3;
+    static constexpr bool BUF = true, HQ = true;
+};
+// RS(12+4) at 16-byte-aligned rows above 1024 stripes: the unaligned-row recipe (8-byte
+// columns of 512-byte tiles, L2 prefetch two tiles ahead, conflict-free LDS rows).
+struct Rs124AlignedBulk : EncShape {
+    static constexpr int G = 8, T = 512, CWX = 8, NTM = 3, EP = 2, PFD = 2, TSP = 1;
+    static constexpr bool BUF = true, UA = true;
+};
+// Small batches of the dyadic shapes: 4 stripes of 512-byte tiles, quad-form hash waves,
+// 4 tiles of prefetch, one workgroup per CU (NTM: 3 = nt loads and stores, 2 = stores).
+template <int NTM_>
+struct QuadSmall : EncShape {
+    static constexpr int G = 4, T = 512, PF = 4, LDSMIN = 83968, NTM = NTM_;
+    static constexpr bool HQ = true;
+};
+// BASELINE config 2 (RS(4+2), 1024-2048 stripes): 2 KiB tiles so each latency-bound
+// chain hashes 64 packets between barriers.
+struct Config2 : EncShape {
+    static constexpr int G = 4, T = 2048, PF = 2, LDSMIN = 83968, NTM = 3;
+    static constexpr bool HQ = true;
+};
+// RS(12+4) on 1 MiB blocks (unaligned rows), above 1024 stripes: 4 stripes of 1 KiB
+// tiles, quad-form hash waves issuing the L2 prefetch, 16-byte columns (round 4).
+// Round 5: with the region-interleaved workgroup order (4 096 / 16 384 x 1 MiB
+// 1.37-1.39 / 5.46-5.48 -> 1.33-1.34 / 5.37-5.38 ms, profiles/r05/ab_enc.jsonl).
+struct Rs124Ua1K : EncShape {
+    static constexpr int G = 4, T = 1024, CWX = 16, NTM = 3, EP = 2, PFD = 2, WPE = 2, TSP = 1, XMAP = 8;
+    static constexpr bool BUF = true, HQ = true, UA = true;
+};
+struct Rs124UaSmall : EncShape {
+    static constexpr int G = 4, T = 512, NTM = 3;
+    static constexpr bool BUF = true, HQ = true, UA = true;
+};
+// General M x K matrix (the non-dyadic server defaults), unaligned rows, L2 prefetch,
+// conflict-free LDS rows: k <= 3 on 8 stripes of 1 KiB tiles; RS(4+3) on 16 stripes of
+// 512; RS(5+4) / RS(6+4) on the RS(12+4) 1 KiB quad-form shape; the rest 8 stripes of 512
+// with 8-byte columns.
+struct GenBase : EncShape {
+    static constexpr int NTM = 3, PFD = 2, TSP = 1;
+    static constexpr bool BUF = true, UA = true, GEN = true;
+};
+struct GenLong1K : GenBase {
+    static constexpr int G = 8, T = 1024, CWX = 16;
+};
+struct Gen16x512 : GenBase {
+    static constexpr int G = 16, T = 512, CWX = 16;
+};
+struct GenQuad1K : GenBase {
+    static constexpr int G = 4, T = 1024, CWX = 16, WPE = 2;
+    static constexpr bool HQ = true;
+};
+struct Gen8x512 : GenBase {
+    static constexpr int G = 8, T = 512, CWX = 8;
+};
+
+// GET / heal (k_vr_ws), requested shapes (launch_vr_ws_t fixes the memory policy).
+// RS(4+m): 8 stripes, quad-form hash waves; verify on 256-byte tiles, rebuild / heal on
+// 1 KiB tiles (PF tiles of prefetch).
+template <int T_, int PF_>
+struct K4Quad : GetShape {
+    static constexpr int G = 8, T = T_, PF = PF_;
+    static constexpr bool HQ = true;
+};
+// RS(8+4): 16 stripes of 256-byte tiles (verify, rebuild 1-2); 8-byte columns with
+// batched scalar tables for rebuild 3-4; heal 1-2 on 128-byte tiles, heal 3-4 on 256 with
+// 16-byte columns.
+struct K8Get : GetShape {
+    static constexpr int G = 16, T = 256, PF = 2;
+};
+struct K8Rebuild34 : GetShape {
+    static constexpr int G = 16, T = 256, CW = 8, BT = 4;
+    static constexpr bool ST = true, BUF = true;
+};
+struct K8Heal12 : GetShape {
+    static constexpr int G = 16, T = 128, PF = 2, CW = 8, BT = 4;
+    static constexpr bool ST = true;
+};
+struct K8Heal34 : GetShape {
+    static constexpr int G = 16, T = 256, CW = 16, BT = 4;
+    static constexpr bool ST = true, BUF = true;
+};
+// RS(16+4): 8 stripes; verify on 256-byte tiles; rebuild 1-2 with 4-byte columns (one
+// table per wait); rebuild 3-4 with 8-byte columns of 512; heal with 8-byte columns of 384.
+struct K16Verify : GetShape {
+    static constexpr int G = 8, T = 256, PF = 2;
+};
+struct K16Rebuild12 : GetShape {
+    static constexpr int G = 8, T = 256, PF = 2, CW = 4;
+    static constexpr bool ST = true;
+};
+struct K16Rebuild34 : GetShape {
+    static constexpr int G = 8, T = 512, CW = 8, BT = 4;
+    static constexpr bool ST = true, BUF = true;
+};
+struct K16Heal : GetShape {
+    static constexpr int G = 8, T = 384, CW = 8, BT = 4;
+    static constexpr bool ST = true, BUF = true;
+};
+// RS(12+4) and k = 9-11: 8 stripes of 8-byte columns of 512-byte tiles, unaligned rows.
+template <bool UA_>
+struct Wide512 : GetShape {
+    static constexpr int G = 8, T = 512, CW = 8, BT = 4;
+    static constexpr bool ST = true, UA = UA_;
+};
+// k = 2, 3: 8 stripes of 1 KiB tiles, quad-form hash waves; k = 5-7: 16 stripes of 256.
+template <bool UA_>
+struct GenGetQuad1K : GetShape {
+    static constexpr int G = 8, T = 1024, PF = 2, BT = 4;
+    static constexpr bool HQ = true, ST = true, UA = UA_;
+};
+template <bool UA_>
+struct GenGet16x256 : GetShape {
+    static constexpr int G = 16, T = 256, CW = 8, BT = 4;
+    static constexpr bool ST = true, UA = UA_;
+};
+
+}  // namespace shape
 
 #if ZS3_DIAG
-// Encode variants of the diagnostics build, one translation unit per shape
-// (fused_v2_km84.hip, fused_v2_km42.hip, fused_v2_km164.hip, fused_v2_km124.hip)
-bool launch_ehx_km_8_4(int v, const EncArgs& a, hipStream_t s);
-bool launch_ehx_km_4_2(int v, const EncArgs& a, hipStream_t s);
-bool launch_ehx_km_16_4(int v, const EncArgs& a, hipStream_t s);
-bool launch_ehx_km_12_4(int v, const EncArgs& a, hipStream_t s);
+// Encode variants of the diagnostics build (fused_v2_diag.hip, fused_v2_gen.hip)
+bool launch_ehx_diag(int v, const EncArgs& a, hipStream_t s);
+bool launch_ehx_gen_xmap(const EncArgs& a, hipStream_t s);
 #endif
 
 }  // namespace zs3k

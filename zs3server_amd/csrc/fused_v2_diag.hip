@@ -1,0 +1,78 @@
+// fused_v2_diag.hip — encode variants of the diagnostics build (libzs3gpu_diag.so only),
+// selected per thread by zs3server_amd.diag(v) / zs3_debug_set_variant.  Each variant is
+// a product shape (fused_v2.hpp, namespace shape) with one knob changed, named here; the
+// product dispatch is fused_v2.hip.  (Round 5 pruned the ~140 earlier-round candidates:
+// their numbers and measurements stay in profiles/r02-r04 and DESIGN.md §4-§12.)
+//
+//  310 / 311 / 312  RS(8+4) Rs84Bulk timing ablations (output differs): no HighwayHash
+//                   arithmetic / no GF arithmetic / neither — the memory pattern alone,
+//                   the headline's pattern roof
+//  313              Rs84Bulk with per-wave barrier / load-wait stamps (scripts/stamps3.py)
+//  400 / 401        the conflict-free LDS row stride (TSP 1) alone on the RS(4+4) bulk shape
+//                   (PairG16) and the RS(16+4) bulk shape
+//  402              RS(4+4) on the RS(8+4) headline shape (Rs84Bulk)
+//  409-414          Rs84Bulk with the region-interleaved workgroup order (ws_group) over 1
+//                   (none: the round-4 product) / 2 / 4 / 8 (the product) / 16 / 32 regions
+//  415              XMAP 8 on the RS(16+4) bulk shape; 417 TSP 1 + XMAP 8 on it
+//  416              the RS(12+4) 1 KiB UA shape without XMAP (the round-4 product)
+//  418              XMAP 8 on PairG16 (RS(4+4) / RS(4+2) bulk); 419 XMAP 8 on every GEN shape
+#include "fused_v2.hpp"
+
+namespace zs3k {
+
+#if ZS3_DIAG
+namespace shape {
+struct Rs84NoHash : Rs84Bulk {
+    static constexpr int ABL = 1;
+};
+struct Rs84NoGf : Rs84Bulk {
+    static constexpr int EP = 9;
+};
+struct Rs84MemOnly : Rs84Bulk {
+    static constexpr int EP = 9, ABL = 1;
+};
+struct Rs84Stamped : Rs84Bulk {
+    static constexpr bool WT = true;
+};
+}  // namespace shape
+
+bool launch_ehx_diag(int v, const EncArgs& a, hipStream_t s) {
+    using namespace shape;
+    if (a.k == 8 && a.m == 4) {
+        switch (v) {
+            case 310: return launch_ws<8, 4, Rs84NoHash>(a, s);
+            case 311: return launch_ws<8, 4, Rs84NoGf>(a, s);
+            case 312: return launch_ws<8, 4, Rs84MemOnly>(a, s);
+            case 313: return launch_ws<8, 4, Rs84Stamped>(a, s);
+            case 409: return launch_ws<8, 4, XMap<Rs84Bulk, 0>>(a, s);
+            case 410: return launch_ws<8, 4, XMap<Rs84Bulk, 2>>(a, s);
+            case 411: return launch_ws<8, 4, XMap<Rs84Bulk, 4>>(a, s);
+            case 412: return launch_ws<8, 4, XMap<Rs84Bulk, 8>>(a, s);
+            case 413: return launch_ws<8, 4, XMap<Rs84Bulk, 16>>(a, s);
+            case 414: return launch_ws<8, 4, XMap<Rs84Bulk, 32>>(a, s);
+            default: return false;
+        }
+    }
+    if (a.k == 4 && (a.m == 4 || a.m == 2)) {
+        switch (v) {
+            case 400: return a.m == 4 && launch_ws<4, 4, Tsp1<PairG16>>(a, s);
+            case 402: return a.m == 4 && launch_ws<4, 4, Rs84Bulk>(a, s);
+            case 418: return a.m == 4 ? launch_ws<4, 4, XMap<PairG16, 8>>(a, s) : launch_ws<4, 2, XMap<PairG16, 8>>(a, s);
+            default: return false;
+        }
+    }
+    if (a.k == 16 && a.m == 4) {
+        switch (v) {
+            case 401: return launch_ws<16, 4, Tsp1<Rs164Bulk>>(a, s);
+            case 415: return launch_ws<16, 4, XMap<Rs164Bulk, 8>>(a, s);
+            case 417: return launch_ws<16, 4, XMap<Tsp1<Rs164Bulk>, 8>>(a, s);
+            default: return false;
+        }
+    }
+    if (a.k == 12 && a.m == 4 && v == 416) return launch_ws<12, 4, XMap<Rs124Ua1K, 0>>(a, s);
+    if (v == 419) return launch_ehx_gen_xmap(a, s);
+    return false;
+}
+#endif
+
+}  // namespace zs3k

@@ -33,16 +33,16 @@ namespace zs3k {
 // prefetch, 16-byte columns on the 256-VGPR budget; diagnostics 345): 2.04-2.05 -> 1.95-1.97
 // and 1.89-1.90 -> 1.88-1.89 ms (sweep_gen_1k.jsonl, one box, three runs); K >= 7 spills
 // there (RS(10+4): 231 VGPRs).
-template <int K, int M>
+template <int K, int M, int XM = 0>
 static bool launch_gen_t(const EncArgs& a, hipStream_t s) {
     if constexpr (K <= 3)
-        return launch_ws_t<K, M, 8, 1024, 1, true, false, 0, false, 0, 16, false, 3, false, 0, 2, true, 3, 1, 0, true>(a, s);
+        return launch_ws<K, M, WithXMap<shape::GenLong1K, XM>>(a, s);
     else if constexpr (K + M <= 8)  // RS(4+3): 1 KiB tiles measured 1.54 -> 1.64 ms (geom_r9.jsonl)
-        return launch_ws_t<K, M, 16, 512, 1, true, false, 0, false, 0, 16, false, 3, false, 0, 2, true, 3, 1, 0, true>(a, s);
+        return launch_ws<K, M, WithXMap<shape::Gen16x512, XM>>(a, s);
     else if constexpr (K <= 6)  // RS(5+4) / (6+4): diagnostics 345 (profiles/r04/sweep_gen_1k.jsonl)
-        return launch_ws_t<K, M, 4, 1024, 1, true, true, 0, false, 0, 16, false, 3, false, 0, 2, true, 2, 1, 0, true>(a, s);
+        return launch_ws<K, M, WithXMap<shape::GenQuad1K, XM>>(a, s);
     else
-        return launch_ws_t<K, M, 8, 512, 1, true, false, 0, false, 0, 8, false, 3, false, 0, 2, true, 3, 1, 0, true>(a, s);
+        return launch_ws<K, M, WithXMap<shape::Gen8x512, XM>>(a, s);
 }
 
 #define ZS3_GEN_KM(X) X(2, 2) X(3, 2) X(3, 3) X(4, 3) X(5, 4) X(6, 4) X(7, 4) X(9, 4) X(10, 4) X(11, 4)
@@ -55,44 +55,19 @@ bool has_gen_encode(int k, int m) {
 }
 
 #if ZS3_DIAG
-// Diagnostics (round 4) shape candidates for the general-matrix encode + sums:
-//  340: no L2 prefetch by the hash waves (PFD = 0)
-//  341: 384-byte tiles
-//  342: quad-form hash waves (one HH lane per thread)
-//  343: temporal data loads (nt stores only), no L2 prefetch
-//  344: 8 stripes, 1 KiB tiles (fewer barriers per hashed byte)
-//  345 / 346: 4 stripes of 1 KiB tiles, quad-form hash waves issuing the L2 prefetch 2
-//  tiles ahead (the RS(12+4) product shape), 16-byte columns (256-VGPR budget) / 8-byte
-template <int K, int M>
-static bool launch_gen_diag(int v, const EncArgs& a, hipStream_t s) {
-    constexpr int G = K + M <= 8 ? 16 : 8;
-    constexpr int CW = K + M <= 8 ? 16 : 8;
-    switch (v) {
-        case 340: return launch_ws_t<K, M, G, 512, 1, true, false, 0, false, 0, CW, false, 3, false, 0, 0, true, 3, 1, 0, true>(a, s);
-        case 341: return launch_ws_t<K, M, G, 384, 1, true, false, 0, false, 0, CW, false, 3, false, 0, 2, true, 3, 1, 0, true>(a, s);
-        case 342: return launch_ws_t<K, M, G, 512, 1, true, true, 0, false, 0, CW, false, 3, false, 0, 0, true, 3, 1, 0, true>(a, s);
-        case 343: return launch_ws_t<K, M, G, 512, 1, true, false, 0, false, 0, CW, false, 2, false, 0, 0, true, 3, 1, 0, true>(a, s);
-        case 344: return launch_ws_t<K, M, 8, 1024, 1, true, false, 0, false, 0, CW, false, 3, false, 0, 2, true, 3, 1, 0, true>(a, s);
-        case 345: return launch_ws_t<K, M, 4, 1024, 1, true, true, 0, false, 0, 16, false, 3, false, 0, 2, true, 2, 1, 0, true>(a, s);
-        case 346: return launch_ws_t<K, M, 4, 1024, 1, true, true, 0, false, 0, 8, false, 3, false, 0, 2, true, 3, 1, 0, true>(a, s);
-        default: return false;
-    }
+// diagnostics 419: every general-matrix shape with the region-interleaved workgroup order
+bool launch_ehx_gen_xmap(const EncArgs& a, hipStream_t s) {
+    if (!a.sums) return false;
+#define X(K, M) \
+    if (a.k == K && a.m == M) return launch_gen_t<K, M, 8>(a, s);
+    ZS3_GEN_KM(X)
+#undef X
+    return false;
 }
 #endif
 
 int launch_ehx_gen(const EncArgs& a, hipStream_t s) {
     if (!a.sums) return PATH_NONE;
-#if ZS3_DIAG
-    if (a.variant >= 340 && a.variant <= 346) {
-        bool ok = false;
-        if (a.k == 3 && a.m == 3) ok = launch_gen_diag<3, 3>(a.variant, a, s);
-        if (a.k == 3 && a.m == 2) ok = launch_gen_diag<3, 2>(a.variant, a, s);
-        if (a.k == 5 && a.m == 4) ok = launch_gen_diag<5, 4>(a.variant, a, s);
-        if (a.k == 6 && a.m == 4) ok = launch_gen_diag<6, 4>(a.variant, a, s);
-        if (a.k == 10 && a.m == 4) ok = launch_gen_diag<10, 4>(a.variant, a, s);
-        return ok ? PATH_WS : PATH_NONE;
-    }
-#endif
 #define X(K, M) \
     if (a.k == K && a.m == M) return launch_gen_t<K, M>(a, s) ? PATH_WS : PATH_NONE;
     ZS3_GEN_KM(X)

@@ -1,6 +1,5 @@
 // fused_v2_get.hip — GET / heal dispatch onto the warp-specialised k_vr_ws instances
-// (templates in fused_v2.hpp): the product defaults (the diagnostics variants are in
-// fused_v2_get_diag.hip).
+// (templates and named shapes in fused_v2.hpp): the product defaults.
 // Replaces the arithmetic of parallelReader + streamingBitrotReader.ReadAt
 // (cmd/erasure-decode.go:165-179, cmd/bitrot-streaming.go:171-186),
 // Erasure.DecodeDataBlocks (cmd/erasure-coding.go:96-109) and Erasure.Heal
@@ -8,10 +7,6 @@
 #include "fused_v2.hpp"
 
 namespace zs3k {
-
-#if ZS3_DIAG
-bool launch_vr_ws_diag(int v, const VrArgs& a, hipStream_t s);  // fused_v2_get_diag.hip
-#endif
 
 // Product GET / heal instances by shape, erasure count e and heal (sums of the rebuilt
 // rows); false = no warp-specialised instance (the caller falls back).
@@ -28,17 +23,17 @@ static bool launch_vr_ws_default(const VrArgs& a, hipStream_t s) {
         // -> 1.92 (2 of prefetch: the 4-deep instance measured 2.19)
         // (profiles/r04/get_ab_k4.jsonl, mean of two rounds)
         if (heal) {
-            if (a.e == 1) return launch_vr_ws_t<4, 1, true, 8, 1024, 4, 16, true>(a, s);
-            if (a.e == 2) return launch_vr_ws_t<4, 2, true, 8, 1024, 4, 16, true>(a, s);
-            if (a.e == 3) return launch_vr_ws_t<4, 3, true, 8, 1024, 4, 16, true>(a, s);
-            if (a.e == 4) return launch_vr_ws_t<4, 4, true, 8, 1024, 2, 16, true>(a, s);
+            if (a.e == 1) return launch_vr_ws_t<4, 1, true, shape::K4Quad<1024, 4>>(a, s);
+            if (a.e == 2) return launch_vr_ws_t<4, 2, true, shape::K4Quad<1024, 4>>(a, s);
+            if (a.e == 3) return launch_vr_ws_t<4, 3, true, shape::K4Quad<1024, 4>>(a, s);
+            if (a.e == 4) return launch_vr_ws_t<4, 4, true, shape::K4Quad<1024, 2>>(a, s);
             return false;
         }
-        if (a.e == 0) return launch_vr_ws_t<4, 0, false, 8, 256, 4, 16, true>(a, s);
-        if (a.e == 1) return launch_vr_ws_t<4, 1, false, 8, 1024, 4, 16, true>(a, s);
-        if (a.e == 2) return launch_vr_ws_t<4, 2, false, 8, 1024, 4, 16, true>(a, s);
-        if (a.e == 3) return launch_vr_ws_t<4, 3, false, 8, 1024, 4, 16, true>(a, s);
-        if (a.e == 4) return launch_vr_ws_t<4, 4, false, 8, 1024, 4, 16, true>(a, s);
+        if (a.e == 0) return launch_vr_ws_t<4, 0, false, shape::K4Quad<256, 4>>(a, s);
+        if (a.e == 1) return launch_vr_ws_t<4, 1, false, shape::K4Quad<1024, 4>>(a, s);
+        if (a.e == 2) return launch_vr_ws_t<4, 2, false, shape::K4Quad<1024, 4>>(a, s);
+        if (a.e == 3) return launch_vr_ws_t<4, 3, false, shape::K4Quad<1024, 4>>(a, s);
+        if (a.e == 4) return launch_vr_ws_t<4, 4, false, shape::K4Quad<1024, 4>>(a, s);
         return false;
     }
     if (a.k == 16) {
@@ -51,11 +46,11 @@ static bool launch_vr_ws_default(const VrArgs& a, hipStream_t s) {
             // 0.463/0.525/0.620/0.699 ms vs 0.492/0.544/0.622/0.741 for the round-2
             // instances (diagnostics 242; profiles/r03/get_ab_rs164_vr16*.jsonl, variants
             // 250 / 256)
-            if (a.e == 0) return launch_vr_ws_t<16, 0, false, 8, 256, 2>(a, s);
-            if (a.e == 1) return launch_vr_ws_t<16, 1, false, 8, 256, 2, 4, false, true, 0>(a, s);
-            if (a.e == 2) return launch_vr_ws_t<16, 2, false, 8, 256, 2, 4, false, true, 0>(a, s);
-            if (a.e == 3) return launch_vr_ws_t<16, 3, false, 8, 512, 1, 8, false, true, 4, false, true>(a, s);
-            if (a.e == 4) return launch_vr_ws_t<16, 4, false, 8, 512, 1, 8, false, true, 4, false, true>(a, s);
+            if (a.e == 0) return launch_vr_ws_t<16, 0, false, shape::K16Verify>(a, s);
+            if (a.e == 1) return launch_vr_ws_t<16, 1, false, shape::K16Rebuild12>(a, s);
+            if (a.e == 2) return launch_vr_ws_t<16, 2, false, shape::K16Rebuild12>(a, s);
+            if (a.e == 3) return launch_vr_ws_t<16, 3, false, shape::K16Rebuild34>(a, s);
+            if (a.e == 4) return launch_vr_ws_t<16, 4, false, shape::K16Rebuild34>(a, s);
             return false;
         }
         // heal 1-4: 8-byte rebuild columns of 384-byte tiles (6 rebuild waves beside 5
@@ -63,10 +58,10 @@ static bool launch_vr_ws_default(const VrArgs& a, hipStream_t s) {
         // 1 MiB: heal 1/2/3/4 0.501/0.573/0.652/0.759 ms vs 0.525/0.816/0.945/1.073 for
         // the round-2 instances (128-byte tiles, 4-byte columns; diagnostics 242)
         // (variant 259, profiles/r03/get_ab_rs164_vr16*.jsonl)
-        if (a.e == 1) return launch_vr_ws_t<16, 1, true, 8, 384, 1, 8, false, true, 4, false, true>(a, s);
-        if (a.e == 2) return launch_vr_ws_t<16, 2, true, 8, 384, 1, 8, false, true, 4, false, true>(a, s);
-        if (a.e == 3) return launch_vr_ws_t<16, 3, true, 8, 384, 1, 8, false, true, 4, false, true>(a, s);
-        if (a.e == 4) return launch_vr_ws_t<16, 4, true, 8, 384, 1, 8, false, true, 4, false, true>(a, s);
+        if (a.e == 1) return launch_vr_ws_t<16, 1, true, shape::K16Heal>(a, s);
+        if (a.e == 2) return launch_vr_ws_t<16, 2, true, shape::K16Heal>(a, s);
+        if (a.e == 3) return launch_vr_ws_t<16, 3, true, shape::K16Heal>(a, s);
+        if (a.e == 4) return launch_vr_ws_t<16, 4, true, shape::K16Heal>(a, s);
         return false;
     }
     if (a.k == 12) {
@@ -86,15 +81,15 @@ static bool launch_vr_ws_default(const VrArgs& a, hipStream_t s) {
         // 1.15/1.43 ms, heal 1/2/3/4 -> 1.14/1.26/1.43/1.60 (get_ab_rs124_temporal.jsonl)
         if (a.e < 1 || a.e > 4) return false;
         if (!heal) {
-            if (a.e == 1) return launch_vr_ws_t<12, 1, false, 8, 512, 1, 8, false, true, 4, true>(a, s);
-            if (a.e == 2) return launch_vr_ws_t<12, 2, false, 8, 512, 1, 8, false, true, 4, true>(a, s);
-            if (a.e == 3) return launch_vr_ws_t<12, 3, false, 8, 512, 1, 8, false, true, 4, true>(a, s);
-            return launch_vr_ws_t<12, 4, false, 8, 512, 1, 8, false, true, 4, true>(a, s);
+            if (a.e == 1) return launch_vr_ws_t<12, 1, false, shape::Wide512<true>>(a, s);
+            if (a.e == 2) return launch_vr_ws_t<12, 2, false, shape::Wide512<true>>(a, s);
+            if (a.e == 3) return launch_vr_ws_t<12, 3, false, shape::Wide512<true>>(a, s);
+            return launch_vr_ws_t<12, 4, false, shape::Wide512<true>>(a, s);
         }
-        if (a.e == 1) return launch_vr_ws_t<12, 1, true, 8, 512, 1, 8, false, true, 4, true>(a, s);
-        if (a.e == 2) return launch_vr_ws_t<12, 2, true, 8, 512, 1, 8, false, true, 4, true>(a, s);
-        if (a.e == 3) return launch_vr_ws_t<12, 3, true, 8, 512, 1, 8, false, true, 4, true>(a, s);
-        return launch_vr_ws_t<12, 4, true, 8, 512, 1, 8, false, true, 4, true>(a, s);
+        if (a.e == 1) return launch_vr_ws_t<12, 1, true, shape::Wide512<true>>(a, s);
+        if (a.e == 2) return launch_vr_ws_t<12, 2, true, shape::Wide512<true>>(a, s);
+        if (a.e == 3) return launch_vr_ws_t<12, 3, true, shape::Wide512<true>>(a, s);
+        return launch_vr_ws_t<12, 4, true, shape::Wide512<true>>(a, s);
     }
     if (a.k != 8) return false;
     if (heal) {
@@ -107,10 +102,10 @@ static bool launch_vr_ws_default(const VrArgs& a, hipStream_t s) {
         // 4096 x 1 MiB: 1.34 / 1.51 ms vs 1.40 / 1.61 for the round-2 instances (8-byte
         // columns of 128-byte tiles, diagnostics 232) (variant 262,
         // profiles/r03/get_ab_r03_84.jsonl)
-        if (a.e == 1) return launch_vr_ws_t<8, 1, true, 16, 128, 2, 8, false, true, 4>(a, s);
-        if (a.e == 2) return launch_vr_ws_t<8, 2, true, 16, 128, 2, 8, false, true, 4>(a, s);
-        if (a.e == 3) return launch_vr_ws_t<8, 3, true, 16, 256, 1, 16, false, true, 4, false, true>(a, s);
-        if (a.e == 4) return launch_vr_ws_t<8, 4, true, 16, 256, 1, 16, false, true, 4, false, true>(a, s);
+        if (a.e == 1) return launch_vr_ws_t<8, 1, true, shape::K8Heal12>(a, s);
+        if (a.e == 2) return launch_vr_ws_t<8, 2, true, shape::K8Heal12>(a, s);
+        if (a.e == 3) return launch_vr_ws_t<8, 3, true, shape::K8Heal34>(a, s);
+        if (a.e == 4) return launch_vr_ws_t<8, 4, true, shape::K8Heal34>(a, s);
         return false;
     }
     // RS(8+4) GET: 16 stripes, 256-byte tiles, verify-only or rebuild 1-2 with 16-byte
@@ -118,21 +113,18 @@ static bool launch_vr_ws_default(const VrArgs& a, hipStream_t s) {
     // waves, batched scalar tables): 4096 x 1 MiB 1.27 / 1.42 ms vs 1.35 / 1.58 with
     // 16-byte columns (profiles/r02/get_ab_waves.jsonl), batching 1.34 vs 1.40 ms for
     // rebuild 4
-    if (a.e == 0) return launch_vr_ws_t<8, 0, false, 16, 256, 2>(a, s);
-    if (a.e == 1) return launch_vr_ws_t<8, 1, false, 16, 256, 2>(a, s);
-    if (a.e == 2) return launch_vr_ws_t<8, 2, false, 16, 256, 2>(a, s);
-    if (a.e == 3) return launch_vr_ws_t<8, 3, false, 16, 256, 1, 8, false, true, 4, false, true>(a, s);
-    if (a.e == 4) return launch_vr_ws_t<8, 4, false, 16, 256, 1, 8, false, true, 4, false, true>(a, s);
+    if (a.e == 0) return launch_vr_ws_t<8, 0, false, shape::K8Get>(a, s);
+    if (a.e == 1) return launch_vr_ws_t<8, 1, false, shape::K8Get>(a, s);
+    if (a.e == 2) return launch_vr_ws_t<8, 2, false, shape::K8Get>(a, s);
+    if (a.e == 3) return launch_vr_ws_t<8, 3, false, shape::K8Rebuild34>(a, s);
+    if (a.e == 4) return launch_vr_ws_t<8, 4, false, shape::K8Rebuild34>(a, s);
     return false;
 }
 
+// v: 0 = the product shapes (the diagnostics build's GET variants change a product
+// shape's memory policy or layout inside launch_vr_ws_t, with a.variant set)
 bool launch_vr_ws(int v, const VrArgs& a, hipStream_t s) {
-    if (v == 0) return launch_vr_ws_default(a, s);
-#if ZS3_DIAG
-    return launch_vr_ws_diag(v, a, s);
-#else
-    return false;
-#endif
+    return v == 0 && launch_vr_ws_default(a, s);
 }
 
 }  // namespace zs3k

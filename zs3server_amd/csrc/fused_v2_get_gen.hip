@@ -28,28 +28,16 @@ namespace zs3k {
 template <int K, int EX, bool HOUT>
 static bool launch_gget_e(const VrArgs& a, hipStream_t s) {
     constexpr bool UA = K != 2;
-#if ZS3_DIAG
-    // round-4 shape candidates: 350 = k <= 3 on 8 stripes of 1 KiB tiles (2 of
-    // prefetch); 351 = k = 5-7 on the k >= 9 shape (8 stripes, 512-byte tiles)
-    if (a.variant == 350) {
-        if constexpr (K <= 3) return launch_vr_ws_t<K, EX, HOUT, 8, 1024, 2, 16, true, true, 4, UA>(a, s);
-        return false;
-    }
-    if (a.variant == 351) {
-        if constexpr (K >= 5 && K <= 7) return launch_vr_ws_t<K, EX, HOUT, 8, 512, 1, 8, false, true, 4, UA>(a, s);
-        return false;
-    }
-#endif
     // k <= 3 (round 4, diagnostics 350): 8 stripes of 1 KiB tiles, 2 of prefetch:
     // 4096 x 1 MiB RS(2+2) rebuild / heal 2 2.30 / 2.38 -> 1.96 / 1.97 ms, RS(3+2)
     // 1.75 / 1.80 -> 1.53 / 1.51, RS(3+3) 1.83 / 1.87 -> 1.65 / 1.65 (16 stripes of
     // 256-byte tiles before; profiles/r04/get_ab_gen.jsonl)
     if constexpr (K <= 3)
-        return launch_vr_ws_t<K, EX, HOUT, 8, 1024, 2, 16, true, true, 4, UA>(a, s);
+        return launch_vr_ws_t<K, EX, HOUT, shape::GenGetQuad1K<UA>>(a, s);
     else if constexpr (K <= 7)
-        return launch_vr_ws_t<K, EX, HOUT, 16, 256, 1, 8, false, true, 4, UA>(a, s);
+        return launch_vr_ws_t<K, EX, HOUT, shape::GenGet16x256<UA>>(a, s);
     else
-        return launch_vr_ws_t<K, EX, HOUT, 8, 512, 1, 8, false, true, 4, UA>(a, s);
+        return launch_vr_ws_t<K, EX, HOUT, shape::Wide512<UA>>(a, s);
 }
 
 template <int K, int MAXE>

@@ -377,185 +377,6 @@ __global__ void __launch_bounds__(NT) k_encode_hash(EncArgs a) {
     }
 }
 
-#if ZS3_DIAG
-// ---------------------------------------------------------------------------
-// (diagnostics build) Software-pipelined fused kernel: in step i every wave hashes tile i (LDS buffer
-// i%2) AND encodes tile i+1 (into buffer (i+1)%2) in ONE basic block, so the
-// serial HighwayHash chain (~200 cycles of dependent latency per packet) is
-// filled with the independent GF(2^8) encode work instead of being serialised
-// with it behind a barrier.  One barrier per step.  Full tiles hash NPK = T/32
-// packets fully unrolled; a trailing partial tile uses the looped path.
-template <int K, int M, int G, int T, int NT, int CW, bool STAMP = false, int DYB = 0>
-__global__ void __launch_bounds__(NT) k_encode_hash_pipe(EncArgs a) {
-    constexpr int R = K + M;
-    constexpr int NWd = CW / 4;
-    constexpr int TS = T + 32;
-    constexpr int CPB = T / CW;
-    constexpr int NCOL = G * CPB;
-    constexpr int NPK = T / 32;
-    static_assert(NCOL <= NT, "one column per thread");
-
-    constexpr int NTAB = DYB ? K * 8 : M * K * 8;
-    __shared__ __attribute__((aligned(16))) uint8_t tile[2][G * R * TS];
-    __shared__ __attribute__((aligned(16))) uint32_t tabs[NTAB];
-    const uint32_t* dtabs = tabs;
-
-    const int tid = threadIdx.x;
-    const int64_t blk0 = (int64_t)blockIdx.x * G;
-    const int64_t S = a.S;
-    const int64_t ntile = (S + T - 1) / T;
-
-    for (int i = tid; i < NTAB; i += NT) tabs[i] = DYB ? a.dtables[i] : a.tables[i];
-
-    const int chain = tid >> 2, lane = tid & 3;
-    const bool chain_live = chain < G * R && (blk0 + chain / R) < a.n_blocks;
-    const int crow = chain < G * R ? chain : 0;
-    const uint32_t sel = zipper_sel(lane);
-    HHLane st = hh_init(lane, a.key[0], a.key[1], a.key[2], a.key[3]);
-
-    // encode column of this thread (dead stripes alias the last live block)
-    const bool col_live = tid < NCOL;
-    const int g = col_live ? tid / CPB : 0;
-    const int o = (tid % CPB) * CW;
-    const int64_t b = (blk0 + g) < a.n_blocks ? (blk0 + g) : (a.n_blocks - 1);
-    const uint8_t* blk = a.data + b * a.data_stride + o;
-    uint8_t* pbase = a.parity + b * a.parity_stride + o;
-
-    Col<NWd> x[K] = {};
-    auto load_tile = [&](int64_t t0) {
-        if (col_live && t0 + o < S) {
-#pragma unroll
-            for (int j = 0; j < K; ++j) x[j] = ldcol<NWd>(blk + (int64_t)j * S + t0);
-        }
-    };
-    // FULL: the caller guarantees tile t0 is a full tile and every thread owns a
-    // column, so the body has no branch and shares a basic block with the hash.
-    auto encode_tile = [&](int64_t t0, uint8_t* tl, auto full) {
-        if constexpr (!decltype(full)::value) {
-            if (!(col_live && t0 + o < S)) return;
-        }
-        Col<NWd> par[M];
-        if constexpr (DYB != 0) {
-            encode_dyadic<NWd, K, M>(x, par, dtabs);
-#pragma unroll
-            for (int j = 0; j < K; ++j) stcol<NWd>(tl + (g * R + j) * TS + o, x[j]);
-        } else {
-            // plain form kept inline: wrapped in a helper, hipcc's scheduling of
-            // this loop doubles the VGPR count (255 vs 120).
-            const uint32_t* tb = tabs + opaque_zero();
-            GfAcc acc[M][NWd];
-#pragma unroll
-            for (int r = 0; r < M; ++r)
-#pragma unroll
-                for (int w = 0; w < NWd; ++w) acc_init(acc[r][w]);
-#pragma unroll
-            for (int j = 0; j < K; ++j) {
-                Nib nb[NWd];
-#pragma unroll
-                for (int w = 0; w < NWd; ++w) nb[w] = split_nibbles(x[j].w[w]);
-#pragma unroll
-                for (int r = 0; r < M; ++r) {
-                    const CoefTab t = load_coef(tb, r * K + j);
-#pragma unroll
-                    for (int w = 0; w < NWd; ++w) acc_add(acc[r][w], gf_lookup(nb[w], t));
-                }
-                stcol<NWd>(tl + (g * R + j) * TS + o, x[j]);
-            }
-#pragma unroll
-            for (int r = 0; r < M; ++r)
-#pragma unroll
-                for (int w = 0; w < NWd; ++w) par[r].w[w] = acc_done(acc[r][w]);
-        }
-#pragma unroll
-        for (int r = 0; r < M; ++r) {
-            const Col<NWd>& p = par[r];
-            stcol<NWd>(tl + (g * R + K + r) * TS + o, p);
-            stcol<NWd>(pbase + (int64_t)r * S + t0, p);
-        }
-    };
-    auto hash_full = [&](const uint8_t* tl) {
-        const uint64_t* p = reinterpret_cast<const uint64_t*>(tl + crow * TS) + lane;
-        uint64_t w[NPK];
-#pragma unroll
-        for (int i = 0; i < NPK; ++i) w[i] = p[4 * i];
-#pragma unroll
-        for (int i = 0; i < NPK; ++i) hh_update(st, w[i], sel);
-    };
-    auto hash_part = [&](const uint8_t* tl, int L) {
-        const uint8_t* row = tl + crow * TS;
-        hh_packets(st, row, L >> 5, lane, sel);
-        if (L & 31) hh_remainder(st, row + (L & ~31), (uint32_t)(L & 31), lane, sel);
-    };
-
-    uint64_t ph[3] = {0, 0, 0};
-    auto stamp = [&]() -> uint64_t {
-        uint64_t t = 0;
-        if constexpr (STAMP) {
-            __builtin_amdgcn_sched_barrier(0);
-            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        return t;
-    };
-
-    uint64_t rt0 = 0, ct0 = 0;
-    if constexpr (STAMP) {
-        rt0 = __builtin_amdgcn_s_memrealtime();
-        ct0 = __builtin_amdgcn_s_memtime();
-    }
-    using Full = std::integral_constant<bool, true>;
-    using Part = std::integral_constant<bool, false>;
-    lds_barrier();  // tables visible
-    load_tile(0);
-    encode_tile(0, tile[0], Part{});
-    if (ntile > 1) load_tile(T);
-    lds_barrier();
-    for (int64_t i = 0; i < ntile; ++i) {
-        uint8_t* cur = tile[i & 1];
-        uint8_t* nxt = tile[(i + 1) & 1];
-        const int64_t t_next = (i + 1) * T;
-        const int Lcur = (int)((S - i * T) < T ? (S - i * T) : T);
-        const uint64_t s0 = stamp();
-        if (NCOL == NT && Lcur == T && t_next + T <= S) {
-            // one basic block: encode(i+1) || hash(i)
-            encode_tile(t_next, nxt, Full{});
-            hash_full(cur);
-        } else if (Lcur == T) {
-            encode_tile(t_next, nxt, Part{});
-            hash_full(cur);
-        } else {
-            encode_tile(t_next, nxt, Part{});
-            hash_part(cur, Lcur);
-        }
-        const uint64_t s1 = stamp();
-        if (t_next + T < S) load_tile(t_next + T);
-        lds_barrier();
-        const uint64_t s2 = stamp();
-        if constexpr (STAMP) {
-            ph[0] += s1 - s0;
-            ph[1] += s2 - s1;
-        }
-    }
-    const uint64_t h = hh_finalize256(st, lane, sel);
-    if (chain_live) {
-        const int64_t bb = blk0 + chain / R;
-        const int s = chain % R;
-        *reinterpret_cast<uint64_t*>(a.sums + (bb * R + s) * 32 + 8 * lane) = h;
-    }
-    if constexpr (STAMP) {
-        if ((tid & 63) == 0 && a.dbg) {
-            uint64_t* d = a.dbg + ((int64_t)blockIdx.x * (NT / 64) + (tid >> 6)) * 5;
-            const uint64_t rt1 = __builtin_amdgcn_s_memrealtime();
-            const uint64_t ct1 = __builtin_amdgcn_s_memtime();
-            d[0] = ph[0];
-            d[1] = rt0;
-            d[2] = ph[1];
-            d[3] = rt1;
-            d[4] = ct1 - ct0;
-        }
-    }
-}
-#endif  // ZS3_DIAG
 
 // ---------------------------------------------------------------------------
 // Encode only (no hash): one thread per 16-byte column, K loads -> M stores.
@@ -1431,115 +1252,6 @@ static void launch_fused(const EncArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((k_encode_hash<K, M, G, T, NBUF, NT, CW, PF, NTL, STAMP>), dim3((unsigned)grid), dim3(NT), 0, s, a);
 }
 
-#if ZS3_DIAG
-// ---- diagnostics build: experimental launch shapes of the first-generation kernels
-template <int K, int M, int G, int T, int CW, bool STAMP = false>
-static void launch_pipe(const EncArgs& a, hipStream_t s) {
-    constexpr int R = K + M;
-    constexpr int NT = round64(4 * G * R);
-    static_assert(T % CW == 0 && T % 32 == 0, "tile");
-    if constexpr (G * T / CW <= NT) {
-        const int64_t grid = (a.n_blocks + G - 1) / G;
-        constexpr bool CAN_DY = (M == 2 || M == 4) && K % M == 0;
-        if constexpr (CAN_DY) {
-            if (a.dyb == M) {
-                hipLaunchKernelGGL((k_encode_hash_pipe<K, M, G, T, NT, CW, STAMP, M>), dim3((unsigned)grid), dim3(NT),
-                                   0, s, a);
-                return;
-            }
-        }
-        hipLaunchKernelGGL((k_encode_hash_pipe<K, M, G, T, NT, CW, STAMP>), dim3((unsigned)grid), dim3(NT), 0, s, a);
-    } else {
-        launch_fused<K, M, G, T, 1, CW>(a, s);
-    }
-}
-
-// Pair-form fused kernel: 2 threads per hash chain, G = stripes so 2*G*R fills whole
-// wavefronts (RS(8+4): G = 8, 192 threads).
-template <int R>
-constexpr int pick_G2() {
-    int g = 32 / gcd_c(R, 32);
-    while (g > 1 && 2 * g * R > 512) g /= 2;
-    while (2 * g * R < 192) g *= 2;
-    return g;
-}
-
-template <int K, int M, int T, int NBUF, int CW, bool STAMP = false>
-static void launch_pair(const EncArgs& a, hipStream_t s) {
-    constexpr int R = K + M;
-    constexpr int G = pick_G2<R>();
-    constexpr int NT = round64(2 * G * R);
-    static_assert(T % CW == 0 && T % 32 == 0, "tile");
-    const int64_t grid = (a.n_blocks + G - 1) / G;
-    constexpr bool CAN_DY = (M == 2 || M == 4) && K % M == 0;
-    if constexpr (CAN_DY) {
-        if (a.dyb == M) {
-            hipLaunchKernelGGL((k_encode_hash<K, M, G, T, NBUF, NT, CW, 1, false, STAMP, M, true>), dim3((unsigned)grid),
-                               dim3(NT), 0, s, a);
-            return;
-        }
-    }
-    hipLaunchKernelGGL((k_encode_hash<K, M, G, T, NBUF, NT, CW, 1, false, STAMP, 0, true>), dim3((unsigned)grid),
-                       dim3(NT), 0, s, a);
-}
-
-template <int K, int M, int ABL, int T = 384, int CW = 8, int NBUF = 1, int PF = 1>
-static void launch_ablation(const EncArgs& a, hipStream_t s) {
-    constexpr int R = K + M;
-    constexpr int G = pick_G<R>();
-    constexpr int NT = round64(4 * G * R);
-    const int64_t grid = (a.n_blocks + G - 1) / G;
-    constexpr int DY = ((M == 2 || M == 4) && K % M == 0) ? M : 0;
-    hipLaunchKernelGGL((k_encode_hash<K, M, G, T, NBUF, NT, CW, PF, false, false, DY, false, ABL>), dim3((unsigned)grid),
-                       dim3(NT), 0, s, a);
-}
-
-// Experimental variants for the headline shapes; returns the path or PATH_NONE.
-template <int K, int M>
-static int launch_variant(int v, const EncArgs& a, hipStream_t s) {
-    constexpr int R = K + M;
-    constexpr int G = pick_G<R>();
-    switch (v) {
-        case 1: launch_fused<K, M, G, 256, 2, 16>(a, s); return PATH_FIRSTGEN;
-        case 2: launch_fused<K, M, G, 768, 1, 16>(a, s); return PATH_FIRSTGEN;
-        case 3: launch_fused<K, M, G, 384, 2, 8>(a, s); return PATH_FIRSTGEN;
-        case 4: launch_fused<K, M, G, 192, 2, 4>(a, s); return PATH_FIRSTGEN;
-        case 5: launch_fused<K, M, G, 384, 1, 8>(a, s); return PATH_FIRSTGEN;
-        case 6: launch_fused<K, M, G, 768, 2, 16>(a, s); return PATH_FIRSTGEN;
-        case 7: launch_fused<K, M, G, 512, 2, 16>(a, s); return PATH_FIRSTGEN;
-        case 8: launch_fused<K, M, G, 192, 1, 4>(a, s); return PATH_FIRSTGEN;
-        case 9: launch_fused<K, M, G, 384, 1, 8, 2>(a, s); return PATH_FIRSTGEN;
-        case 10: launch_fused<K, M, G, 384, 1, 8, 2, true>(a, s); return PATH_FIRSTGEN;
-        case 11: launch_fused<K, M, G, 256, 2, 16, 2>(a, s); return PATH_FIRSTGEN;
-        case 12: launch_fused<K, M, G, 192, 2, 4, 2>(a, s); return PATH_FIRSTGEN;
-        case 13: launch_fused<K, M, G, 768, 1, 16, 2>(a, s); return PATH_FIRSTGEN;
-        case 14: launch_fused<K, M, G, 384, 1, 8, 1, true>(a, s); return PATH_FIRSTGEN;
-        case 15: launch_fused<K, M, G, 384, 1, 8, 3>(a, s); return PATH_FIRSTGEN;
-        case 16: launch_fused<K, M, G, 192, 1, 4, 3>(a, s); return PATH_FIRSTGEN;
-        case 17: launch_fused<K, M, G, 384, 1, 8, 1, false, true>(a, s); return PATH_FIRSTGEN;
-        case 18: launch_fused<K, M, G, 256, 2, 16, 1, false, true>(a, s); return PATH_FIRSTGEN;
-        case 20: launch_pipe<K, M, G, 384, 8>(a, s); return PATH_FIRSTGEN;
-        case 21: launch_pipe<K, M, G, 192, 4>(a, s); return PATH_FIRSTGEN;
-        case 22: launch_pipe<K, M, G, 256, 8>(a, s); return PATH_FIRSTGEN;
-        case 23: launch_pipe<K, M, G, 320, 8>(a, s); return PATH_FIRSTGEN;
-        case 24: launch_pipe<K, M, G, 384, 8, true>(a, s); return PATH_FIRSTGEN;
-        case 30: launch_pair<K, M, 384, 1, 16>(a, s); return PATH_FIRSTGEN;
-        case 31: launch_pair<K, M, 384, 2, 16>(a, s); return PATH_FIRSTGEN;
-        case 32: launch_pair<K, M, 192, 2, 8>(a, s); return PATH_FIRSTGEN;
-        case 33: launch_pair<K, M, 256, 1, 16>(a, s); return PATH_FIRSTGEN;
-        case 34: launch_pair<K, M, 192, 1, 8>(a, s); return PATH_FIRSTGEN;
-        case 41: launch_ablation<K, M, 1>(a, s); return PATH_FIRSTGEN;
-        case 42: launch_ablation<K, M, 2>(a, s); return PATH_FIRSTGEN;
-        case 43: launch_ablation<K, M, 3>(a, s); return PATH_FIRSTGEN;
-        case 44: launch_ablation<K, M, 4>(a, s); return PATH_FIRSTGEN;
-        case 45: launch_ablation<K, M, 1, 768, 16>(a, s); return PATH_FIRSTGEN;
-        case 46: launch_ablation<K, M, 1, 384, 8, 1, 2>(a, s); return PATH_FIRSTGEN;
-        case 47: launch_ablation<K, M, 3, 768, 16>(a, s); return PATH_FIRSTGEN;
-        case 48: launch_ablation<K, M, 4, 768, 16>(a, s); return PATH_FIRSTGEN;
-        default: return launch_ehx(v, a, s);
-    }
-}
-#endif  // ZS3_DIAG
 
 template <int K, int M>
 static hipError_t run_encode_fast(const EncArgs& a, hipStream_t s, int* path) {
@@ -1565,14 +1277,9 @@ static hipError_t run_encode_fast(const EncArgs& a, hipStream_t s, int* path) {
             launch_encode_lat<K, M>(a, s);
             p = PATH_LATENCY;
         }
-        if constexpr ((K == 8 && M == 4) || (K == 4 && M == 2) || (K == 16 && M == 4)) {
-            if (fv > 0 && p == PATH_NONE) p = launch_variant<K, M>(fv, a, s);
-        }
-        if constexpr ((K == 12 || K == 4) && M == 4) {
-            // the RS(12+4) unaligned-row shapes at aligned rows (memory-pattern A/B); the
-            // RS(4+4) candidates 369-371
-            if (fv >= 330 && p == PATH_NONE) p = launch_ehx(fv, a, s);
-        }
+        // the encode variants of fused_v2_diag.hip (PATH_NONE where one does not apply:
+        // the first-generation launch below then serves the call)
+        if (fv > 0 && p == PATH_NONE) p = launch_ehx(fv, a, s);
 #endif
         // Dyadic shapes (RS(4+2), RS(8+4), RS(16+4), ...): the second-generation
         // kernels of fused_v2.hip pick their launch shape from (k, m, n_blocks).
@@ -1632,8 +1339,7 @@ hipError_t launch_encode(const EncArgs& a, hipStream_t s, int* path) {
     // RS(2+2) / RS(4+3)) on the warp-specialised kernel with a general matrix
     // (fused_v2_gen.hip) once the batch fills the chip (a workgroup takes 8-16 stripes);
     // smaller batches keep the latency-bound paths below.
-    if (a.sums && (a.variant == 0 || (ZS3_DIAG && a.variant >= 340 && a.variant <= 346)) && a.n_blocks >= 1024 &&
-        has_gen_encode(a.k, a.m)) {
+    if (a.sums && a.variant == 0 && a.n_blocks >= 1024 && has_gen_encode(a.k, a.m)) {
         const int p = launch_ehx_gen(a, s);
         if (p != PATH_NONE) {
             if (path) *path = p;
@@ -1650,8 +1356,8 @@ hipError_t launch_encode(const EncArgs& a, hipStream_t s, int* path) {
 #undef X
     // fused encode + sums at shard sizes that are not a multiple of 16 (RS(12+4) on
     // 1 MiB blocks: S = 87 382)
-    // (diagnostics: the RS(12+4) UA variants of fused_v2_km124.hip, same guard)
-    if (a.sums && a.dyb && (a.variant == 0 || (ZS3_DIAG && ((a.variant >= 100 && a.variant < 200) || a.variant >= 330)))) {
+    // (diagnostics: the RS(12+4) unaligned-row variants of fused_v2_diag.hip, same guard)
+    if (a.sums && a.dyb && (a.variant == 0 || (ZS3_DIAG && a.variant >= 300))) {
         const int p = a.variant == 0 ? launch_ehx_ua(a, s) : launch_ehx(a.variant, a, s);
         if (p != PATH_NONE) {
             if (path) *path = p;
@@ -1698,27 +1404,6 @@ static hipError_t run_rec_fast(const RecArgs& a, hipStream_t s) {
     const int64_t cols = (a.S + 15) >> 4;
     const unsigned gx = (unsigned)((cols + 255) / 256);
     const unsigned gy = (unsigned)(a.n_blocks < 65535 ? a.n_blocks : 65535);
-#if ZS3_DIAG
-    if (a.e <= 2 && (a.variant == 220 || a.variant == 221)) {
-        // 2 or 4 columns per thread, all loads issued before the products (measured
-        // slower: 1.04-1.06 vs 1.00 ms, scripts/rec_ab.py)
-        const int nc = a.variant == 220 ? 2 : 4;
-        const unsigned gx2 = (unsigned)((cols + 256 * nc - 1) / (256 * nc));
-        if (nc == 2)
-            hipLaunchKernelGGL((k_reconstruct<K, 2, 2>), dim3(gx2, gy), dim3(256), 0, s, a);
-        else
-            hipLaunchKernelGGL((k_reconstruct<K, 2, 4>), dim3(gx2, gy), dim3(256), 0, s, a);
-        return hipGetLastError();
-    }
-    // 222: the default launch with plain (temporal) loads and stores
-    if (a.variant == 222) {
-        if (a.e <= 2)
-            hipLaunchKernelGGL((k_reconstruct<K, 2>), dim3(gx, gy), dim3(256), 0, s, a);
-        else
-            hipLaunchKernelGGL((k_reconstruct<K, 4>), dim3(gx, gy), dim3(256), 0, s, a);
-        return hipGetLastError();
-    }
-#endif
     // Default: non-temporal survivor loads and rebuilt-row stores (each byte is touched
     // once): RS(8+4) 4096 x 1 MiB {0,5} 1.016 -> 0.93 ms, {2,10} 0.905 -> 0.823 ms
     // (profiles/r02/ab_reconstruct_nt.jsonl).  Needs 16-byte aligned rows.
@@ -1805,24 +1490,6 @@ hipError_t launch_reconstruct(const RecArgs& a, hipStream_t s, int* path) {
 
 template <int K, int EMAX, bool HOUT>
 static hipError_t run_vr(const VrArgs& a, hipStream_t s) {
-#if ZS3_DIAG
-    // Variant 201: 16 stripes per workgroup, one workgroup per CU (LDS >= 80 KiB + 1).
-    // Measured SLOWER than the default on RS(8+4) 4096 x 1 MiB (verify 1.09 vs 0.84 ms,
-    // verify+rebuild 1.57 vs 1.40, heal 1.69 vs 1.50; scripts/get_ab.py): at 2 waves per
-    // SIMD this kernel, unlike the encode, is short of loads in flight.
-    using Big = VrShape<K, EMAX, HOUT, 16>;
-    if constexpr (Big::NT <= 1024) {
-        if (a.n_blocks >= 16 * 256 && a.variant == 201) {
-            auto kern = k_verify_reconstruct<K, EMAX, HOUT, 16>;
-            constexpr size_t dyn = Big::TILE > 82 * 1024 ? Big::TILE : 82 * 1024;
-            hipError_t e = ensure_dyn_lds((const void*)kern, dyn);
-            if (e != hipSuccess) return e;
-            const int64_t grid = (a.n_blocks + Big::G - 1) / Big::G;
-            hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(Big::NT), dyn, s, a);
-            return hipGetLastError();
-        }
-    }
-#endif
     using Sh = VrShape<K, EMAX, HOUT>;
     static_assert(Sh::TILE <= 65536, "default GET tile fits the default LDS limit");
     const int64_t grid = (a.n_blocks + Sh::G - 1) / Sh::G;
@@ -1830,25 +1497,12 @@ static hipError_t run_vr(const VrArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-// HighwayHash-256 of the rebuilt rows of every block of a GET / heal batch (a heal's
-// new bitrot sums) with the standalone hash kernel, one launch per rebuilt row.
-static hipError_t hash_rebuilt_rows(const VrArgs& a, hipStream_t s) {
-    const int R = a.k + a.m;
-    for (int i = 0; i < a.e; ++i) {
-        const int row = a.h_rows[a.k + i];
-        HashArgs h{};
-        h.msgs = a.shards + (int64_t)row * a.S;
-        h.stride = a.block_stride;
-        h.len = a.S;
-        h.n = a.n_blocks;
-        h.sums = a.sums_out + (int64_t)row * 32;
-        h.sum_stride = (int64_t)R * 32;
-        h.ids = a.ids;
-        for (int q = 0; q < 4; ++q) h.key[q] = a.key[q];
-        hipError_t e = launch_hash(h, s);
-        if (e != hipSuccess) return e;
-    }
-    return hipSuccess;
+// The product GET / heal dispatch serves variant 0 and, in the diagnostics build, the
+// variants that change a product shape's memory policy or layout (launch_vr_ws_t in
+// fused_v2.hpp: 246 plain loads, 247 64-bit addresses, 420 conflict-free LDS stride,
+// 421 XCD-region workgroup order).
+static bool product_get_variant(int v) {
+    return v == 0 || (ZS3_DIAG && (v == 246 || v == 247 || v == 420 || v == 421));
 }
 
 // GET / heal small-batch path: k_reconstruct rebuilds the missing rows, then one chain
@@ -1894,32 +1548,15 @@ static hipError_t run_vr_k(const VrArgs& a, hipStream_t s, int* path) {
     }
     // Default for the RS(8+4)-, RS(4+2)- and RS(16+4)-shaped GETs: the warp-specialised
     // k_vr_ws (fused_v2.hip): RS(8+4) verify 0.85 -> 0.70 ms, verify + rebuild 2
-    // 1.41 -> 1.13 ms on 4096 x 1 MiB (scripts/get_ab.py).  Variants 200-209 (diagnostics)
-    // force the first-generation kernel.
-    // diagnostics 231: the product dispatch without the latency path
-    // diagnostics 240: the product dispatch without that path, batched scalar tables
-    const int wv = (ZS3_DIAG && (a.variant == 231 || a.variant == 240 || a.variant == 241 || a.variant == 246 ||
-                                  a.variant == 247)) ? 0 : a.variant;
-    if (wv == 0 || (ZS3_DIAG && ((wv >= 210 && wv <= 219) || wv == 232 || wv == 242 || (wv >= 250 && wv <= 263) ||
-                                    (wv >= 270 && wv <= 272))))
-        if (launch_vr_ws(wv, a, s)) {
+    // 1.41 -> 1.13 ms on 4096 x 1 MiB (scripts/get_ab.py).  Diagnostics: 231 = the
+    // product dispatch without the latency path; the variants of the product GET shapes
+    // (product_get_variant) reach launch_vr_ws_t through the product dispatch; any other
+    // variant runs the first-generation kernel.
+    if (product_get_variant(a.variant) || (ZS3_DIAG && a.variant == 231))
+        if (launch_vr_ws(0, a, s)) {
             if (path) *path = PATH_WS;
             return hipGetLastError();
         }
-    // Diagnostics variant 218: heal split into the k_vr_ws GET rebuild and the standalone
-    // hash kernel over the e rebuilt rows.  Measured SLOWER than the fused kernels
-    // (RS(16+4) heal 2: 1.12 vs 0.95 ms, heal 4: 1.87 vs 1.32; profiles/r02/get_ab.txt):
-    // e*n_blocks serial chains are too few to hide the hash kernel's load latency.
-    if (ZS3_DIAG && a.sums_out && a.e > 0 && a.h_rows && a.variant == 218) {
-        VrArgs g = a;
-        g.sums_out = nullptr;
-        if (launch_vr_ws(0, g, s)) {
-            hipError_t e = hipGetLastError();
-            if (e == hipSuccess) e = hash_rebuilt_rows(a, s);
-            if (path) *path = PATH_WS;
-            return e;
-        }
-    }
     if (path) *path = PATH_FIRSTGEN;
     const bool hout = a.sums_out != nullptr;
     if (a.e == 0) return run_vr<K, 0, false>(a, s);
@@ -1933,8 +1570,7 @@ hipError_t launch_verify_reconstruct(const VrArgs& a, hipStream_t s, int* path) 
     // Server-default geometries whose k is not 4, 8, 12 or 16 (RS(2+2), (3+2), (5+4),
     // (6+4), ...; fused_v2_get_gen.hip): rebuild / heal on the warp-specialised kernel
     // in one launch (4096 x 1 MiB: see that file); small batches keep the launches below
-    if ((a.variant == 0 || (ZS3_DIAG && (a.variant == 350 || a.variant == 351))) && a.e >= 1 && a.e <= 4 &&
-        a.n_blocks >= 1024 && launch_vr_ws_gen(a, s)) {
+    if (product_get_variant(a.variant) && a.e >= 1 && a.e <= 4 && a.n_blocks >= 1024 && launch_vr_ws_gen(a, s)) {
         if (path) *path = PATH_WS;
         return hipGetLastError();
     }
@@ -1953,8 +1589,7 @@ hipError_t launch_verify_reconstruct(const VrArgs& a, hipStream_t s, int* path) 
     // RS(12+4) on 1 MiB blocks (unaligned rows): the warp-specialised kernel in UA mode
     // (diagnostics 97: the any-geometry launches below)
     if (a.e <= 4 && a.k == 12 && !(ZS3_DIAG && a.variant == 97)) {
-        const int wv = (ZS3_DIAG && a.variant >= 264 && a.variant <= 269) ? a.variant : 0;  // diagnostics shapes
-        if (launch_vr_ws(wv, a, s)) {
+        if (launch_vr_ws(0, a, s)) {
             if (path) *path = PATH_WS;
             return hipGetLastError();
         }

@@ -168,8 +168,6 @@ bool has_gen_encode(int k, int m);
 // Warp-specialised GET / heal for the same geometries (fused_v2_get_gen.hip); false when
 // (k, e) has no instance or the layout does not fit.
 bool launch_vr_ws_gen(const VrArgs& a, hipStream_t s);
-// LDS-DMA fused encode (fused_dma.hip); PATH_NONE when the shape / layout does not fit.
-int launch_ehx_dma(int v, const EncArgs& a, hipStream_t s);
 // Warp-specialised GET / heal pass (fused_v2.hip); false if the shape has no instance.
 bool launch_vr_ws(int v, const VrArgs& a, hipStream_t s);
 

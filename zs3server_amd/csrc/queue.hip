@@ -52,6 +52,7 @@
 #include <vector>
 
 #include "../../include/zs3gpu.h"
+#include "queue_policy.hpp"
 
 bool zs3i_pinned(const void* p, size_t n);  // zs3gpu.hip: inside a live zs3_host_alloc range
 bool zs3i_pinned_map(const void* p, size_t n, void** dev);  // ... and its device-side address
@@ -65,8 +66,10 @@ struct Slot;
 
 }  // namespace
 
+struct DevQ;
+
 struct zs3_req {
-    zs3_queue* q = nullptr;
+    DevQ* q = nullptr;
     Slot* slot = nullptr;
     int lane = ENC;
     int pos = 0;
@@ -112,12 +115,15 @@ struct Slot {
 
 }  // namespace
 
-struct zs3_queue {
+// One device's part of a queue: its lanes, staging slots, streams and threads.  A queue
+// (zs3_queue, below) holds one per listed device and assigns every submitted block to
+// one of them (zs3q::pick_device); each device batches its own blocks.
+struct DevQ {
     const zs3_codec* c = nullptr;
     int k = 0, m = 0, R = 0;
     int64_t B = 0, S = 0, E = 0;  // block size, full shard size, bytes per position
     int device = 0;
-    int cap = 128;                // positions per slot
+    int cap = 64;                 // positions per slot = the largest batch (zs3q::slot_blocks)
     int max_wait_us = 200;
     int nslots = 4;
     // Pinned callers (round 4; ZS3_QUEUE_ZC=<mode> selects another for A/B measurements,
@@ -148,8 +154,8 @@ struct zs3_queue {
     int inflight[NLANE] = {0, 0, 0};
     int inflight_blocks[NLANE] = {0, 0, 0};  // blocks of the launched, unfinished slots
     std::vector<Slot*> sealed[NLANE];         // closed to new blocks, waiting for copiers
-    int pipe_cap = 64;                        // ready_to_close: blocks per 64 MiB of input
     int pipe_pct = 50;                        // seal at this % of the live blocks (ZS3_QUEUE_PIPE_PCT)
+    std::atomic<int> live[NLANE]{};           // blocks assigned to this device, not yet finished
     std::deque<Slot*> launched;
     bool flush = false;
     bool stop = false;       // dispatcher: drain the open slots and exit
@@ -177,13 +183,13 @@ int map_hip(hipError_t e) { return e == hipSuccess ? ZS3_OK : (e == hipErrorOutO
 // on return, but the allocation itself runs unlocked so the dispatcher and completer
 // keep serving the other lanes; other submitters of this lane wait for it).  A failed
 // allocation leaves the lane unallocated, so a later submit retries.
-int ensure_lane(zs3_queue* q, std::unique_lock<std::mutex>& lk, int lane) {
+int ensure_lane(DevQ* q, std::unique_lock<std::mutex>& lk, int lane) {
     for (;;) {
-        if (q->lane_state[lane] == zs3_queue::LANE_READY) return ZS3_OK;
-        if (q->lane_state[lane] == zs3_queue::LANE_NONE) break;
+        if (q->lane_state[lane] == DevQ::LANE_READY) return ZS3_OK;
+        if (q->lane_state[lane] == DevQ::LANE_NONE) break;
         q->cv_space.wait(lk);
     }
-    q->lane_state[lane] = zs3_queue::LANE_INIT;
+    q->lane_state[lane] = DevQ::LANE_INIT;
     const size_t bytes = q->slot_bytes(lane);
     const int nslots = q->nslots, cap = q->cap, device = q->device;
     lk.unlock();
@@ -210,7 +216,7 @@ int ensure_lane(zs3_queue* q, std::unique_lock<std::mutex>& lk, int lane) {
     (void)hipSetDevice(prev);
     lk.lock();
     if (rc == ZS3_OK) q->slots[lane] = std::move(v);
-    q->lane_state[lane] = rc == ZS3_OK ? zs3_queue::LANE_READY : zs3_queue::LANE_NONE;
+    q->lane_state[lane] = rc == ZS3_OK ? DevQ::LANE_READY : DevQ::LANE_NONE;
     q->cv_space.notify_all();
     return rc;
 }
@@ -297,10 +303,10 @@ void for_runs(const std::vector<uint8_t>& skip, int n, F f) {
     }
 }
 
-int pipe_size(const zs3_queue* q, const Slot* s, int lane);
+int pipe_size(const DevQ* q, const Slot* s, int lane);
 
 // Reserve a position for one block in the lane's open slot (caller holds lk).
-int reserve(zs3_queue* q, std::unique_lock<std::mutex>& lk, zs3_req* r, bool full) {
+int reserve(DevQ* q, std::unique_lock<std::mutex>& lk, zs3_req* r, bool full) {
     int rc = ensure_lane(q, lk, r->lane);
     if (rc) return rc;
     for (;;) {
@@ -339,13 +345,13 @@ int reserve(zs3_queue* q, std::unique_lock<std::mutex>& lk, zs3_req* r, bool ful
     }
 }
 
-void copy_in_done(zs3_queue* q, Slot* s) {
+void copy_in_done(DevQ* q, Slot* s) {
     std::lock_guard<std::mutex> g(q->mu);
     if (--s->copying == 0) q->cv_disp.notify_one();
 }
 
 // ---- launch of a closed slot (dispatcher thread, no lock held) ----------------------
-void launch_slot(zs3_queue* q, Slot* s) {
+void launch_slot(DevQ* q, Slot* s) {
     hipStream_t st = s->stream;
     const int k = q->k, m = q->m, R = q->R;
     const int64_t E = q->E, S = q->S;
@@ -479,20 +485,19 @@ void launch_slot(zs3_queue* q, Slot* s) {
 }
 
 // Blocks at which the open slot closes for pipelining (ready_to_close); caller holds mu.
-int pipe_size(const zs3_queue* q, const Slot* s, int lane) {
-    const int live = (int)s->reqs.size() + q->inflight_blocks[lane];
-    return std::max(8, std::min((live * q->pipe_pct + 99) / 100, q->pipe_cap));
+int pipe_size(const DevQ* q, const Slot* s, int lane) {
+    return zs3q::seal_blocks((int)s->reqs.size() + q->inflight_blocks[lane], q->pipe_pct, q->cap);
 }
 
-bool ready_to_close(zs3_queue* q, Slot* s, int lane, Clock::time_point now) {
+bool ready_to_close(DevQ* q, Slot* s, int lane, Clock::time_point now) {
     if (s->reqs.empty()) return false;
     if (s->front + s->back == q->cap || q->flush || q->stop) return true;
     // Pipelining cap (round 4): T synchronous submitters keep about T blocks live (open
     // slot + in flight); closing the slot at half of them keeps two batches alternating,
     // one's H2D under the other's kernel and D2H, instead of one batch of all of them
     // (1 MiB RS(8+4), 64 submitters: 29.9-30.5 GiB/s at batches of 32 vs 21-24 at 64-128;
-    // 256 submitters: 33-35 at 64; profiles/r04/queue_ab3.jsonl), at most 64 MiB of input
-    // per batch
+    // 256 submitters: 33-35 at 64; profiles/r04/queue_ab3.jsonl), at most the slot's
+    // size (zs3q::slot_blocks: 64 MiB of input)
     if (s->front + s->back >= pipe_size(q, s, lane)) return true;
     // batch while busy: launch at once while fewer than slots-1 batches are in flight
     // (a small batch is bound by one hash chain's latency, ~0.5 ms for 128 KiB shards,
@@ -502,7 +507,7 @@ bool ready_to_close(zs3_queue* q, Slot* s, int lane, Clock::time_point now) {
     return now - s->opened >= std::chrono::microseconds(q->max_wait_us);
 }
 
-void dispatcher(zs3_queue* q) {
+void dispatcher(DevQ* q) {
     (void)hipSetDevice(q->device);
     std::unique_lock<std::mutex> lk(q->mu);
     for (;;) {
@@ -557,7 +562,7 @@ void dispatcher(zs3_queue* q) {
 }
 
 // Copy one finished block's results from the pinned slot into its caller's buffers.
-void finish_req(zs3_queue* q, Slot* s, zs3_req* r) {
+void finish_req(DevQ* q, Slot* s, zs3_req* r) {
     int64_t rc = s->launch_status != ZS3_OK ? s->launch_status : r->status;
     const size_t o = (size_t)r->pos * q->E;
     const int k = q->k, R = q->R;
@@ -586,10 +591,11 @@ void finish_req(zs3_queue* q, Slot* s, zs3_req* r) {
         }
     }
     r->result = rc;
+    q->live[r->lane].fetch_sub(1, std::memory_order_relaxed);
 }
 
 // Drop one pending block of the slot; the last one frees the slot (caller holds no lock).
-void finish_one(zs3_queue* q, Slot* s) {
+void finish_one(DevQ* q, Slot* s) {
     if (s->pending.fetch_sub(1) != 1) return;
     std::lock_guard<std::mutex> g(q->mu);
     s->reqs.clear();
@@ -600,7 +606,7 @@ void finish_one(zs3_queue* q, Slot* s) {
     q->cv_disp.notify_one();  // batch-while-busy: the next open slot may go now
 }
 
-void completer(zs3_queue* q) {
+void completer(DevQ* q) {
     std::unique_lock<std::mutex> lk(q->mu);
     for (;;) {
         q->cv_comp.wait(lk, [&] { return !q->launched.empty() || q->comp_stop; });
@@ -638,14 +644,11 @@ void completer(zs3_queue* q) {
     }
 }
 
-}  // namespace
-
-extern "C" {
-
-int zs3_queue_new(const zs3_codec* c, const zs3_queue_opts* opts, zs3_queue** out) {
-    if (!c || !out) return ZS3_ERR_INVALID_ARG;
+// One device's queue part: validated codec parameters, its own threads; the slots of a
+// lane are allocated on the lane's first submit (ensure_lane).
+int devq_new(const zs3_codec* c, int device, const zs3_queue_opts* opts, DevQ** out) {
     *out = nullptr;
-    auto* q = new zs3_queue();
+    auto* q = new DevQ();
     q->c = c;
     if (zs3_codec_params(c, &q->k, &q->m, &q->B) != ZS3_OK) {
         delete q;
@@ -656,17 +659,19 @@ int zs3_queue_new(const zs3_codec* c, const zs3_queue_opts* opts, zs3_queue** ou
     q->E = (int64_t)q->R * q->S;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) dev = 0;
-    q->device = dev;
+    q->device = device;
     if (opts) {
-        if (opts->device >= 0) q->device = opts->device;
-        if (opts->max_batch > 0) q->cap = opts->max_batch;
         if (opts->max_wait_us > 0) q->max_wait_us = opts->max_wait_us;
         if (opts->slots > 0) q->nslots = opts->slots;
     }
     if (q->nslots < 2) q->nslots = 2;
-    q->pipe_cap = (int)std::max<int64_t>(4, std::min<int64_t>(q->cap, ((int64_t)64 << 20) / std::max<int64_t>(1, q->B)));
+    q->cap = zs3q::slot_blocks(opts ? opts->max_batch : 0, q->B);
+#if ZS3_DIAG
+    // A/B switches of the diagnostics build only (a stray variable never changes a
+    // production server's transport: ADVICE r04)
     if (const char* e = std::getenv("ZS3_QUEUE_ZC")) q->zc_mode = std::max(0, std::min(3, std::atoi(e)));
     if (const char* e = std::getenv("ZS3_QUEUE_PIPE_PCT")) q->pipe_pct = std::max(10, std::min(100, std::atoi(e)));
+#endif
     int prev = dev;
     if (hipSetDevice(q->device) != hipSuccess) {
         delete q;
@@ -679,7 +684,7 @@ int zs3_queue_new(const zs3_codec* c, const zs3_queue_opts* opts, zs3_queue** ou
     return ZS3_OK;
 }
 
-void zs3_queue_free(zs3_queue* q) {
+void devq_free(DevQ* q) {
     if (!q) return;
     {
         std::lock_guard<std::mutex> g(q->mu);
@@ -704,13 +709,10 @@ void zs3_queue_free(zs3_queue* q) {
     delete q;
 }
 
-int zs3_queue_submit_encode(zs3_queue* q, uint8_t* h_buf, int64_t len, int64_t cap, uint8_t* h_sums,
-                            zs3_req** req) {
-    if (!q || !req || len < 0 || len > q->B || (len > 0 && !h_buf)) return ZS3_ERR_INVALID_ARG;
-    *req = nullptr;
-    if (len == 0) return ZS3_OK;  // EncodeData len 0: k+m empty shards, nothing to do
+// Submits on one device (the caller validated the arguments and counted the block in
+// q->live[lane]; a failed reserve uncounts it).
+int devq_submit_encode(DevQ* q, uint8_t* h_buf, int64_t len, uint8_t* h_sums, zs3_req** req) {
     const int64_t Sb = (len + q->k - 1) / q->k;
-    if (cap < (int64_t)q->R * Sb) return ZS3_ERR_INVALID_ARG;
     auto* r = new zs3_req();
     r->q = q;
     r->lane = ENC;
@@ -724,6 +726,7 @@ int zs3_queue_submit_encode(zs3_queue* q, uint8_t* h_buf, int64_t len, int64_t c
         std::unique_lock<std::mutex> lk(q->mu);
         const int rc = reserve(q, lk, r, len == q->B);
         if (rc) {
+            q->live[ENC].fetch_sub(1, std::memory_order_relaxed);
             delete r;
             return rc;
         }
@@ -757,13 +760,8 @@ int zs3_queue_submit_encode(zs3_queue* q, uint8_t* h_buf, int64_t len, int64_t c
     return ZS3_OK;
 }
 
-int zs3_queue_submit_decode(zs3_queue* q, uint8_t* h_shards, int64_t shard_len, const uint8_t* h_present,
-                            int data_only, const uint8_t* h_expect, int32_t* h_bad, uint8_t* h_sums_out,
-                            zs3_req** req) {
-    if (!q || !req || !h_present || shard_len < 0 || shard_len > q->S || (shard_len > 0 && !h_shards))
-        return ZS3_ERR_INVALID_ARG;
-    *req = nullptr;
-    if (shard_len == 0) return ZS3_ERR_SHARD_NO_DATA;
+int devq_submit_decode(DevQ* q, uint8_t* h_shards, int64_t shard_len, const uint8_t* h_present, int data_only,
+                       const uint8_t* h_expect, int32_t* h_bad, uint8_t* h_sums_out, zs3_req** req) {
     auto* r = new zs3_req();
     r->q = q;
     r->lane = data_only ? GET : HEAL;
@@ -779,6 +777,7 @@ int zs3_queue_submit_decode(zs3_queue* q, uint8_t* h_shards, int64_t shard_len, 
         std::unique_lock<std::mutex> lk(q->mu);
         const int rc = reserve(q, lk, r, shard_len == q->S);
         if (rc) {
+            q->live[r->lane].fetch_sub(1, std::memory_order_relaxed);
             delete r;
             return rc;
         }
@@ -817,9 +816,98 @@ int zs3_queue_submit_decode(zs3_queue* q, uint8_t* h_shards, int64_t shard_len, 
     return ZS3_OK;
 }
 
+}  // namespace
+
+// A queue: one DevQ per listed device (opts->devices, or the one opts->device), each with
+// its own slots, streams and threads; a submitted block goes to the device with the
+// fewest live blocks of its lane (zs3q::pick_device), so T concurrent callers spread
+// over the devices' PCIe links and HBM, and each device batches its own blocks.
+struct zs3_queue {
+    std::vector<DevQ*> devs;
+    std::atomic<unsigned> rr{0};  // rotating tie-break start
+
+    DevQ* pick(int lane) {
+        const int n = (int)devs.size();
+        if (n == 1) {
+            devs[0]->live[lane].fetch_add(1, std::memory_order_relaxed);
+            return devs[0];
+        }
+        int live[64];
+        for (int i = 0; i < n; ++i) live[i] = devs[(size_t)i]->live[lane].load(std::memory_order_relaxed);
+        DevQ* d = devs[(size_t)zs3q::pick_device(live, n, rr.fetch_add(1, std::memory_order_relaxed))];
+        d->live[lane].fetch_add(1, std::memory_order_relaxed);
+        return d;
+    }
+};
+
+extern "C" {
+
+int zs3_queue_new(const zs3_codec* c, const zs3_queue_opts* opts, zs3_queue** out) {
+    if (!c || !out) return ZS3_ERR_INVALID_ARG;
+    *out = nullptr;
+    int k = 0, m = 0;
+    int64_t B = 0;
+    if (zs3_codec_params(c, &k, &m, &B) != ZS3_OK) return ZS3_ERR_INVALID_ARG;
+    std::vector<int> devices;
+    if (opts && opts->n_devices > 0) {
+        if (!opts->devices || opts->n_devices > 64) return ZS3_ERR_INVALID_ARG;
+        for (int i = 0; i < opts->n_devices; ++i) {
+            if (opts->devices[i] < 0) return ZS3_ERR_INVALID_ARG;
+            devices.push_back(opts->devices[i]);
+        }
+    } else {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+        devices.push_back(opts && opts->device >= 0 ? opts->device : dev);
+    }
+    auto* q = new zs3_queue();
+    for (int d : devices) {
+        DevQ* dq = nullptr;
+        const int rc = devq_new(c, d, opts, &dq);
+        if (rc != ZS3_OK) {
+            for (DevQ* x : q->devs) devq_free(x);
+            delete q;
+            return rc;
+        }
+        q->devs.push_back(dq);
+    }
+    *out = q;
+    return ZS3_OK;
+}
+
+void zs3_queue_free(zs3_queue* q) {
+    if (!q) return;
+    for (DevQ* d : q->devs) devq_free(d);
+    delete q;
+}
+
+int zs3_queue_submit_encode(zs3_queue* q, uint8_t* h_buf, int64_t len, int64_t cap, uint8_t* h_sums,
+                            zs3_req** req) {
+    if (!q || !req || q->devs.empty()) return ZS3_ERR_INVALID_ARG;
+    const DevQ* d0 = q->devs[0];
+    if (len < 0 || len > d0->B || (len > 0 && !h_buf)) return ZS3_ERR_INVALID_ARG;
+    *req = nullptr;
+    if (len == 0) return ZS3_OK;  // EncodeData len 0: k+m empty shards, nothing to do
+    const int64_t Sb = (len + d0->k - 1) / d0->k;
+    if (cap < (int64_t)d0->R * Sb) return ZS3_ERR_INVALID_ARG;
+    return devq_submit_encode(q->pick(ENC), h_buf, len, h_sums, req);
+}
+
+int zs3_queue_submit_decode(zs3_queue* q, uint8_t* h_shards, int64_t shard_len, const uint8_t* h_present,
+                            int data_only, const uint8_t* h_expect, int32_t* h_bad, uint8_t* h_sums_out,
+                            zs3_req** req) {
+    if (!q || !req || q->devs.empty()) return ZS3_ERR_INVALID_ARG;
+    const DevQ* d0 = q->devs[0];
+    if (!h_present || shard_len < 0 || shard_len > d0->S || (shard_len > 0 && !h_shards)) return ZS3_ERR_INVALID_ARG;
+    *req = nullptr;
+    if (shard_len == 0) return ZS3_ERR_SHARD_NO_DATA;
+    return devq_submit_decode(q->pick(data_only ? GET : HEAL), h_shards, shard_len, h_present, data_only, h_expect,
+                              h_bad, h_sums_out, req);
+}
+
 int64_t zs3_req_wait(zs3_req* r) {
     if (!r) return ZS3_OK;  // the empty-block case returned no handle
-    zs3_queue* q = r->q;
+    DevQ* q = r->q;
     Slot* s = r->slot;  // not freed before r is finished
     bool own = false;
     {
@@ -840,20 +928,41 @@ int64_t zs3_req_wait(zs3_req* r) {
 
 int zs3_queue_flush(zs3_queue* q) {
     if (!q) return ZS3_ERR_INVALID_ARG;
-    std::lock_guard<std::mutex> g(q->mu);
-    q->flush = true;
-    q->cv_disp.notify_one();
+    for (DevQ* d : q->devs) {
+        std::lock_guard<std::mutex> g(d->mu);
+        d->flush = true;
+        d->cv_disp.notify_one();
+    }
     return ZS3_OK;
 }
 
 int zs3_queue_stats(const zs3_queue* q, int64_t* batches, int64_t* blocks) {
     if (!q) return ZS3_ERR_INVALID_ARG;
-    if (batches) *batches = q->n_batches.load();
-    if (blocks) *blocks = q->n_blocks.load();
+    int64_t b = 0, n = 0;
+    for (const DevQ* d : q->devs) {
+        b += d->n_batches.load();
+        n += d->n_blocks.load();
+    }
+    if (batches) *batches = b;
+    if (blocks) *blocks = n;
     return ZS3_OK;
 }
 
-int64_t zs3_queue_zero_copy_blocks(const zs3_queue* q) { return q ? q->n_zc.load() : ZS3_ERR_INVALID_ARG; }
+int zs3_queue_device_stats(const zs3_queue* q, int index, int* device, int64_t* batches, int64_t* blocks) {
+    if (!q || index < 0 || index >= (int)q->devs.size()) return ZS3_ERR_INVALID_ARG;
+    const DevQ* d = q->devs[(size_t)index];
+    if (device) *device = d->device;
+    if (batches) *batches = d->n_batches.load();
+    if (blocks) *blocks = d->n_blocks.load();
+    return ZS3_OK;
+}
+
+int64_t zs3_queue_zero_copy_blocks(const zs3_queue* q) {
+    if (!q) return ZS3_ERR_INVALID_ARG;
+    int64_t n = 0;
+    for (const DevQ* d : q->devs) n += d->n_zc.load();
+    return n;
+}
 
 int64_t zs3_queue_encode_data(zs3_queue* q, uint8_t* h_buf, int64_t len, int64_t cap, uint8_t* h_sums) {
     zs3_req* r = nullptr;

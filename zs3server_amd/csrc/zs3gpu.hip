@@ -188,15 +188,30 @@ struct PatternGroup {
     std::shared_ptr<RecPlan> plan;
     std::vector<int32_t> blocks;
     size_t ids_off = 0;  // offset of this group's ids in the call's device id list
+    // first block when the group's blocks are one ascending run b0, b0+1, ... (-1 if not):
+    // such a group launches on the shifted batch without an id list, so it takes the same
+    // instances as a single-pattern call (the buffer-addressed ones need no id list)
+    int64_t run0 = -1;
 };
+
+void mark_runs(std::vector<PatternGroup>& groups) {
+    for (auto& g : groups) {
+        g.run0 = -1;
+        if (g.blocks.empty()) continue;
+        bool run = true;
+        for (size_t i = 1; i < g.blocks.size() && run; ++i) run = g.blocks[i] == g.blocks[0] + (int32_t)i;
+        if (run) g.run0 = g.blocks[0];
+    }
+}
 
 // One upload of every launched group's block ids (see IdsStage).
 int upload_group_ids(std::vector<PatternGroup>& groups, bool skip_noop, hipStream_t s, int32_t** d_out) {
     *d_out = nullptr;
     size_t n = 0;
+    mark_runs(groups);
     for (auto& g : groups) {
         g.ids_off = n;
-        if (!g.blocks.empty() && !(skip_noop && g.plan->noop)) n += g.blocks.size();
+        if (!g.blocks.empty() && !(skip_noop && g.plan->noop) && g.run0 < 0) n += g.blocks.size();
     }
     if (n == 0) return ZS3_OK;
     const int d = current_device();
@@ -216,7 +231,7 @@ int upload_group_ids(std::vector<PatternGroup>& groups, bool skip_noop, hipStrea
         sp->cap[i] = bytes;
     }
     for (auto& g : groups)
-        if (!g.blocks.empty() && !(skip_noop && g.plan->noop))
+        if (!g.blocks.empty() && !(skip_noop && g.plan->noop) && g.run0 < 0)
             std::memcpy(sp->h[i] + g.ids_off, g.blocks.data(), g.blocks.size() * sizeof(int32_t));
     if (hipMallocAsync((void**)d_out, bytes, s) != hipSuccess) return ZS3_ERR_NOMEM;
     if (hipMemcpyAsync(*d_out, sp->h[i], bytes, hipMemcpyHostToDevice, s) != hipSuccess ||
@@ -449,9 +464,10 @@ int64_t zs3_bitrot_shard_file_size(int64_t size, int64_t shard_size) {
 // Encode: block b reads d_data + b*ds + [0, len) and writes d_parity + b*ps + [0, m*S);
 // blocks must not overlap (ds >= len, ps >= m*S when n > 1) and no parity row may land
 // on a data byte (the kernels read a tile's data rows before its parity rows are
-// written, but a later tile's data must survive).  Equal strides (the reference's
-// in-place Split layout, parity = data + k*S) are checked per period; distinct strides
-// (separate data / parity regions, as the queue's slots) as two disjoint spans.  The
+// written, but a later tile's data must survive).  Disjoint data and parity spans
+// (separate regions, as the queue's slots — whatever the strides, so k == m slots with
+// equal strides pass) are accepted first; overlapping spans only with equal strides (the
+// reference's in-place Split layout, parity = data + k*S), checked per period.  The
 // diagnostics build also accepts ds = ps = 0: every block aliased onto block 0
 // (timing-only L2-resident runs, scripts/sweep_variants.py SWEEP_ALIAS).
 static bool encode_layout_ok(const uint8_t* data, int64_t ds, int64_t len, int64_t n, const uint8_t* parity,
@@ -462,11 +478,10 @@ static bool encode_layout_ok(const uint8_t* data, int64_t ds, int64_t len, int64
     if (ds < 0 || ps < 0) return false;
     if (n > 1 && (ds < len || ps < mS)) return false;
     const int64_t off = (int64_t)((uintptr_t)parity - (uintptr_t)data);
-    if (n == 1 || ds != ps) {
-        const int64_t d_end = (n - 1) * ds + len, p_end = off + (n - 1) * ps + mS;
-        return p_end <= 0 || off >= d_end;
-    }
-    // equal strides: the parity rows of every block sit in the gap of one period
+    const int64_t d_end = (n - 1) * ds + len, p_end = off + (n - 1) * ps + mS;
+    if (p_end <= 0 || off >= d_end) return true;  // disjoint spans
+    if (n == 1 || ds != ps) return false;
+    // equal strides, interleaved spans: the parity rows of every block sit in the gap of one period
     const int64_t r = ((off % ds) + ds) % ds;
     return r >= len && r + mS <= ds;
 }
@@ -691,13 +706,13 @@ int zs3_reconstruct_batch_masks(const zs3_codec* cc, uint8_t* d_shards, int64_t 
         zs3k::RecArgs a{};
         rc = plan_device(c, g.plan.get(), &a.tables, &a.coef, &a.rows);
         if (rc) break;
-        a.shards = d_shards;
+        a.shards = g.run0 >= 0 ? d_shards + g.run0 * block_stride : d_shards;
         a.block_stride = block_stride;
         a.S = shard_len;
         a.n_blocks = (int64_t)g.blocks.size();
         a.k = c->k;
         a.e = g.plan->e;
-        a.ids = d_ids + g.ids_off;
+        a.ids = g.run0 >= 0 ? nullptr : d_ids + g.ids_off;
         a.variant = call_variant();
         rc = map_hip(zs3k::launch_reconstruct(a, s, &last));
         if (rc) break;
@@ -733,18 +748,19 @@ int zs3_verify_reconstruct_batch_masks(const zs3_codec* cc, uint8_t* d_shards, i
         zs3k::VrArgs a{};
         rc = plan_device(c, g.plan.get(), &a.tables, &a.coef, &a.rows);
         if (rc) break;
-        a.shards = d_shards;
+        const int64_t b0 = g.run0 >= 0 ? g.run0 : 0;
+        a.shards = d_shards + b0 * block_stride;
         a.block_stride = block_stride;
         a.S = shard_len;
         a.n_blocks = (int64_t)g.blocks.size();
         a.k = c->k;
         a.m = c->m;
         a.e = g.plan->noop ? 0 : g.plan->e;
-        a.expect = d_expect;
-        a.bad = d_bad;
-        a.sums_out = a.e > 0 ? d_sums_out : nullptr;
+        a.expect = d_expect + b0 * R * 32;
+        a.bad = d_bad + b0 * R;
+        a.sums_out = a.e > 0 && d_sums_out ? d_sums_out + b0 * R * 32 : nullptr;
         a.h_rows = g.plan->rows.data();
-        a.ids = d_ids + g.ids_off;
+        a.ids = g.run0 >= 0 ? nullptr : d_ids + g.ids_off;
         key_words(nullptr, a.key);
         a.variant = call_variant();
         rc = map_hip(zs3k::launch_verify_reconstruct(a, s, &last));
@@ -1061,6 +1077,173 @@ int stream_range(zs3_codec* c, int device, const uint8_t* src, int64_t b0, int64
     return rc;
 }
 
+// Streamed GET / heal of one object's blocks on one device (zs3_stream_decode): the
+// Erasure.Decode / Erasure.Heal block loops (erasure-decode.go:230-276, :287-332) as a
+// 3-slot pipeline of batches: H2D of batch i+1's survivor rows || the fused verify +
+// rebuild (+ heal sums) of batch i || D2H of batch i-1's rebuilt rows, flags and sums.
+// Stripe b is at h + b*E (E = (k+m)*S), row j at + j*S.  Pinned caller buffers move by
+// DMA, row by row across the batch (only rows some block of the batch has); pageable ones
+// are staged whole-stripe by helper threads, as stream_range does.
+int stream_vr_range(zs3_codec* c, uint8_t* h, int64_t nblk, const uint8_t* present, int data_only,
+                    const uint8_t* h_expect, int32_t* h_bad, uint8_t* h_sums_out, int32_t* status, int64_t NB,
+                    bool pinned, int cpu_threads) {
+    if (nblk <= 0) return ZS3_OK;
+    const int k = c->k, m = c->m, R = k + m;
+    const int64_t S = ceil_frac(c->block_size, k);
+    const int64_t E = (int64_t)R * S;
+    const bool heal = !data_only;
+    const bool hash_out = heal && h_sums_out;
+    constexpr int NS = 3;
+    struct Slot {
+        uint8_t* d = nullptr;    // NB stripes | NB*R*32 expected sums | NB*R int32 flags | NB*R*32 heal sums
+        uint8_t* hs = nullptr;   // pinned staging of NB stripes (pageable caller)
+        hipEvent_t in_done = nullptr, out_done = nullptr;
+        bool used = false;
+        std::future<int> fill, drain;
+    };
+    Slot sl[NS];
+    hipStream_t s_in = nullptr, s_comp = nullptr, s_out = nullptr;
+    hipEvent_t ev_in = nullptr, ev_comp = nullptr;
+    int rc = ZS3_OK, first_block_err = ZS3_OK;
+    auto chk = [&](hipError_t e) {
+        if (e != hipSuccess && rc == ZS3_OK) rc = map_hip(e);
+        return e == hipSuccess;
+    };
+    chk(hipStreamCreateWithFlags(&s_in, hipStreamNonBlocking));
+    chk(hipStreamCreateWithFlags(&s_comp, hipStreamNonBlocking));
+    chk(hipStreamCreateWithFlags(&s_out, hipStreamNonBlocking));
+    chk(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
+    chk(hipEventCreateWithFlags(&ev_comp, hipEventDisableTiming));
+    const size_t off_exp = (size_t)NB * E, off_bad = off_exp + (size_t)NB * R * 32, off_out = off_bad + (size_t)NB * R * 4;
+    const size_t dbytes = off_out + (size_t)NB * R * 32;
+    for (auto& x : sl) {
+        chk(hipMalloc(&x.d, dbytes));
+        if (!pinned) chk(hipHostMalloc(&x.hs, (size_t)NB * E, hipHostMallocDefault));
+        chk(hipEventCreateWithFlags(&x.in_done, hipEventDisableTiming));
+        chk(hipEventCreateWithFlags(&x.out_done, hipEventDisableTiming));
+    }
+    const int th = std::max(1, cpu_threads / 2);
+    const int64_t nbatch = (nblk + NB - 1) / NB;
+    // rows of a batch: `any_present` to upload, `any_rebuilt` to bring back
+    auto rows_of = [&](int64_t bb, int64_t nb, std::vector<uint8_t>& any_present, std::vector<uint8_t>& any_rebuilt) {
+        any_present.assign((size_t)R, 0);
+        any_rebuilt.assign((size_t)R, 0);
+        for (int64_t b = bb; b < bb + nb; ++b)
+            for (int j = 0; j < R; ++j) {
+                if (present[b * R + j]) any_present[(size_t)j] = 1;
+                else if (j < k || heal) any_rebuilt[(size_t)j] = 1;
+            }
+    };
+    auto start_fill = [&](int64_t i) {
+        Slot& x = sl[i % NS];
+        const int64_t bb = i * NB, nb = std::min(NB, nblk - bb);
+        const bool wait_prev = x.used;
+        hipEvent_t prev = x.in_done;
+        uint8_t* hs = x.hs;
+        x.fill = std::async(std::launch::async, [=]() -> int {
+            if (wait_prev && hipEventSynchronize(prev) != hipSuccess) return ZS3_ERR_DEVICE;
+            par_memcpy(hs, h + bb * E, (size_t)(nb * E), th);
+            return ZS3_OK;
+        });
+    };
+    if (!pinned && rc == ZS3_OK) start_fill(0);
+    std::vector<uint8_t> anyp, anyr;
+    for (int64_t i = 0; i < nbatch && rc == ZS3_OK; ++i) {
+        Slot& x = sl[i % NS];
+        const int64_t bb = i * NB, nb = std::min(NB, nblk - bb);
+        if (x.drain.valid()) {
+            const int e = x.drain.get();
+            if (e && rc == ZS3_OK) rc = e;
+        }
+        if (!pinned) {
+            const int e = x.fill.get();
+            if (e && rc == ZS3_OK) rc = e;
+        }
+        if (rc) break;
+        if (!pinned && i + 1 < nbatch) {
+            Slot& y = sl[(i + 1) % NS];
+            if (y.drain.valid()) {
+                const int e = y.drain.get();
+                if (e && rc == ZS3_OK) rc = e;
+            }
+            start_fill(i + 1);
+        }
+        rows_of(bb, nb, anyp, anyr);
+        if (x.used) chk(hipStreamWaitEvent(s_in, x.out_done, 0));
+        if (pinned) {
+            for (int j = 0; j < R; ++j)
+                if (anyp[(size_t)j])
+                    chk(hipMemcpy2DAsync(x.d + (size_t)j * S, (size_t)E, h + bb * E + (size_t)j * S, (size_t)E, (size_t)S,
+                                         (size_t)nb, hipMemcpyHostToDevice, s_in));
+        } else {
+            chk(hipMemcpyAsync(x.d, x.hs, (size_t)(nb * E), hipMemcpyHostToDevice, s_in));
+        }
+        if (h_expect)
+            chk(hipMemcpyAsync(x.d + off_exp, h_expect + bb * R * 32, (size_t)nb * R * 32, hipMemcpyHostToDevice, s_in));
+        else
+            chk(hipMemsetAsync(x.d + off_exp, 0, (size_t)nb * R * 32, s_in));
+        chk(hipEventRecord(x.in_done, s_in));
+        chk(hipEventRecord(ev_in, s_in));
+        chk(hipStreamWaitEvent(s_comp, ev_in, 0));
+        const int e = zs3_verify_reconstruct_batch_masks(c, x.d, E, S, nb, present + bb * R, data_only, x.d + off_exp,
+                                                         (int32_t*)(x.d + off_bad), hash_out ? x.d + off_out : nullptr,
+                                                         status ? status + bb : nullptr, s_comp);
+        if (e == ZS3_ERR_TOO_FEW_SHARDS || e == ZS3_ERR_SHARD_NO_DATA) {
+            if (first_block_err == ZS3_OK) first_block_err = e;
+        } else if (e && rc == ZS3_OK) {
+            rc = e;
+        }
+        chk(hipEventRecord(ev_comp, s_comp));
+        chk(hipStreamWaitEvent(s_out, ev_comp, 0));
+        // rebuilt rows back into the caller's stripes (pinned) or the slot's staging
+        uint8_t* dst = pinned ? h + bb * E : x.hs;
+        for (int j = 0; j < R; ++j)
+            if (anyr[(size_t)j])
+                chk(hipMemcpy2DAsync(dst + (size_t)j * S, (size_t)E, x.d + (size_t)j * S, (size_t)E, (size_t)S, (size_t)nb,
+                                     hipMemcpyDeviceToHost, s_out));
+        if (h_bad)
+            chk(hipMemcpyAsync(h_bad + bb * R, x.d + off_bad, (size_t)nb * R * 4, hipMemcpyDeviceToHost, s_out));
+        if (hash_out)
+            chk(hipMemcpyAsync(h_sums_out + bb * R * 32, x.d + off_out, (size_t)nb * R * 32, hipMemcpyDeviceToHost, s_out));
+        chk(hipEventRecord(x.out_done, s_out));
+        x.used = true;
+        if (!pinned) {
+            // the rebuilt rows of each block from the staging into the caller's stripes
+            hipEvent_t done = x.out_done;
+            uint8_t* hs = x.hs;
+            std::vector<uint8_t> pres(present + bb * R, present + (bb + nb) * R);
+            x.drain = std::async(std::launch::async, [=]() -> int {
+                if (hipEventSynchronize(done) != hipSuccess) return ZS3_ERR_DEVICE;
+                for (int64_t b = 0; b < nb; ++b)
+                    for (int j = 0; j < R; ++j)
+                        if (!pres[(size_t)(b * R + j)] && (j < k || heal))
+                            std::memcpy(h + (bb + b) * E + (size_t)j * S, hs + b * E + (size_t)j * S, (size_t)S);
+                return ZS3_OK;
+            });
+        }
+    }
+    for (auto& x : sl) {
+        if (x.fill.valid()) (void)x.fill.get();
+        if (x.drain.valid()) {
+            const int e = x.drain.get();
+            if (e && rc == ZS3_OK) rc = e;
+        }
+    }
+    chk(hipStreamSynchronize(s_out));
+    for (auto& x : sl) {
+        if (x.d) (void)hipFree(x.d);
+        if (x.hs) (void)hipHostFree(x.hs);
+        if (x.in_done) (void)hipEventDestroy(x.in_done);
+        if (x.out_done) (void)hipEventDestroy(x.out_done);
+    }
+    if (ev_in) (void)hipEventDestroy(ev_in);
+    if (ev_comp) (void)hipEventDestroy(ev_comp);
+    if (s_in) (void)hipStreamDestroy(s_in);
+    if (s_comp) (void)hipStreamDestroy(s_comp);
+    if (s_out) (void)hipStreamDestroy(s_out);
+    return rc ? rc : first_block_err;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1140,6 +1323,74 @@ int64_t zs3_stream_encode(const zs3_codec* c, const uint8_t* src, int64_t total_
     return zs3_stream_encode_multi(c, &dev, 1, src, total_len, h_parity, h_sums, batch_blocks);
 }
 
+int64_t zs3_stream_decode(const zs3_codec* cc, uint8_t* h_stripes, int64_t total_len, const uint8_t* h_present,
+                          int data_only, const uint8_t* h_expect, int32_t* h_bad, uint8_t* h_sums_out,
+                          int32_t* h_status, int64_t batch_blocks) {
+    zs3_codec* c = const_cast<zs3_codec*>(cc);
+    if (!c || total_len < 0 || batch_blocks <= 0 || (total_len > 0 && (!h_stripes || !h_present)))
+        return ZS3_ERR_INVALID_ARG;
+    if (total_len == 0) return 0;
+    const int k = c->k, R = c->k + c->m;
+    const int64_t B = c->block_size;
+    const int64_t S = ceil_frac(B, k);
+    const int64_t E = (int64_t)R * S;
+    const int64_t nfull = total_len / B, tail = total_len % B;
+    const int64_t nblocks = nfull + (tail ? 1 : 0);
+    const size_t bytes = (size_t)(nblocks * E);
+    const bool pinned = zs3i_pinned(h_stripes, bytes) || is_pinned(h_stripes);
+    const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
+    int rc = stream_vr_range(c, h_stripes, nfull, h_present, data_only, h_expect, h_bad, h_sums_out, h_status,
+                             batch_blocks, pinned, std::max(2, std::min(16, hw)));
+    if (rc && rc != ZS3_ERR_TOO_FEW_SHARDS && rc != ZS3_ERR_SHARD_NO_DATA) return rc;
+    if (tail) {
+        // the short last block on its own shard size (erasure-decode.go:112-114): rows at
+        // j*S' inside its stripe slot
+        const int64_t St = ceil_frac(tail, k);
+        uint8_t* stripe = h_stripes + nfull * E;
+        uint8_t* d = nullptr;
+        const size_t db = (size_t)R * St + (size_t)R * 32 + (size_t)R * 4 + (size_t)R * 32;
+        hipStream_t s = nullptr;
+        int e = map_hip(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        if (!e) e = map_hip(hipMalloc(&d, db));
+        const uint8_t* pres = h_present + nfull * R;
+        if (!e) e = map_hip(hipMemcpyAsync(d, stripe, (size_t)R * St, hipMemcpyHostToDevice, s));
+        if (!e) {
+            if (h_expect)
+                e = map_hip(hipMemcpyAsync(d + (size_t)R * St, h_expect + nfull * R * 32, (size_t)R * 32,
+                                           hipMemcpyHostToDevice, s));
+            else
+                e = map_hip(hipMemsetAsync(d + (size_t)R * St, 0, (size_t)R * 32, s));
+        }
+        int32_t one = ZS3_OK;
+        uint8_t* dbad = d + (size_t)R * St + (size_t)R * 32;
+        uint8_t* dout = dbad + (size_t)R * 4;
+        if (!e) {
+            const int ee = zs3_verify_reconstruct_batch_masks(c, d, (int64_t)R * St, St, 1, pres, data_only,
+                                                              d + (size_t)R * St, (int32_t*)dbad,
+                                                              !data_only && h_sums_out ? dout : nullptr, &one, s);
+            if (ee && ee != ZS3_ERR_TOO_FEW_SHARDS && ee != ZS3_ERR_SHARD_NO_DATA) e = ee;
+        }
+        if (h_status) h_status[nfull] = one;
+        if (!e && one == ZS3_OK) {
+            for (int j = 0; j < R && !e; ++j)
+                if (!pres[j] && (j < k || !data_only))
+                    e = map_hip(hipMemcpyAsync(stripe + (size_t)j * St, d + (size_t)j * St, (size_t)St,
+                                               hipMemcpyDeviceToHost, s));
+        }
+        if (!e && h_bad) e = map_hip(hipMemcpyAsync(h_bad + nfull * R, dbad, (size_t)R * 4, hipMemcpyDeviceToHost, s));
+        if (!e && !data_only && h_sums_out)
+            e = map_hip(hipMemcpyAsync(h_sums_out + nfull * R * 32, dout, (size_t)R * 32, hipMemcpyDeviceToHost, s));
+        if (s) {
+            if (!e) e = map_hip(hipStreamSynchronize(s));
+            (void)hipStreamDestroy(s);
+        }
+        if (d) (void)hipFree(d);
+        if (e) return e;
+        if (one != ZS3_OK && rc == ZS3_OK) rc = one;
+    }
+    return rc ? rc : nblocks;
+}
+
 int zs3_selftest(void) {
     // erasureSelfTest, cmd/erasure-coding.go:158-216 (want table from :169)
     int nkat = 0;
@@ -1199,6 +1450,12 @@ int zs3_debug_set_variant(int variant) {
 int zs3_debug_set_buffer(void* d_dbg) {
     t_dbg = (uint64_t*)d_dbg;
     return ZS3_OK;
+}
+
+int zs3_debug_encode_layout_ok(const void* d_data, int64_t data_stride, int64_t block_len, int64_t n_blocks,
+                               const void* d_parity, int64_t parity_stride, int64_t parity_bytes) {
+    return encode_layout_ok((const uint8_t*)d_data, data_stride, block_len, n_blocks, (const uint8_t*)d_parity,
+                            parity_stride, parity_bytes) ? 1 : 0;
 }
 #endif
 

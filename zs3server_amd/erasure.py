@@ -8,6 +8,7 @@ All arithmetic runs in the HIP kernels (host-staged through pinned memory).
 from __future__ import annotations
 
 import io
+import os
 import threading
 
 import numpy as np
@@ -458,16 +459,16 @@ def _hash_chunks(bufs: list, key: bytes, hh256_batch) -> list:
 # legacy object's full 10 MiB blocks batch together in their own queue, and a 1 MiB
 # object's full blocks are never mistaken for short blocks of a 10 MiB queue (nor
 # rejected by it).
-QUEUE_SLOT_BYTES = 384 << 20  # pinned staging per queue slot (and as much device memory)
-QUEUE_MAX_BATCH = 512
+QUEUE_BATCH_BYTES = 64 << 20  # input bytes per device batch (queue_policy.hpp kBatchInputBytes)
+QUEUE_MIN_BATCH, QUEUE_MAX_BATCH = 8, 512
 
 
 def queue_max_batch(k: int, m: int, block_size: int) -> int:
-    """Blocks per queue batch for a geometry: as many stripes as one slot's byte budget
-    holds (RS(8+4) at 1 MiB: 256, so a closed batch leaves the <= 128-stripe latency path
-    for the tuned kernels; at blockSizeV1 = 10 MiB: 25), at least 4, at most 512."""
-    S = -(-block_size // k)
-    return max(4, min(QUEUE_MAX_BATCH, QUEUE_SLOT_BYTES // ((k + m) * S)))
+    """Blocks per queue batch for a block size: the library's own rule
+    (zs3server_amd/csrc/queue_policy.hpp slot_blocks with max_batch 0): 64 MiB of input,
+    at least 8 and at most 512 blocks (RS(8+4) at 1 MiB: 64; at blockSizeV1 = 10 MiB: 8).
+    The staging slots are sized to it; the shim passes max_batch 0."""
+    return max(QUEUE_MIN_BATCH, min(QUEUE_MAX_BATCH, QUEUE_BATCH_BYTES // block_size))
 
 
 class GPUCodec:
@@ -478,7 +479,8 @@ class GPUCodec:
         from . import Queue
         self.key = (k, m, block_size)
         self.codec = Codec(k, m, block_size)  # ErrInvShardNum / ErrMaxShardNum as NewErasure
-        factory = queue_factory or (lambda c, mb: Queue(c, max_batch=mb, max_wait_us=200, slots=4))
+        devices = gpu_devices()
+        factory = queue_factory or (lambda c, mb: Queue(c, max_batch=0, max_wait_us=200, slots=4, devices=devices))
         self.max_batch = queue_max_batch(k, m, block_size)
         self.queue = factory(self.codec, self.max_batch)
 
@@ -489,6 +491,19 @@ class GPUCodec:
     def decode(self, shards, present, data_only: bool, expect=None, bad=None, sums_out=None) -> int:
         """reconstructGPU: DecodeDataBlocks / DecodeDataAndParityBlocks (+ verify / heal sums)."""
         return self.queue.decode(shards, present, data_only, expect=expect, bad=bad, sums_out=sums_out)
+
+
+def gpu_devices() -> list:
+    """The node's GPUs a queue spreads its blocks over: every visible
+    device, or ZS3_QUEUE_DEVICES (a comma list of HIP ordinals) when set."""
+    env = os.environ.get("ZS3_QUEUE_DEVICES")
+    if env:
+        return [int(x) for x in env.split(",") if x.strip()]
+    from . import device_count
+    try:
+        return list(range(max(1, device_count())))
+    except Exception:  # noqa: BLE001 - no device: the single-device default
+        return []
 
 
 _GPU_CODECS: dict = {}

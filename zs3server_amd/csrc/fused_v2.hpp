@@ -206,6 +206,7 @@ struct EncShape {
     static constexpr int ABL = 0;        // diagnostics timing ablations (output differs)
     static constexpr bool GEN = false;   // general M x K coding matrix (not dyadic)
     static constexpr int XMAP = 0;       // workgroup -> stripe-group order (ws_group)
+    static constexpr bool DIAGMOD = false;  // a diagnostics modifier of a product shape
 };
 
 // workgroup -> stripe group (XMAP above k_ehx_ws); a bijection on [0, gridDim.x)
@@ -859,6 +860,8 @@ struct GetShape {
     static constexpr int PFD = 0;        // L2 prefetch distance of the hash waves
     static constexpr int TSP = 0;        // LDS row stride rule
     static constexpr int XMAP = 0;       // workgroup -> stripe-group order
+    static constexpr bool STH = false;   // with ST + BT: the tables' high dwords from LDS (below)
+    static constexpr bool DIAGMOD = false;  // a diagnostics modifier of a product shape (Tsp0, XMap, ...)
 };
 // The instance a launch picks for a requested shape: its memory policy (non-temporal,
 // buffer-addressed) fixed by the batch (launch_vr_ws_t).
@@ -873,6 +876,12 @@ __global__ void __launch_bounds__((vr_nh<C::G, K + (HOUT ? EX : 0), C::HQ>() + C
 __attribute__((amdgpu_waves_per_eu(2))) k_vr_ws(VrArgs a) {
     constexpr int G = C::G, T = C::T, PF = C::PF, CW = C::CW, BT = C::BT, PFD = C::PFD;
     constexpr bool HQ = C::HQ, ST = C::ST, NTL = C::NTL, UA = C::UA, BUF = C::BUF;
+    // STH (round 5): a v_perm reads at most one SGPR, so with scalar tables each
+    // coefficient's two high table dwords were copied to VGPRs by two v_mov per step
+    // (~15 % of the rebuild role's VALU for RS(16+4) heal 4); with STH they come from an
+    // LDS copy instead (one broadcast ds_read_b64 per coefficient, issued with its batch's
+    // scalar loads), and the scalar loads fetch only the three dwords used as SGPRs.
+    constexpr bool STH = C::STH && ST && BT > 0 && EX > 0;
     constexpr int RH = K + (HOUT ? EX : 0);
     constexpr int NH = vr_nh<G, RH, HQ>();
     constexpr int CPS = T / CW;
@@ -886,6 +895,7 @@ __attribute__((amdgpu_waves_per_eu(2))) k_vr_ws(VrArgs a) {
     uint8_t(*tile)[G * RH * TS] = reinterpret_cast<uint8_t(*)[G * RH * TS]>(smem_dyn);
     __shared__ __attribute__((aligned(16))) uint32_t tabs[NTAB];
     __shared__ int32_t srows[K + EX];
+    __shared__ __attribute__((aligned(8))) uint2 htabs[STH ? EX * K : 1];
 
     const int tid = threadIdx.x;
     const int64_t blk0 = (int64_t)ws_group<C::XMAP>() * G;
@@ -893,6 +903,8 @@ __attribute__((amdgpu_waves_per_eu(2))) k_vr_ws(VrArgs a) {
     const int R = a.k + a.m;
     if (EX > 0)
         for (int i = tid; i < EX * K * 8; i += NT) tabs[i] = a.tables[i];
+    if constexpr (STH)
+        for (int i = tid; i < EX * K; i += NT) htabs[i] = make_uint2(a.tables[8 * i + 1], a.tables[8 * i + 3]);
     for (int i = tid; i < K + EX; i += NT) srows[i] = a.rows[i];
     const int64_t nfull = S / T;
     const int tail = (int)(S - nfull * T);
@@ -1127,21 +1139,37 @@ __attribute__((amdgpu_waves_per_eu(2))) k_vr_ws(VrArgs a) {
             const ctab_ptr tg = const_tables(a.tables) + opaque_zero();
             constexpr int NB = BT > 0 ? BT : 4;  // BT: coefficients per scalar batch
             CoefTab tbat[2][NB];
+            uint2 hbat[2][STH ? NB : 1];  // STH: the batch's high table dwords (VGPRs, from LDS)
+            const uint2* hb = htabs + opaque_zero();
             // (a batch may straddle two rebuilt rows; the last one re-reads table EX*K-1
             // for its slots past the end)
-            auto load_batch = [&](CoefTab (&d)[NB], int c0) {
+            auto load_batch = [&](CoefTab (&d)[NB], uint2 (&h)[STH ? NB : 1], int c0) {
 #pragma unroll
-                for (int i = 0; i < NB; ++i) d[i] = load_coef_s(tg, c0 + i < EX * K ? c0 + i : EX * K - 1);
+                for (int i = 0; i < NB; ++i) {
+                    const int ci = c0 + i < EX * K ? c0 + i : EX * K - 1;
+                    if constexpr (STH) {
+                        d[i].ab.x = tg[8 * ci + 0];
+                        d[i].ab.z = tg[8 * ci + 2];
+                        d[i].c = tg[8 * ci + 4];
+                        h[i] = hb[ci];
+                    } else {
+                        d[i] = load_coef_s(tg, ci);
+                    }
+                }
             };
             // BT: consume batch d (the wait for its scalar loads sits here), then issue the
             // next batch's loads, then compute; the scheduling barriers keep that order
-            auto wait_batch = [&](const CoefTab (&d)[NB]) {
+            auto wait_batch = [&](const CoefTab (&d)[NB], const uint2 (&h)[STH ? NB : 1]) {
 #pragma unroll
-                for (int i = 0; i < NB; ++i)
-                    asm volatile("" ::"s"(d[i].ab.x), "s"(d[i].ab.y), "s"(d[i].ab.z), "s"(d[i].ab.w), "s"(d[i].c));
+                for (int i = 0; i < NB; ++i) {
+                    if constexpr (STH)
+                        asm volatile("" ::"s"(d[i].ab.x), "s"(d[i].ab.z), "s"(d[i].c), "v"(h[i].x), "v"(h[i].y));
+                    else
+                        asm volatile("" ::"s"(d[i].ab.x), "s"(d[i].ab.y), "s"(d[i].ab.z), "s"(d[i].ab.w), "s"(d[i].c));
+                }
                 __builtin_amdgcn_sched_barrier(0);
             };
-            if constexpr (ST && BT) load_batch(tbat[0], 0);
+            if constexpr (ST && BT) load_batch(tbat[0], hbat[0], 0);
 #pragma unroll
             for (int r = 0; r < EX; ++r) {
                 GfAcc acc[NWd];
@@ -1152,13 +1180,20 @@ __attribute__((amdgpu_waves_per_eu(2))) k_vr_ws(VrArgs a) {
                     if constexpr (ST && BT) {
                         const int c = r * K + j, bi = c / NB, cur = bi & 1;
                         if (c % NB == 0) {
-                            wait_batch(tbat[cur]);
-                            if (c + NB < EX * K) load_batch(tbat[cur ^ 1], c + NB);
+                            wait_batch(tbat[cur], hbat[cur]);
+                            if (c + NB < EX * K) load_batch(tbat[cur ^ 1], hbat[cur ^ 1], c + NB);
                             __builtin_amdgcn_sched_barrier(0);
                         }
                         const CoefTab t = tbat[cur][c % NB];
+                        if constexpr (STH) {
+                            const uint2 hi = hbat[cur][c % NB];
 #pragma unroll
-                        for (int w = 0; w < NWd; ++w) acc_add(acc[w], gf_lookup_s(split_nibbles(xs[j].w[w]), t));
+                            for (int w = 0; w < NWd; ++w)
+                                acc_add(acc[w], gf_lookup_sh(split_nibbles(xs[j].w[w]), t, hi.x, hi.y));
+                        } else {
+#pragma unroll
+                            for (int w = 0; w < NWd; ++w) acc_add(acc[w], gf_lookup_s(split_nibbles(xs[j].w[w]), t));
+                        }
                     } else if constexpr (ST) {
                         const CoefTab t = load_coef_s(tg, r * K + j);
 #pragma unroll
@@ -1262,10 +1297,22 @@ static bool launch_vr_inst(const VrArgs& a, hipStream_t s);
 template <class C>
 struct Tsp1 : C {
     static constexpr int TSP = 1;
+    static constexpr bool DIAGMOD = true;
 };
 template <class C, int P>
 struct XMap : C {
     static constexpr int XMAP = P;
+    static constexpr bool DIAGMOD = true;
+};
+template <class C>
+struct Tsp0 : C {
+    static constexpr int TSP = 0;
+    static constexpr bool DIAGMOD = true;
+};
+template <class C>
+struct Sth : C {
+    static constexpr bool STH = true;
+    static constexpr bool DIAGMOD = true;
 };
 // C itself when P == 0 (product instances keep their shape's name)
 template <class C, int P>
@@ -1275,16 +1322,22 @@ using WithXMap = std::conditional_t<P == 0, C, XMap<C, P>>;
 template <int K, int EX, bool HOUT, class C>
 static bool launch_vr_ws_t(const VrArgs& a, hipStream_t s) {
 #if ZS3_DIAG
-    // diagnostics 420: the same shape with the conflict-free LDS row stride (ws_ts TSP 1;
-    // pair-form shapes of k = 8 / 12 / 16: for the quad form at T % 64 == 0 both rules
-    // give T + 32); 421: with the region-interleaved workgroup order (ws_group, 8 regions;
-    // k = 8 / 16).  Instantiated for those k only: every modifier multiplies the
+    // Diagnostics A/B of a product GET shape (one modifier at a time: a modified shape is
+    // not modified again): 420 = the round-4 LDS row stride (TSP 0) on the pair-form
+    // shapes of k = 8 / 12 / 16; 421 = the region-interleaved workgroup order (ws_group, 8
+    // regions; k = 8 / 12 / 16); 423 = the tables' high dwords from LDS (STH) on every
+    // scalar-table shape.  Instantiated for those k only: every modifier multiplies the
     // diagnostics library by the product GET instances.
-    if constexpr (C::TSP == 0 && !C::HQ && (K == 8 || K == 12 || K == 16)) {
-        if (a.variant == 420) return launch_vr_ws_t<K, EX, HOUT, Tsp1<C>>(a, s);
-    }
-    if constexpr (C::XMAP == 0 && C::TSP == 0 && (K == 8 || K == 16)) {
-        if (a.variant == 421) return launch_vr_ws_t<K, EX, HOUT, XMap<C, 8>>(a, s);
+    if constexpr (!C::DIAGMOD) {
+        if constexpr (C::TSP == 1 && !C::HQ && (K == 8 || K == 12 || K == 16)) {
+            if (a.variant == 420) return launch_vr_ws_t<K, EX, HOUT, Tsp0<C>>(a, s);
+        }
+        if constexpr (C::XMAP == 0 && (K == 8 || K == 12 || K == 16)) {
+            if (a.variant == 421) return launch_vr_ws_t<K, EX, HOUT, XMap<C, 8>>(a, s);
+        }
+        if constexpr (C::ST && C::BT > 0 && EX > 0) {
+            if (a.variant == 423) return launch_vr_ws_t<K, EX, HOUT, Sth<C>>(a, s);
+        }
     }
 #endif
     if constexpr (C::BUF && !C::UA) {
@@ -1292,7 +1345,7 @@ static bool launch_vr_ws_t(const VrArgs& a, hipStream_t s) {
         // their span below 2^31 bytes; otherwise the 64-bit-address instance (diagnostics
         // 247: always that one)
         if (!a.ids && (int64_t)C::G * a.block_stride < ((int64_t)1 << 31) && a.block_stride > 0 &&
-            !(ZS3_DIAG && a.variant == 247 && C::TSP == 0 && C::XMAP == 0))
+            !(ZS3_DIAG && a.variant == 247 && !C::DIAGMOD))
             return launch_vr_inst<K, EX, HOUT, VrMem<C, true, true>>(a, s);
         return launch_vr_inst<K, EX, HOUT, VrMem<C, true, false>>(a, s);
     }
@@ -1306,7 +1359,7 @@ static bool launch_vr_ws_t(const VrArgs& a, hipStream_t s) {
         // Survivor loads and rebuilt-row stores are non-temporal (each byte is touched once):
         // RS(8+4) verify 0.706 -> 0.627 ms, RS(16+4) verify 0.386 -> 0.351, rebuild 1-4 and
         // heals 1-5 % faster (profiles/r02/ab_get_nt.jsonl).  Diagnostics 246: plain loads.
-        if constexpr (ZS3_DIAG && (K == 8 || K == 16) && C::TSP == 0 && C::XMAP == 0) {
+        if constexpr (ZS3_DIAG && (K == 8 || K == 16) && !C::DIAGMOD) {
             if (a.variant == 246) return launch_vr_inst<K, EX, HOUT, VrMem<C, false, false>>(a, s);
         }
         return launch_vr_inst<K, EX, HOUT, VrMem<C, true, false>>(a, s);
@@ -1321,7 +1374,7 @@ static bool launch_vr_inst(const VrArgs& a, hipStream_t s) {
     constexpr size_t tiles = (size_t)2 * G * RH * ws_ts<T, C::HQ, C::TSP>();
     constexpr size_t dyn = tiles > 83968 ? tiles : 83968;  // one workgroup per CU
     static_assert(G > 0 && T > 0, "a shape names its stripes per workgroup and tile length");
-    if constexpr (dyn + (size_t)(EX > 0 ? EX : 1) * K * 32 + 4 * (K + EX) > 163840 || NT > 1024 ||
+    if constexpr (dyn + (size_t)(EX > 0 ? EX : 1) * K * (32 + (C::STH ? 8 : 0)) + 4 * (K + EX) > 163840 || NT > 1024 ||
                   vr_nh<G, RH, C::HQ>() % 64 != 0 || (G * (T / CW)) % 64 != 0) {
         return false;
     } else {
@@ -1361,9 +1414,11 @@ struct Rs84Mid : EncShape {
     static constexpr bool HQ = true;
 };
 // RS(16+4) above 1024 stripes: 8 stripes of 384-byte tiles, 8-byte buffer-addressed
-// columns, data rows to LDS before the encode.
+// columns, data rows to LDS before the encode; round 5: conflict-free LDS rows and the
+// region-interleaved workgroup order (8 192 x 1 MiB 2.342-2.370 -> 2.314-2.341 ms,
+// diagnostics 417, profiles/r05/ab_enc2.jsonl).
 struct Rs164Bulk : EncShape {
-    static constexpr int G = 8, T = 384, NTM = 3, EP = 2;
+    static constexpr int G = 8, T = 384, NTM = 3, EP = 2, TSP = 1, XMAP = 8;
     static constexpr bool BUF = true;
 };
 // Quad-form hash waves on 4 stripes of 512-byte tiles (RS(16+4) / RS(12+4) small batches).
@@ -1425,6 +1480,9 @@ struct Gen8x512 : GenBase {
 };
 
 // GET / heal (k_vr_ws), requested shapes (launch_vr_ws_t fixes the memory policy).
+// Round 5: every pair-form shape uses the conflict-free LDS row stride (TSP 1):
+// SQ_LDS_BANK_CONFLICT 25 % -> 0 % of SQ_LDS_IDX_ACTIVE at equal time (diagnostics 420,
+// profiles/r05/pmc_lds_get.json, get_ab.jsonl); the quad-form shapes already had it.
 // RS(4+m): 8 stripes, quad-form hash waves; verify on 256-byte tiles, rebuild / heal on
 // 1 KiB tiles (PF tiles of prefetch).
 template <int T_, int PF_>
@@ -1436,41 +1494,41 @@ struct K4Quad : GetShape {
 // batched scalar tables for rebuild 3-4; heal 1-2 on 128-byte tiles, heal 3-4 on 256 with
 // 16-byte columns.
 struct K8Get : GetShape {
-    static constexpr int G = 16, T = 256, PF = 2;
+    static constexpr int G = 16, T = 256, PF = 2, TSP = 1;
 };
 struct K8Rebuild34 : GetShape {
-    static constexpr int G = 16, T = 256, CW = 8, BT = 4;
+    static constexpr int G = 16, T = 256, CW = 8, BT = 4, TSP = 1;
     static constexpr bool ST = true, BUF = true;
 };
 struct K8Heal12 : GetShape {
-    static constexpr int G = 16, T = 128, PF = 2, CW = 8, BT = 4;
+    static constexpr int G = 16, T = 128, PF = 2, CW = 8, BT = 4, TSP = 1;
     static constexpr bool ST = true;
 };
 struct K8Heal34 : GetShape {
-    static constexpr int G = 16, T = 256, CW = 16, BT = 4;
+    static constexpr int G = 16, T = 256, CW = 16, BT = 4, TSP = 1;
     static constexpr bool ST = true, BUF = true;
 };
 // RS(16+4): 8 stripes; verify on 256-byte tiles; rebuild 1-2 with 4-byte columns (one
 // table per wait); rebuild 3-4 with 8-byte columns of 512; heal with 8-byte columns of 384.
 struct K16Verify : GetShape {
-    static constexpr int G = 8, T = 256, PF = 2;
+    static constexpr int G = 8, T = 256, PF = 2, TSP = 1;
 };
 struct K16Rebuild12 : GetShape {
-    static constexpr int G = 8, T = 256, PF = 2, CW = 4;
+    static constexpr int G = 8, T = 256, PF = 2, CW = 4, TSP = 1;
     static constexpr bool ST = true;
 };
 struct K16Rebuild34 : GetShape {
-    static constexpr int G = 8, T = 512, CW = 8, BT = 4;
+    static constexpr int G = 8, T = 512, CW = 8, BT = 4, TSP = 1;
     static constexpr bool ST = true, BUF = true;
 };
 struct K16Heal : GetShape {
-    static constexpr int G = 8, T = 384, CW = 8, BT = 4;
+    static constexpr int G = 8, T = 384, CW = 8, BT = 4, TSP = 1;
     static constexpr bool ST = true, BUF = true;
 };
 // RS(12+4) and k = 9-11: 8 stripes of 8-byte columns of 512-byte tiles, unaligned rows.
 template <bool UA_>
 struct Wide512 : GetShape {
-    static constexpr int G = 8, T = 512, CW = 8, BT = 4;
+    static constexpr int G = 8, T = 512, CW = 8, BT = 4, TSP = 1;
     static constexpr bool ST = true, UA = UA_;
 };
 // k = 2, 3: 8 stripes of 1 KiB tiles, quad-form hash waves; k = 5-7: 16 stripes of 256.
@@ -1481,7 +1539,7 @@ struct GenGetQuad1K : GetShape {
 };
 template <bool UA_>
 struct GenGet16x256 : GetShape {
-    static constexpr int G = 16, T = 256, CW = 8, BT = 4;
+    static constexpr int G = 16, T = 256, CW = 8, BT = 4, TSP = 1;
     static constexpr bool ST = true, UA = UA_;
 };
 

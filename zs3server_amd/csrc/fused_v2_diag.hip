@@ -13,7 +13,8 @@
 //  402              RS(4+4) on the RS(8+4) headline shape (Rs84Bulk)
 //  409-414          Rs84Bulk with the region-interleaved workgroup order (ws_group) over 1
 //                   (none: the round-4 product) / 2 / 4 / 8 (the product) / 16 / 32 regions
-//  415              XMAP 8 on the RS(16+4) bulk shape; 417 TSP 1 + XMAP 8 on it
+//  401 / 415 / 417  the RS(16+4) bulk shape without XMAP / without TSP / without either
+//                   (417 = the round-4 product)
 //  416              the RS(12+4) 1 KiB UA shape without XMAP (the round-4 product)
 //  418              XMAP 8 on PairG16 (RS(4+4) / RS(4+2) bulk); 419 XMAP 8 on every GEN shape
 #include "fused_v2.hpp"
@@ -63,9 +64,9 @@ bool launch_ehx_diag(int v, const EncArgs& a, hipStream_t s) {
     }
     if (a.k == 16 && a.m == 4) {
         switch (v) {
-            case 401: return launch_ws<16, 4, Tsp1<Rs164Bulk>>(a, s);
-            case 415: return launch_ws<16, 4, XMap<Rs164Bulk, 8>>(a, s);
-            case 417: return launch_ws<16, 4, XMap<Tsp1<Rs164Bulk>, 8>>(a, s);
+            case 401: return launch_ws<16, 4, XMap<Rs164Bulk, 0>>(a, s);
+            case 415: return launch_ws<16, 4, Tsp0<Rs164Bulk>>(a, s);
+            case 417: return launch_ws<16, 4, XMap<Tsp0<Rs164Bulk>, 0>>(a, s);
             default: return false;
         }
     }

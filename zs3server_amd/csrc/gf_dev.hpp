@@ -93,6 +93,16 @@ __device__ __forceinline__ Prod3 gf_lookup_s(const Nib& n, const CoefTab& t) {
     return p;
 }
 
+// gf_lookup with the low table dwords in SGPRs and the high ones in VGPRs (hx = Ta.hi,
+// hz = Tb.hi): no v_mov per coefficient to satisfy the one-SGPR operand limit.
+__device__ __forceinline__ Prod3 gf_lookup_sh(const Nib& n, const CoefTab& t, uint32_t hx, uint32_t hz) {
+    Prod3 p;
+    p.a = __builtin_amdgcn_perm(hx, t.ab.x, n.a);
+    p.b = __builtin_amdgcn_perm(hz, t.ab.z, n.b);
+    p.c = __builtin_amdgcn_perm(n.c, t.c, n.c);
+    return p;
+}
+
 // Accumulator with one pending term so that lookups fold two at a time.
 struct GfAcc {
     uint32_t acc, pend;

@@ -920,6 +920,69 @@ void par_memcpy(uint8_t* dst, const uint8_t* src, size_t n, int threads) {
     for (auto& x : th) x.join();
 }
 
+// Staging buffers of the stream drivers (stream_range, stream_vr_range), kept across
+// calls: pinning hundreds of MiB of host memory and allocating the device slots cost more
+// than a 4 GiB stream's own transfers (a 4 GiB pageable RS(16+4) stream: 0.35 s, most of
+// it hipHostMalloc; profiles/r05/stream.jsonl).  Idle buffers are reused by the next call
+// on the same device (first fit of at most twice the size asked for); at most
+// kPoolIdleMax bytes stay idle, the rest is freed.
+struct PoolBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    bool host = false;
+    int dev = -1;
+};
+std::mutex g_pool_mu;
+std::vector<PoolBuf> g_pool;  // idle
+size_t g_pool_idle = 0;
+constexpr size_t kPoolIdleMax = (size_t)6 << 30;
+
+hipError_t pool_get(bool host, size_t bytes, void** out) {
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess) return hipErrorInvalidDevice;
+    {
+        std::lock_guard<std::mutex> g(g_pool_mu);
+        for (size_t i = 0; i < g_pool.size(); ++i) {
+            const PoolBuf& b = g_pool[i];
+            if (b.host == host && (host || b.dev == dev) && b.cap >= bytes && b.cap <= 2 * bytes + (1 << 20)) {
+                *out = b.p;
+                g_pool_idle -= b.cap;
+                g_pool.erase(g_pool.begin() + (std::ptrdiff_t)i);
+                return hipSuccess;
+            }
+        }
+    }
+    return host ? hipHostMalloc(out, bytes, hipHostMallocDefault) : hipMalloc(out, bytes);
+}
+
+void pool_put(bool host, void* p, size_t bytes) {
+    if (!p) return;
+    int dev = -1;
+    (void)hipGetDevice(&dev);
+    std::vector<PoolBuf> drop;
+    {
+        std::lock_guard<std::mutex> g(g_pool_mu);
+        g_pool.push_back(PoolBuf{p, bytes, host, dev});
+        g_pool_idle += bytes;
+        while (g_pool_idle > kPoolIdleMax && !g_pool.empty()) {
+            drop.push_back(g_pool.front());
+            g_pool_idle -= g_pool.front().cap;
+            g_pool.erase(g_pool.begin());
+        }
+    }
+    for (auto& b : drop) {
+        if (b.host) {
+            (void)hipHostFree(b.p);
+        } else {
+            int cur = -1;
+            (void)hipGetDevice(&cur);
+            (void)hipSetDevice(b.dev);
+            (void)hipFree(b.p);
+            (void)hipSetDevice(cur);
+        }
+    }
+}
+
 bool is_pinned(const void* p) {
     hipPointerAttribute_t attr;
     if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
@@ -975,9 +1038,9 @@ int stream_range(zs3_codec* c, int device, const uint8_t* src, int64_t b0, int64
     const size_t dbytes = (size_t)NB * stride + (size_t)NB * R * 32;
     const size_t obytes = (size_t)NB * m * S + (size_t)NB * R * 32;
     for (auto& x : sl) {
-        chk(hipMalloc(&x.d, dbytes));
-        if (!src_pinned) chk(hipHostMalloc(&x.hin, (size_t)NB * B, hipHostMallocDefault));
-        if (!out_pinned) chk(hipHostMalloc(&x.hout, obytes, hipHostMallocDefault));
+        chk(pool_get(false, dbytes, (void**)&x.d));
+        if (!src_pinned) chk(pool_get(true, (size_t)NB * B, (void**)&x.hin));
+        if (!out_pinned) chk(pool_get(true, obytes, (void**)&x.hout));
         chk(hipEventCreateWithFlags(&x.in_done, hipEventDisableTiming));
         chk(hipEventCreateWithFlags(&x.out_done, hipEventDisableTiming));
     }
@@ -1063,9 +1126,9 @@ int stream_range(zs3_codec* c, int device, const uint8_t* src, int64_t b0, int64
     }
     chk(hipStreamSynchronize(s_out));
     for (auto& x : sl) {
-        if (x.d) (void)hipFree(x.d);
-        if (x.hin) (void)hipHostFree(x.hin);
-        if (x.hout) (void)hipHostFree(x.hout);
+        pool_put(false, x.d, dbytes);
+        pool_put(true, x.hin, (size_t)NB * B);
+        pool_put(true, x.hout, obytes);
         if (x.in_done) (void)hipEventDestroy(x.in_done);
         if (x.out_done) (void)hipEventDestroy(x.out_done);
     }
@@ -1117,13 +1180,14 @@ int stream_vr_range(zs3_codec* c, uint8_t* h, int64_t nblk, const uint8_t* prese
     const size_t off_exp = (size_t)NB * E, off_bad = off_exp + (size_t)NB * R * 32, off_out = off_bad + (size_t)NB * R * 4;
     const size_t dbytes = off_out + (size_t)NB * R * 32;
     for (auto& x : sl) {
-        chk(hipMalloc(&x.d, dbytes));
-        if (!pinned) chk(hipHostMalloc(&x.hs, (size_t)NB * E, hipHostMallocDefault));
+        chk(pool_get(false, dbytes, (void**)&x.d));
+        if (!pinned) chk(pool_get(true, (size_t)NB * E, (void**)&x.hs));
         chk(hipEventCreateWithFlags(&x.in_done, hipEventDisableTiming));
         chk(hipEventCreateWithFlags(&x.out_done, hipEventDisableTiming));
     }
     const int th = std::max(1, cpu_threads / 2);
     const int64_t nbatch = (nblk + NB - 1) / NB;
+    const bool rows2d = (S % 256) == 0;  // per-row strided DMA only for aligned rows
     // rows of a batch: `any_present` to upload, `any_rebuilt` to bring back
     auto rows_of = [&](int64_t bb, int64_t nb, std::vector<uint8_t>& any_present, std::vector<uint8_t>& any_rebuilt) {
         any_present.assign((size_t)R, 0);
@@ -1170,11 +1234,13 @@ int stream_vr_range(zs3_codec* c, uint8_t* h, int64_t nblk, const uint8_t* prese
         }
         rows_of(bb, nb, anyp, anyr);
         if (x.used) chk(hipStreamWaitEvent(s_in, x.out_done, 0));
-        if (pinned) {
+        if (pinned && rows2d) {
             for (int j = 0; j < R; ++j)
                 if (anyp[(size_t)j])
                     chk(hipMemcpy2DAsync(x.d + (size_t)j * S, (size_t)E, h + bb * E + (size_t)j * S, (size_t)E, (size_t)S,
                                          (size_t)nb, hipMemcpyHostToDevice, s_in));
+        } else if (pinned) {
+            chk(hipMemcpyAsync(x.d, h + bb * E, (size_t)(nb * E), hipMemcpyHostToDevice, s_in));
         } else {
             chk(hipMemcpyAsync(x.d, x.hs, (size_t)(nb * E), hipMemcpyHostToDevice, s_in));
         }
@@ -1195,12 +1261,20 @@ int stream_vr_range(zs3_codec* c, uint8_t* h, int64_t nblk, const uint8_t* prese
         }
         chk(hipEventRecord(ev_comp, s_comp));
         chk(hipStreamWaitEvent(s_out, ev_comp, 0));
-        // rebuilt rows back into the caller's stripes (pinned) or the slot's staging
+        // rebuilt rows back into the caller's stripes (pinned) or the slot's staging: one
+        // strided copy per rebuilt row index, or — for rows that are not 256-byte aligned,
+        // which the DMA engine copies strided at a fraction of its rate (RS(12+4) on 1 MiB
+        // blocks: 7.2 vs 30 GiB/s, profiles/r05/stream.jsonl) — the whole stripes (the
+        // present rows come back unchanged)
         uint8_t* dst = pinned ? h + bb * E : x.hs;
-        for (int j = 0; j < R; ++j)
-            if (anyr[(size_t)j])
-                chk(hipMemcpy2DAsync(dst + (size_t)j * S, (size_t)E, x.d + (size_t)j * S, (size_t)E, (size_t)S, (size_t)nb,
-                                     hipMemcpyDeviceToHost, s_out));
+        if (rows2d) {
+            for (int j = 0; j < R; ++j)
+                if (anyr[(size_t)j])
+                    chk(hipMemcpy2DAsync(dst + (size_t)j * S, (size_t)E, x.d + (size_t)j * S, (size_t)E, (size_t)S,
+                                         (size_t)nb, hipMemcpyDeviceToHost, s_out));
+        } else {
+            chk(hipMemcpyAsync(dst, x.d, (size_t)(nb * E), hipMemcpyDeviceToHost, s_out));
+        }
         if (h_bad)
             chk(hipMemcpyAsync(h_bad + bb * R, x.d + off_bad, (size_t)nb * R * 4, hipMemcpyDeviceToHost, s_out));
         if (hash_out)
@@ -1231,8 +1305,8 @@ int stream_vr_range(zs3_codec* c, uint8_t* h, int64_t nblk, const uint8_t* prese
     }
     chk(hipStreamSynchronize(s_out));
     for (auto& x : sl) {
-        if (x.d) (void)hipFree(x.d);
-        if (x.hs) (void)hipHostFree(x.hs);
+        pool_put(false, x.d, dbytes);
+        pool_put(true, x.hs, (size_t)NB * E);
         if (x.in_done) (void)hipEventDestroy(x.in_done);
         if (x.out_done) (void)hipEventDestroy(x.out_done);
     }

@@ -82,3 +82,45 @@ def content_sha256(objects: list[bytes]) -> list[bytes]:
     torch.cuda.synchronize()
     o = out.cpu().numpy().reshape(n, 32)
     return [r.tobytes() for r in o]
+
+
+# ---- digest routing ------------------------------------------------
+# One message's 64-byte blocks form a serial chain, so a device lane hashes one message at
+# its chain roof (profiles/r04/bench_paths_enc_ua_digest.jsonl: one 5 MiB
+# part MD5 0.555 us / SHA-256 1.696 us per 64-byte block), i.e. ~115 MB/s (MD5) and ~38 MB/s
+# (SHA-256) per message, against ~0.6-1 GB/s for one host core.  The device wins only on
+# many concurrent messages: it hashes up to GPU_DIGEST_LANES of them at once.
+GPU_LANE_BPS = {"md5": 64 / 0.555e-6, "sha256": 64 / 1.696e-6}
+GPU_DIGEST_LANES = 256 * 4 * 64 // 2      # one lane per message, two waves per 64 messages, 4 per SIMD
+GPU_LAUNCH_S = 30e-6                      # launch + result copy of one zs3_*_parts call
+PCIE_BPS = 50e9                           # one x16 Gen5 link, measured pinned H2D
+
+
+def digest_on_device(algo: str, n_msgs: int, msg_bytes: int, cpu_threads: int, cpu_Bps: float,
+                     resident: bool = False) -> bool:
+    """Where the rocm build hashes n_msgs concurrent messages (parts) of about msg_bytes:
+    True = zs3_md5_parts / zs3_sha256_parts, False = the host's crypto/md5 and sha256-simd
+    (internal/etag/reader.go:114, internal/hash/reader.go:137 unchanged).  Device time =
+    one chain per message, GPU_DIGEST_LANES at a time, plus the launch and, unless the
+    messages are already in HBM, their PCIe transfer; host time = the messages spread over
+    cpu_threads cores at cpu_Bps each.  A single part always stays on the host."""
+    if n_msgs <= 1 or msg_bytes <= 0:
+        return False
+    rounds = -(-n_msgs // GPU_DIGEST_LANES)
+    t_dev = rounds * msg_bytes / GPU_LANE_BPS[algo] + GPU_LAUNCH_S
+    if not resident:
+        t_dev += n_msgs * msg_bytes / PCIE_BPS
+    t_cpu = -(-n_msgs // max(1, cpu_threads)) * msg_bytes / cpu_Bps
+    return t_dev < t_cpu
+
+
+def host_digest_Bps(algo: str, nbytes: int = 8 << 20) -> float:
+    """One host core's MD5 / SHA-256 rate (the calibration the rule above takes)."""
+    import hashlib
+    import time
+    buf = bytes(nbytes)
+    h = hashlib.md5 if algo == "md5" else hashlib.sha256
+    h(buf[: 1 << 20]).digest()
+    t0 = time.perf_counter()
+    h(buf).digest()
+    return nbytes / (time.perf_counter() - t0)

@@ -76,7 +76,7 @@ WS_CASES = [(8, 4, 1 << 16, []), (8, 4, 1 << 16, [0, 5]), (8, 4, 1 << 16, [3, 9]
 @pytest.mark.parametrize("k,m,blen,erased", WS_CASES)
 @pytest.mark.parametrize("data_only", [True, False])
 @pytest.mark.parametrize("heal", [False, True])
-@pytest.mark.parametrize("variant", [0, 230, 231, 246, 247, 420, 421, 423])
+@pytest.mark.parametrize("variant", [0, 230, 231, 246, 247, 420, 421, 423, 424, 429])
 def test_verify_reconstruct_ws(oracle, k, m, blen, erased, data_only, heal, variant):
     """Variant 0: the product dispatch; at 17 blocks it takes the small-batch latency
     path (k_reconstruct + one chain per quad; 230 forces it).  231 = the product dispatch
@@ -97,7 +97,7 @@ WS4_CASES = [(4, 2, 1 << 16, []), (4, 2, 1 << 16, [1]), (4, 2, 1 << 16, [0, 5]),
 @pytest.mark.parametrize("k,m,blen,erased", WS4_CASES)
 @pytest.mark.parametrize("data_only", [True, False])
 @pytest.mark.parametrize("heal", [False, True])
-@pytest.mark.parametrize("variant", [0, 231])
+@pytest.mark.parametrize("variant", [0, 231, 429])
 def test_verify_reconstruct_ws_rs42(oracle, k, m, blen, erased, data_only, heal, variant):
     """RS(4+2)-shaped GET / heal on k_vr_ws (quad-form hash waves): tile edges and dead
     stripes; 231 = the product dispatch asserted to run the warp-specialised kernel."""
@@ -114,13 +114,13 @@ WS16_HEAL_CASES = [(16, 4, 1 << 16, [0, 5]), (16, 4, 1 << 16, [3, 17]), (16, 4, 
 
 
 @pytest.mark.parametrize("k,m,blen,erased", WS16_HEAL_CASES)
-@pytest.mark.parametrize("variant", [0, 231, 246, 247, 420, 421, 423])
+@pytest.mark.parametrize("variant", [0, 231, 246, 247, 420, 421, 423, 424, 429])
 def test_heal_ws_rs164(oracle, k, m, blen, erased, variant):
     """RS(16+4) heal (rebuild 1-4 shards and hash them) on k_vr_ws: the product shapes
     (231 = the product dispatch without the small-batch latency path that variant 0 takes
     at 11 blocks) and their memory-policy / layout variants (246 plain loads, 247 64-bit
     addresses, 420 round-4 LDS stride, 421 region-interleaved workgroups, 423 high table
-    dwords from LDS).  The
+    dwords from LDS, 424 per-wave stamps, 429 the rebuild role without issue priority).  The
     launched family is asserted: tile edges, ragged tails and dead stripes of the
     8-stripe workgroup."""
     want = 4 if variant == 0 else 2
@@ -138,7 +138,7 @@ WS16_GET_CASES = [(16, 4, blen, erased, data_only)
 
 
 @pytest.mark.parametrize("k,m,blen,erased,data_only", WS16_GET_CASES)
-@pytest.mark.parametrize("variant", [0, 231, 246, 247, 420, 421, 423])
+@pytest.mark.parametrize("variant", [0, 231, 246, 247, 420, 421, 423, 424, 429])
 def test_verify_reconstruct_ws_rs164(oracle, k, m, blen, erased, data_only, variant):
     """The RS(16+4) rebuild-1..4 defaults (231: without the small-batch latency path
     that variant 0 takes at 11 blocks) run the warp-specialised kernel (asserted through
@@ -249,7 +249,7 @@ def test_fused_kernel_selected():
                                                   (8, 4, 8 * 640, [2, 10], True), (4, 2, 4 * 512, [1], True),
                                                   (16, 4, 16 * 256, [3, 17], False),
                                                   (16, 4, 16 * 256, [3, 17], True)])
-@pytest.mark.parametrize("variant", [0, 200, 420, 421, 423])
+@pytest.mark.parametrize("variant", [0, 200, 420, 421, 423, 429])
 def test_verify_reconstruct_large_batch(oracle, k, m, blen, erased, heal, variant):
     """4096 stripes through the default launch (k_vr_ws where it applies), the
     first-generation kernel (200, any variant the product GET dispatch does not serve) and
@@ -391,3 +391,51 @@ def test_verify_reconstruct_batch_masks(oracle, k, m, blen, heal, variant):
                 assert np.array_equal(got[b, i], sh[b, i]), (b, i)
             if heal and not pats[b, i]:
                 assert np.array_equal(out.cpu().numpy()[b, i], sums[b, i]), (b, i)
+
+
+@pytest.mark.parametrize("erased,heal", [([0, 5], False), ([0, 5], True), ([3, 13], True), ([1, 2, 3, 4], False),
+                                         ([7], True)])
+@pytest.mark.parametrize("variant", [0, 421, 423, 429])
+def test_verify_reconstruct_rs124_large(oracle, erased, heal, variant):
+    """RS(12+4) GET / heal above 1024 stripes on the warp-specialised kernel with
+    unaligned rows (S = 1 100: two 512-byte tiles and a 76-byte tail) and the
+    diagnostics forms of those instances (421 region-interleaved workgroups, 423 high
+    table dwords from LDS, 429 rebuild role without issue priority); every stripe vs the
+    oracle, one corrupt survivor flagged exactly."""
+    k, m, nb, S = 12, 4, 1030, 1100
+    R = k + m
+    mat = oracle.build_matrix(k, m)
+    base = np.stack([oracle.encode_data(k, m, oracle.fill(9, b, k * S), mat).reshape(R, S) for b in range(32)])
+    sh = np.concatenate([base] * (-(-nb // 32)))[:nb]
+    sums = np.stack([oracle.hh256_rows(KEY, s) for s in base])
+    sums = np.concatenate([sums] * (-(-nb // 32)))[:nb]
+    d = torch.from_numpy(sh.copy()).to(DEV)
+    for e in erased:
+        d[:, e, :] = 0x5A
+    survivors = [i for i in range(R) if i not in erased][:k]
+    bad_blk, bad_row = 1027, survivors[2]
+    d[bad_blk, bad_row, 1099] ^= 0x80
+    exp = torch.from_numpy(sums).to(DEV)
+    bad = torch.full((nb, R), 7, dtype=torch.int32, device=DEV)
+    out = torch.zeros((nb, R, 32), dtype=torch.uint8, device=DEV) if heal else None
+    with variant_ctx(variant):
+        z.Codec(k, m).verify_reconstruct_batch(d, R * S, S, nb, [i not in erased for i in range(R)], not heal, exp,
+                                               bad, sums_out=out)
+        torch.cuda.synchronize()
+        assert z.last_path() == 2, f"kernel family {z.last_path()} ran"
+    want = np.zeros((nb, R), np.int32)
+    want[bad_blk, bad_row] = 1
+    assert np.array_equal(bad.cpu().numpy(), want)
+    got = d.cpu().numpy()
+    rebuilt = [i for i in erased if i < k or heal]
+    ok = np.ones(nb, bool)
+    ok[bad_blk] = False
+    for i in range(R):
+        if i in erased and i not in rebuilt:
+            assert (got[:, i] == 0x5A).all()
+        else:
+            assert np.array_equal(got[ok, i], sh[ok, i]), f"shard {i}"
+    if heal:
+        o = out.cpu().numpy()
+        for i in rebuilt:
+            assert np.array_equal(o[ok, i], sums[ok, i]), f"heal sum of shard {i}"

@@ -86,9 +86,11 @@ static int launch_ehx_default(const EncArgs& a, hipStream_t s) {
     } else if constexpr (K == 4 && M == 4) {
         // RS(4+4), the 8-drive default: the RS(8+4) shape (16 stripes, 16-byte columns,
         // pair-form hash waves) for large batches, the RS(4+2) config-2 shape (4 stripes,
-        // quad-form hash waves, 4 tiles of prefetch) below.
+        // quad-form hash waves, 4 tiles of prefetch) below.  Round 5: with the conflict-free
+        // LDS row stride (SQ_LDS_BANK_CONFLICT 33.5 M per launch -> 0 at equal time,
+        // diagnostics 400 = the round-4 instance, profiles/r05/ab_enc.jsonl)
         if (n > 8 * 256)
-            return launch_ws<K, M, shape::PairG16>(a, s) ? PATH_WS : PATH_NONE;
+            return launch_ws<K, M, shape::Rs44Bulk>(a, s) ? PATH_WS : PATH_NONE;
         return launch_ws<K, M, shape::QuadSmall<3>>(a, s) ? PATH_WS : PATH_NONE;
     } else if constexpr (K == 4 && M == 2) {
         // config 2 (1024 objects, 6 144 chains: the chain latency sets the pace): 2 KiB

@@ -846,6 +846,14 @@ constexpr int vr_nh() {
 // result discarded), so the rebuild waves' survivor loads hit L2.
 // TSP (round 5): LDS row stride rule, as k_ehx_ws (ws_ts; 0 = the round-1 padding).
 // XMAP (round 5): workgroup -> stripe-group order, as k_ehx_ws (ws_group).
+// PRIO (round 5): the rebuild role's s_setprio.  The hash waves are the oldest waves of the
+// workgroup, so age-ordered VALU arbitration served them first although they wait 60-80 %
+// of each step at the barrier (per-wave stamps, diagnostics 424), while the younger
+// rebuild wave of each SIMD finished the step alone.  Priority 1 for the rebuild role:
+// RS(16+4) rebuild 2-4 / heal 2-4 5-8 % faster, RS(12+4) 3-8 %, RS(8+4) 1-4 %, RS(6+4)
+// 1-4 % (profiles/r05/ab_prio_get.jsonl, diagnostics 429 = the other priority).  The
+// quad-form shapes keep 0: their hash chains are few and latency-bound, and the priority
+// cost RS(4+2) heal 8 % and RS(2+2) 12-20 %.
 struct GetShape {
     static constexpr int G = 0;          // stripes per workgroup (every shape sets it)
     static constexpr int T = 0;          // tile: bytes of each row per step (every shape sets it)
@@ -861,6 +869,10 @@ struct GetShape {
     static constexpr int TSP = 0;        // LDS row stride rule
     static constexpr int XMAP = 0;       // workgroup -> stripe-group order
     static constexpr bool STH = false;   // with ST + BT: the tables' high dwords from LDS (below)
+    static constexpr bool WT = false;    // diagnostics: per-wave barrier / load-wait cycle stamps
+    static constexpr int WPE = 2;        // waves per SIMD the register budget is sized for
+    static constexpr int LDSMIN = 83968; // dynamic-LDS floor (83 968: one workgroup per CU)
+    static constexpr int PRIO = 1;       // s_setprio of the rebuild role
     static constexpr bool DIAGMOD = false;  // a diagnostics modifier of a product shape (Tsp0, XMap, ...)
 };
 // The instance a launch picks for a requested shape: its memory policy (non-temporal,
@@ -873,7 +885,7 @@ struct VrMem : C {
 
 template <int K, int EX, bool HOUT, class C>
 __global__ void __launch_bounds__((vr_nh<C::G, K + (HOUT ? EX : 0), C::HQ>() + C::G * (C::T / C::CW)))
-__attribute__((amdgpu_waves_per_eu(2))) k_vr_ws(VrArgs a) {
+__attribute__((amdgpu_waves_per_eu(C::WPE))) k_vr_ws(VrArgs a) {
     constexpr int G = C::G, T = C::T, PF = C::PF, CW = C::CW, BT = C::BT, PFD = C::PFD;
     constexpr bool HQ = C::HQ, ST = C::ST, NTL = C::NTL, UA = C::UA, BUF = C::BUF;
     // STH (round 5): a v_perm reads at most one SGPR, so with scalar tables each
@@ -905,6 +917,35 @@ __attribute__((amdgpu_waves_per_eu(2))) k_vr_ws(VrArgs a) {
         for (int i = tid; i < EX * K * 8; i += NT) tabs[i] = a.tables[i];
     if constexpr (STH)
         for (int i = tid; i < EX * K; i += NT) htabs[i] = make_uint2(a.tables[8 * i + 1], a.tables[8 * i + 3]);
+    // WT (diagnostics): per-wave real time, shader cycles, HW_ID and the cycles spent in
+    // barriers / in the rebuild role's survivor-load waits (k_ehx_ws's stamp format: waves
+    // 0..NH/64-1 of a workgroup hash, the rest rebuild)
+    uint64_t rt0 = 0, ct0 = 0, wbar = 0, wvm = 0;
+    if (C::WT && a.dbg) {
+        rt0 = __builtin_amdgcn_s_memrealtime();
+        ct0 = __builtin_amdgcn_s_memtime();
+    }
+    auto bar = [&]() {
+        if constexpr (C::WT) {
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            lds_barrier2();
+            wbar += __builtin_amdgcn_s_memtime() - t;
+        } else {
+            lds_barrier2();
+        }
+    };
+    auto stamp = [&]() {
+        if (C::WT && a.dbg && (tid & 63) == 0) {
+            const uint64_t rt1 = __builtin_amdgcn_s_memrealtime();
+            const uint64_t ct1 = __builtin_amdgcn_s_memtime();
+            uint64_t* d = a.dbg + ((int64_t)blockIdx.x * (NT / 64) + (tid >> 6)) * 5;
+            d[0] = rt0;
+            d[1] = rt1;
+            d[2] = ct1 - ct0;
+            d[3] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_ID
+            d[4] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) | ((wbar & 0xFFFFFFF) << 8) | (wvm << 36);
+        }
+    };
     for (int i = tid; i < K + EX; i += NT) srows[i] = a.rows[i];
     const int64_t nfull = S / T;
     const int tail = (int)(S - nfull * T);
@@ -950,9 +991,9 @@ __attribute__((amdgpu_waves_per_eu(2))) k_vr_ws(VrArgs a) {
         const int row_off = crow * TS + 8 * lane;
         const uint32_t sel = zipper_sel(lane);
         HHLane st = hh_init(lane, a.key[0], a.key[1], a.key[2], a.key[3]);
-        lds_barrier2();  // tables / rows (matches the rebuild role)
+        bar();  // tables / rows (matches the rebuild role)
         pf_setup();
-        lds_barrier2();  // step 0
+        bar();  // step 0
         for (int64_t s = 1; s <= nfull; ++s) {
             pf_issue(s);
             const uint64_t* p = reinterpret_cast<const uint64_t*>(tile[(s - 1) & 1] + row_off);
@@ -961,7 +1002,7 @@ __attribute__((amdgpu_waves_per_eu(2))) k_vr_ws(VrArgs a) {
             for (int i = 0; i < NPK; ++i) w[i] = p[4 * i];
 #pragma unroll
             for (int i = 0; i < NPK; ++i) hh_update(st, w[i], sel);
-            lds_barrier2();
+            bar();
         }
         pf_drain();
         if (tail) {
@@ -969,7 +1010,7 @@ __attribute__((amdgpu_waves_per_eu(2))) k_vr_ws(VrArgs a) {
             hh_packets(st, row, tail >> 5, lane, sel);
             if (tail & 31) hh_remainder(st, row + (tail & ~31), (uint32_t)(tail & 31), lane, sel);
         }
-        for (int64_t s = nfull + 1; s < total; ++s) lds_barrier2();
+        for (int64_t s = nfull + 1; s < total; ++s) bar();
         const uint64_t h = hh_finalize256(st, lane, sel);
         const bool live = chain < G * RH && blk0 + g < a.n_blocks;
         const int64_t b = live && a.ids ? (int64_t)a.ids[blk0 + g] : blk0 + g;
@@ -987,6 +1028,7 @@ __attribute__((amdgpu_waves_per_eu(2))) k_vr_ws(VrArgs a) {
         } else if (HOUT && live && a.sums_out) {
             *reinterpret_cast<uint64_t*>(a.sums_out + (b * R + srow) * 32 + 8 * lane) = h;
         }
+        stamp();
         return;
     }
     if (!HQ && __builtin_amdgcn_readfirstlane(tid) < NH) {
@@ -998,9 +1040,9 @@ __attribute__((amdgpu_waves_per_eu(2))) k_vr_ws(VrArgs a) {
         const int g = chain / RH, cj = chain % RH;
         const int row_off = chain * TS;
         HHPair st = hh2_init(hh, a.key[0], a.key[1], a.key[2], a.key[3]);
-        lds_barrier2();  // tables / rows (matches the rebuild role)
+        bar();  // tables / rows (matches the rebuild role)
         pf_setup();
-        lds_barrier2();  // step 0
+        bar();  // step 0
         for (int64_t s = 1; s <= nfull; ++s) {
             pf_issue(s);
             const uint4* p = reinterpret_cast<const uint4*>(tile[(s - 1) & 1] + row_off) + hh;
@@ -1010,7 +1052,7 @@ __attribute__((amdgpu_waves_per_eu(2))) k_vr_ws(VrArgs a) {
 #pragma unroll
             for (int i = 0; i < NPK; ++i)
                 hh2_update(st, ((uint64_t)w[i].y << 32) | w[i].x, ((uint64_t)w[i].w << 32) | w[i].z);
-            lds_barrier2();
+            bar();
         }
         pf_drain();
         if (tail) {
@@ -1018,7 +1060,7 @@ __attribute__((amdgpu_waves_per_eu(2))) k_vr_ws(VrArgs a) {
             hh2_packets(st, row, tail >> 5, hh);
             if (tail & 31) hh2_remainder(st, row + (tail & ~31), (uint32_t)(tail & 31), hh);
         }
-        for (int64_t s = nfull + 1; s < total; ++s) lds_barrier2();
+        for (int64_t s = nfull + 1; s < total; ++s) bar();
         uint64_t d0, d1;
         hh2_finalize256(st, d0, d1);
         const bool live = !pad && blk0 + g < a.n_blocks;
@@ -1041,6 +1083,7 @@ __attribute__((amdgpu_waves_per_eu(2))) k_vr_ws(VrArgs a) {
             out[0] = d0;
             out[1] = d1;
         }
+        stamp();
         return;
     }
 
@@ -1058,7 +1101,8 @@ __attribute__((amdgpu_waves_per_eu(2))) k_vr_ws(VrArgs a) {
     const __amdgpu_buffer_rsrc_t rs_s =
         __builtin_amdgcn_make_buffer_rsrc((void*)(a.shards + blk0 * a.block_stride), 0, 0x7FFFFFFF, 0x00020000);
     const uint32_t vo_s = (uint32_t)((bl - blk0) * a.block_stride + o);
-    lds_barrier2();  // tables / rows visible
+    bar();  // tables / rows visible
+    if constexpr (C::PRIO > 0) __builtin_amdgcn_s_setprio(C::PRIO);
     // row offsets in 32 bits (the launch requires (k + m) * S < 2^31): half the SGPRs
     uint32_t roff[K];
 #pragma unroll
@@ -1237,11 +1281,17 @@ __attribute__((amdgpu_waves_per_eu(2))) k_vr_ws(VrArgs a) {
     };
     auto step = [&](VT (&xs)[K], int64_t ti) {
         Col<NWd> y[EX > 0 ? EX : 1];
-        vm_wait<EX + (PF - 1) * (K + EX)>(xs);
+        if constexpr (C::WT) {
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            vm_wait<EX + (PF - 1) * (K + EX)>(xs);
+            wvm += __builtin_amdgcn_s_memtime() - t;
+        } else {
+            vm_wait<EX + (PF - 1) * (K + EX)>(xs);
+        }
         rebuild(xs, tile[ti & 1], y);
         load(xs, (ti + PF) * T);
         store_rows(y, ti * T);
-        lds_barrier2();
+        bar();
     };
     auto store_tail = [&](const Col<NWd> (&y)[EX > 0 ? EX : 1]) {
         uint8_t* t0p = blk + nfull * T;
@@ -1268,7 +1318,7 @@ __attribute__((amdgpu_waves_per_eu(2))) k_vr_ws(VrArgs a) {
         } else {
             if (full || (part && o < tail)) store_rows(y, ti * T);
         }
-        lds_barrier2();
+        bar();
     };
 #pragma unroll
     for (int p = 0; p < PF; ++p) prefetch_any(x[p], p);
@@ -1284,9 +1334,10 @@ __attribute__((amdgpu_waves_per_eu(2))) k_vr_ws(VrArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
     for (int p = 0; p < 2 * PF; ++p) edge(x[p % PF], i + p);
-    lds_barrier2();  // the hash-only step
+    bar();  // the hash-only step
 #pragma unroll
     for (int p = 0; p < PF; ++p) vm_wait<0>(x[p]);
+    stamp();
 }
 
 template <int K, int EX, bool HOUT, class C>
@@ -1294,11 +1345,6 @@ static bool launch_vr_inst(const VrArgs& a, hipStream_t s);
 
 // Shape modifiers (diagnostics A/B of a product shape): the conflict-free LDS row stride,
 // the region-interleaved workgroup order.
-template <class C>
-struct Tsp1 : C {
-    static constexpr int TSP = 1;
-    static constexpr bool DIAGMOD = true;
-};
 template <class C, int P>
 struct XMap : C {
     static constexpr int XMAP = P;
@@ -1310,8 +1356,31 @@ struct Tsp0 : C {
     static constexpr bool DIAGMOD = true;
 };
 template <class C>
+struct Stamped : C {
+    static constexpr bool WT = true;
+    static constexpr bool DIAGMOD = true;
+};
+template <class C>
 struct Sth : C {
     static constexpr bool STH = true;
+    static constexpr bool DIAGMOD = true;
+};
+// The rebuild role's issue priority (PRIO above k_vr_ws).
+template <class C, int P>
+struct RbPrio : C {
+    static constexpr int PRIO = P;
+    static constexpr bool DIAGMOD = true;
+};
+// Encode non-temporal policy (NTM above k_ehx_ws).
+template <class C, int N>
+struct Ntm : C {
+    static constexpr int NTM = N;
+    static constexpr bool DIAGMOD = true;
+};
+// Encode issue-priority scheme (PM above k_ehx_ws).
+template <class C, int P>
+struct Pm : C {
+    static constexpr int PM = P;
     static constexpr bool DIAGMOD = true;
 };
 // C itself when P == 0 (product instances keep their shape's name)
@@ -1326,7 +1395,7 @@ static bool launch_vr_ws_t(const VrArgs& a, hipStream_t s) {
     // not modified again): 420 = the round-4 LDS row stride (TSP 0) on the pair-form
     // shapes of k = 8 / 12 / 16; 421 = the region-interleaved workgroup order (ws_group, 8
     // regions; k = 8 / 12 / 16); 423 = the tables' high dwords from LDS (STH) on every
-    // scalar-table shape.  Instantiated for those k only: every modifier multiplies the
+    // scalar-table shape; 424 = per-wave stamps (WT).  Instantiated for those k only: every modifier multiplies the
     // diagnostics library by the product GET instances.
     if constexpr (!C::DIAGMOD) {
         if constexpr (C::TSP == 1 && !C::HQ && (K == 8 || K == 12 || K == 16)) {
@@ -1338,6 +1407,13 @@ static bool launch_vr_ws_t(const VrArgs& a, hipStream_t s) {
         if constexpr (C::ST && C::BT > 0 && EX > 0) {
             if (a.variant == 423) return launch_vr_ws_t<K, EX, HOUT, Sth<C>>(a, s);
         }
+        // 424: the product shape with per-wave stamps (k = 8 / 12 / 16)
+        if constexpr (K == 8 || K == 12 || K == 16) {
+            if (a.variant == 424) return launch_vr_ws_t<K, EX, HOUT, Stamped<C>>(a, s);
+        }
+        // 429: the other rebuild-role priority (the pair-form shapes without it, as in round
+        // 4; the quad-form shapes with it)
+        if (a.variant == 429) return launch_vr_ws_t<K, EX, HOUT, RbPrio<C, C::PRIO ? 0 : 1>>(a, s);
     }
 #endif
     if constexpr (C::BUF && !C::UA) {
@@ -1372,7 +1448,7 @@ static bool launch_vr_inst(const VrArgs& a, hipStream_t s) {
     constexpr int RH = K + (HOUT ? EX : 0);
     constexpr int NT = vr_nh<G, RH, C::HQ>() + G * (T / CW);
     constexpr size_t tiles = (size_t)2 * G * RH * ws_ts<T, C::HQ, C::TSP>();
-    constexpr size_t dyn = tiles > 83968 ? tiles : 83968;  // one workgroup per CU
+    constexpr size_t dyn = tiles > (size_t)C::LDSMIN ? tiles : (size_t)C::LDSMIN;
     static_assert(G > 0 && T > 0, "a shape names its stripes per workgroup and tile length");
     if constexpr (dyn + (size_t)(EX > 0 ? EX : 1) * K * (32 + (C::STH ? 8 : 0)) + 4 * (K + EX) > 163840 || NT > 1024 ||
                   vr_nh<G, RH, C::HQ>() % 64 != 0 || (G * (T / CW)) % 64 != 0) {
@@ -1407,6 +1483,11 @@ struct Rs84Bulk : PairG16 {
     static constexpr bool BUF = true;
     static constexpr int TSP = 1, XMAP = 8;
 };
+// RS(4+4) above 2048 stripes: PairG16 with the conflict-free LDS row stride (round 5:
+// 4 096 / 16 384 x 1 MiB 1.78-1.83 / 7.09-7.14 ms either way, bank conflicts 20 % -> 0).
+struct Rs44Bulk : PairG16 {
+    static constexpr int TSP = 1;
+};
 // RS(8+4) up to 2048 stripes: 4 stripes of 1 KiB tiles, quad-form hash waves, two tiles
 // of prefetch, one workgroup per CU (LDSMIN), the 256-VGPR budget.
 struct Rs84Mid : EncShape {
@@ -1416,9 +1497,11 @@ struct Rs84Mid : EncShape {
 // RS(16+4) above 1024 stripes: 8 stripes of 384-byte tiles, 8-byte buffer-addressed
 // columns, data rows to LDS before the encode; round 5: conflict-free LDS rows and the
 // region-interleaved workgroup order (8 192 x 1 MiB 2.342-2.370 -> 2.314-2.341 ms,
-// diagnostics 417, profiles/r05/ab_enc2.jsonl).
+// diagnostics 417, profiles/r05/ab_enc2.jsonl), then the encode waves at issue priority 1
+// (PM 1, as the RS(8+4) shape: 2.37-2.40 -> 2.28-2.29 ms, diagnostics 403 before its
+// adoption, profiles/r05/ab_prio_enc.jsonl).
 struct Rs164Bulk : EncShape {
-    static constexpr int G = 8, T = 384, NTM = 3, EP = 2, TSP = 1, XMAP = 8;
+    static constexpr int G = 8, T = 384, NTM = 3, EP = 2, TSP = 1, XMAP = 8, PM = 1;
     static constexpr bool BUF = true;
 };
 // Quad-form hash waves on 4 stripes of 512-byte tiles (RS(16+4) / RS(12+4) small batches).
@@ -1487,7 +1570,7 @@ struct Gen8x512 : GenBase {
 // 1 KiB tiles (PF tiles of prefetch).
 template <int T_, int PF_>
 struct K4Quad : GetShape {
-    static constexpr int G = 8, T = T_, PF = PF_;
+    static constexpr int G = 8, T = T_, PF = PF_, PRIO = 0;
     static constexpr bool HQ = true;
 };
 // RS(8+4): 16 stripes of 256-byte tiles (verify, rebuild 1-2); 8-byte columns with
@@ -1534,7 +1617,7 @@ struct Wide512 : GetShape {
 // k = 2, 3: 8 stripes of 1 KiB tiles, quad-form hash waves; k = 5-7: 16 stripes of 256.
 template <bool UA_>
 struct GenGetQuad1K : GetShape {
-    static constexpr int G = 8, T = 1024, PF = 2, BT = 4;
+    static constexpr int G = 8, T = 1024, PF = 2, BT = 4, PRIO = 0;
     static constexpr bool HQ = true, ST = true, UA = UA_;
 };
 template <bool UA_>

@@ -8,8 +8,8 @@
 //                   arithmetic / no GF arithmetic / neither — the memory pattern alone,
 //                   the headline's pattern roof
 //  313              Rs84Bulk with per-wave barrier / load-wait stamps (scripts/stamps3.py)
-//  400 / 401        the conflict-free LDS row stride (TSP 1) alone on the RS(4+4) bulk shape
-//                   (PairG16) and the RS(16+4) bulk shape
+//  400 / 401        the RS(4+4) bulk shape without the conflict-free LDS row stride (PairG16,
+//                   the round-4 product) / the RS(16+4) bulk shape without XMAP
 //  402              RS(4+4) on the RS(8+4) headline shape (Rs84Bulk)
 //  409-414          Rs84Bulk with the region-interleaved workgroup order (ws_group) over 1
 //                   (none: the round-4 product) / 2 / 4 / 8 (the product) / 16 / 32 regions
@@ -17,6 +17,12 @@
 //                   (417 = the round-4 product)
 //  416              the RS(12+4) 1 KiB UA shape without XMAP (the round-4 product)
 //  418              XMAP 8 on PairG16 (RS(4+4) / RS(4+2) bulk); 419 XMAP 8 on every GEN shape
+//  403 / 404        the RS(16+4) bulk shape with PM 0 (the encode waves without issue
+//                   priority) / the RS(12+4) 1 KiB UA shape with PM 1; 405 / 406 Rs84Bulk
+//                   with PM 2 (the younger encode wave of each SIMD pair at 2) / PM 0;
+//                   407 the RS(16+4) bulk shape with PM 2
+//  408              the RS(12+4) 1 KiB UA shape with temporal data loads (NTM 2): a tile's
+//                   last 128-byte line of a row is the next tile's first
 #include "fused_v2.hpp"
 
 namespace zs3k {
@@ -51,12 +57,14 @@ bool launch_ehx_diag(int v, const EncArgs& a, hipStream_t s) {
             case 412: return launch_ws<8, 4, XMap<Rs84Bulk, 8>>(a, s);
             case 413: return launch_ws<8, 4, XMap<Rs84Bulk, 16>>(a, s);
             case 414: return launch_ws<8, 4, XMap<Rs84Bulk, 32>>(a, s);
+            case 405: return launch_ws<8, 4, Pm<Rs84Bulk, 2>>(a, s);
+            case 406: return launch_ws<8, 4, Pm<Rs84Bulk, 0>>(a, s);
             default: return false;
         }
     }
     if (a.k == 4 && (a.m == 4 || a.m == 2)) {
         switch (v) {
-            case 400: return a.m == 4 && launch_ws<4, 4, Tsp1<PairG16>>(a, s);
+            case 400: return a.m == 4 && launch_ws<4, 4, PairG16>(a, s);
             case 402: return a.m == 4 && launch_ws<4, 4, Rs84Bulk>(a, s);
             case 418: return a.m == 4 ? launch_ws<4, 4, XMap<PairG16, 8>>(a, s) : launch_ws<4, 2, XMap<PairG16, 8>>(a, s);
             default: return false;
@@ -67,10 +75,14 @@ bool launch_ehx_diag(int v, const EncArgs& a, hipStream_t s) {
             case 401: return launch_ws<16, 4, XMap<Rs164Bulk, 0>>(a, s);
             case 415: return launch_ws<16, 4, Tsp0<Rs164Bulk>>(a, s);
             case 417: return launch_ws<16, 4, XMap<Tsp0<Rs164Bulk>, 0>>(a, s);
+            case 403: return launch_ws<16, 4, Pm<Rs164Bulk, 0>>(a, s);
+            case 407: return launch_ws<16, 4, Pm<Rs164Bulk, 2>>(a, s);
             default: return false;
         }
     }
     if (a.k == 12 && a.m == 4 && v == 416) return launch_ws<12, 4, XMap<Rs124Ua1K, 0>>(a, s);
+    if (a.k == 12 && a.m == 4 && v == 404) return launch_ws<12, 4, Pm<Rs124Ua1K, 1>>(a, s);
+    if (a.k == 12 && a.m == 4 && v == 408) return launch_ws<12, 4, Ntm<Rs124Ua1K, 2>>(a, s);
     if (v == 419) return launch_ehx_gen_xmap(a, s);
     return false;
 }

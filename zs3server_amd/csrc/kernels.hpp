@@ -122,6 +122,7 @@ struct VrArgs {
     const int32_t* ids;       // optional device block-slot list
     int variant;
     const int32_t* h_rows;    // host copy of `rows` (k survivors, then e rebuilt rows)
+    uint64_t* dbg;            // diagnostics build only: per-wave stamps (nullptr in the product)
 };
 
 // Batched MD5 / SHA-256 (digest.hip): message i of lens[i] (or len) bytes at

@@ -582,6 +582,9 @@ int zs3_verify_reconstruct_batch(const zs3_codec* cc, uint8_t* d_shards, int64_t
     a.h_rows = plan->rows.data();
     key_words(nullptr, a.key);
     a.variant = call_variant();
+#if ZS3_DIAG
+    a.dbg = t_dbg;
+#endif
     int path = zs3k::PATH_NONE;
     rc = map_hip(zs3k::launch_verify_reconstruct(a, (hipStream_t)stream, &path));
     t_last_path = path;

@@ -79,9 +79,9 @@ def test_other_shapes_variants(oracle, variant, k, m, blen):
 
 # RS(12+4) on blocks whose shard rows are not 16-byte aligned (1 MiB: S = 87 382) runs
 # k_ehx_ws in UA mode; diagnostics 416 = the product shape with the region-interleaved
-# workgroup order, 404 = encode waves at priority 1, 408 = temporal data loads
-# (fused_v2_diag.hip)
-@pytest.mark.parametrize("variant", [0, 404, 408, 416])
+# workgroup order, 404 = encode waves at priority 1, 408 / 435 / 436 = temporal data loads /
+# parity stores / both (fused_v2_diag.hip)
+@pytest.mark.parametrize("variant", [0, 404, 408, 416, 435, 436])
 @pytest.mark.parametrize("blen,nb", [(1 << 20, 3), (1 << 20, 9), (12 * (512 * 3 + 100) - 6, 17)])
 def test_rs124_ua_variants(oracle, variant, blen, nb):
     with variant_ctx(variant):

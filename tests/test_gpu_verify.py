@@ -76,7 +76,7 @@ WS_CASES = [(8, 4, 1 << 16, []), (8, 4, 1 << 16, [0, 5]), (8, 4, 1 << 16, [3, 9]
 @pytest.mark.parametrize("k,m,blen,erased", WS_CASES)
 @pytest.mark.parametrize("data_only", [True, False])
 @pytest.mark.parametrize("heal", [False, True])
-@pytest.mark.parametrize("variant", [0, 230, 231, 246, 247, 420, 421, 423, 424, 429])
+@pytest.mark.parametrize("variant", [0, 230, 231, 246, 247, 420, 421, 423, 424, 429, 434])
 def test_verify_reconstruct_ws(oracle, k, m, blen, erased, data_only, heal, variant):
     """Variant 0: the product dispatch; at 17 blocks it takes the small-batch latency
     path (k_reconstruct + one chain per quad; 230 forces it).  231 = the product dispatch
@@ -114,13 +114,14 @@ WS16_HEAL_CASES = [(16, 4, 1 << 16, [0, 5]), (16, 4, 1 << 16, [3, 17]), (16, 4, 
 
 
 @pytest.mark.parametrize("k,m,blen,erased", WS16_HEAL_CASES)
-@pytest.mark.parametrize("variant", [0, 231, 246, 247, 420, 421, 423, 424, 429])
+@pytest.mark.parametrize("variant", [0, 231, 246, 247, 420, 421, 423, 424, 429, 434])
 def test_heal_ws_rs164(oracle, k, m, blen, erased, variant):
     """RS(16+4) heal (rebuild 1-4 shards and hash them) on k_vr_ws: the product shapes
     (231 = the product dispatch without the small-batch latency path that variant 0 takes
     at 11 blocks) and their memory-policy / layout variants (246 plain loads, 247 64-bit
     addresses, 420 round-4 LDS stride, 421 region-interleaved workgroups, 423 high table
-    dwords from LDS, 424 per-wave stamps, 429 the rebuild role without issue priority).  The
+    dwords from LDS, 424 per-wave stamps, 429 the rebuild role without issue priority, 434
+    survivor splits before the first table wait).  The
     launched family is asserted: tile edges, ragged tails and dead stripes of the
     8-stripe workgroup."""
     want = 4 if variant == 0 else 2
@@ -138,7 +139,7 @@ WS16_GET_CASES = [(16, 4, blen, erased, data_only)
 
 
 @pytest.mark.parametrize("k,m,blen,erased,data_only", WS16_GET_CASES)
-@pytest.mark.parametrize("variant", [0, 231, 246, 247, 420, 421, 423, 424, 429])
+@pytest.mark.parametrize("variant", [0, 231, 246, 247, 420, 421, 423, 424, 429, 434])
 def test_verify_reconstruct_ws_rs164(oracle, k, m, blen, erased, data_only, variant):
     """The RS(16+4) rebuild-1..4 defaults (231: without the small-batch latency path
     that variant 0 takes at 11 blocks) run the warp-specialised kernel (asserted through
@@ -395,12 +396,13 @@ def test_verify_reconstruct_batch_masks(oracle, k, m, blen, heal, variant):
 
 @pytest.mark.parametrize("erased,heal", [([0, 5], False), ([0, 5], True), ([3, 13], True), ([1, 2, 3, 4], False),
                                          ([7], True)])
-@pytest.mark.parametrize("variant", [0, 421, 423, 429])
+@pytest.mark.parametrize("variant", [0, 421, 423, 429, 434])
 def test_verify_reconstruct_rs124_large(oracle, erased, heal, variant):
     """RS(12+4) GET / heal above 1024 stripes on the warp-specialised kernel with
     unaligned rows (S = 1 100: two 512-byte tiles and a 76-byte tail) and the
     diagnostics forms of those instances (421 region-interleaved workgroups, 423 high
-    table dwords from LDS, 429 rebuild role without issue priority); every stripe vs the
+    table dwords from LDS, 429 rebuild role without issue priority, 434 survivor splits
+    first); every stripe vs the
     oracle, one corrupt survivor flagged exactly."""
     k, m, nb, S = 12, 4, 1030, 1100
     R = k + m

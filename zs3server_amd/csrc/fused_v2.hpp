@@ -854,6 +854,10 @@ constexpr int vr_nh() {
 // 1-4 % (profiles/r05/ab_prio_get.jsonl, diagnostics 429 = the other priority).  The
 // quad-form shapes keep 0: their hash chains are few and latency-bound, and the priority
 // cost RS(4+2) heal 8 % and RS(2+2) 12-20 %.
+// SPL (round 5): the survivors' nibble splits are computed before the first coefficient
+// batch is waited for, so its scalar loads land behind that work: RS(16+4) rebuild 3-4 /
+// heal 4 and RS(8+4) rebuild 4 1.5-4 % faster, the other shapes within noise
+// (profiles/r05/ab_spl.jsonl; diagnostics 434 = the other placement).
 struct GetShape {
     static constexpr int G = 0;          // stripes per workgroup (every shape sets it)
     static constexpr int T = 0;          // tile: bytes of each row per step (every shape sets it)
@@ -873,6 +877,8 @@ struct GetShape {
     static constexpr int WPE = 2;        // waves per SIMD the register budget is sized for
     static constexpr int LDSMIN = 83968; // dynamic-LDS floor (83 968: one workgroup per CU)
     static constexpr int PRIO = 1;       // s_setprio of the rebuild role
+    static constexpr int ABL = 0;        // diagnostics timing ablations (output differs)
+    static constexpr bool SPL = false;   // with ST + BT: survivor splits before the first table wait
     static constexpr bool DIAGMOD = false;  // a diagnostics modifier of a product shape (Tsp0, XMap, ...)
 };
 // The instance a launch picks for a requested shape: its memory policy (non-temporal,
@@ -894,6 +900,7 @@ __attribute__((amdgpu_waves_per_eu(C::WPE))) k_vr_ws(VrArgs a) {
     // LDS copy instead (one broadcast ds_read_b64 per coefficient, issued with its batch's
     // scalar loads), and the scalar loads fetch only the three dwords used as SGPRs.
     constexpr bool STH = C::STH && ST && BT > 0 && EX > 0;
+    constexpr bool SPL = C::SPL && ST && BT > 0 && !STH && EX > 0;
     constexpr int RH = K + (HOUT ? EX : 0);
     constexpr int NH = vr_nh<G, RH, HQ>();
     constexpr int CPS = T / CW;
@@ -1049,9 +1056,15 @@ __attribute__((amdgpu_waves_per_eu(C::WPE))) k_vr_ws(VrArgs a) {
             uint4 w[NPK];
 #pragma unroll
             for (int i = 0; i < NPK; ++i) w[i] = p[2 * i];
+            if constexpr (C::ABL == 3) {
+                // ablation: the tile's LDS reads without the HighwayHash arithmetic
 #pragma unroll
-            for (int i = 0; i < NPK; ++i)
-                hh2_update(st, ((uint64_t)w[i].y << 32) | w[i].x, ((uint64_t)w[i].w << 32) | w[i].z);
+                for (int i = 0; i < NPK; ++i) asm volatile("" ::"v"(w[i].x), "v"(w[i].y), "v"(w[i].z), "v"(w[i].w));
+            } else {
+#pragma unroll
+                for (int i = 0; i < NPK; ++i)
+                    hh2_update(st, ((uint64_t)w[i].y << 32) | w[i].x, ((uint64_t)w[i].w << 32) | w[i].z);
+            }
             bar();
         }
         pf_drain();
@@ -1214,6 +1227,19 @@ __attribute__((amdgpu_waves_per_eu(C::WPE))) k_vr_ws(VrArgs a) {
                 __builtin_amdgcn_sched_barrier(0);
             };
             if constexpr (ST && BT) load_batch(tbat[0], hbat[0], 0);
+            // SPL: every survivor's nibble split before the first table wait (they are all
+            // live across the rebuilt rows anyway), so the first batch's scalar loads land
+            // behind that VALU work instead of stalling the step's first product
+            Nib sp[SPL ? K : 1][NWd];
+            if constexpr (SPL) {
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int j = 0; j < K; ++j)
+#pragma unroll
+                    for (int w = 0; w < NWd; ++w) sp[j][w] = split_nibbles(xs[j].w[w]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            auto nib = [&](int j, int w) { return SPL ? sp[SPL ? j : 0][w] : split_nibbles(xs[j].w[w]); };
 #pragma unroll
             for (int r = 0; r < EX; ++r) {
                 GfAcc acc[NWd];
@@ -1222,10 +1248,12 @@ __attribute__((amdgpu_waves_per_eu(C::WPE))) k_vr_ws(VrArgs a) {
 #pragma unroll
                 for (int j = 0; j < K; ++j) {
                     if constexpr (ST && BT) {
-                        const int c = r * K + j, bi = c / NB, cur = bi & 1;
-                        if (c % NB == 0) {
+                        // ABL 1 (ablation): every product uses the first batch's tables, so
+                        // the loop issues no scalar loads and waits for none
+                        const int c = r * K + j, bi = C::ABL == 1 ? 0 : c / NB, cur = bi & 1;
+                        if (c % NB == 0 && (C::ABL != 1 || c == 0)) {
                             wait_batch(tbat[cur], hbat[cur]);
-                            if (c + NB < EX * K) load_batch(tbat[cur ^ 1], hbat[cur ^ 1], c + NB);
+                            if (c + NB < EX * K && C::ABL != 1) load_batch(tbat[cur ^ 1], hbat[cur ^ 1], c + NB);
                             __builtin_amdgcn_sched_barrier(0);
                         }
                         const CoefTab t = tbat[cur][c % NB];
@@ -1236,7 +1264,7 @@ __attribute__((amdgpu_waves_per_eu(C::WPE))) k_vr_ws(VrArgs a) {
                                 acc_add(acc[w], gf_lookup_sh(split_nibbles(xs[j].w[w]), t, hi.x, hi.y));
                         } else {
 #pragma unroll
-                            for (int w = 0; w < NWd; ++w) acc_add(acc[w], gf_lookup_s(split_nibbles(xs[j].w[w]), t));
+                            for (int w = 0; w < NWd; ++w) acc_add(acc[w], gf_lookup_s(nib(j, w), t));
                         }
                     } else if constexpr (ST) {
                         const CoefTab t = load_coef_s(tg, r * K + j);
@@ -1371,6 +1399,18 @@ struct RbPrio : C {
     static constexpr int PRIO = P;
     static constexpr bool DIAGMOD = true;
 };
+// Survivor splits before the first table wait (SPL above k_vr_ws).
+template <class C, bool S>
+struct Spl : C {
+    static constexpr bool SPL = S;
+    static constexpr bool DIAGMOD = true;
+};
+// Timing ablation of a product shape (output differs).
+template <class C, int A>
+struct Abl : C {
+    static constexpr int ABL = A;
+    static constexpr bool DIAGMOD = true;
+};
 // Encode non-temporal policy (NTM above k_ehx_ws).
 template <class C, int N>
 struct Ntm : C {
@@ -1410,6 +1450,17 @@ static bool launch_vr_ws_t(const VrArgs& a, hipStream_t s) {
         // 424: the product shape with per-wave stamps (k = 8 / 12 / 16)
         if constexpr (K == 8 || K == 12 || K == 16) {
             if (a.variant == 424) return launch_vr_ws_t<K, EX, HOUT, Stamped<C>>(a, s);
+        }
+        // 431 / 433: timing ablations (output differs) of RS(16+4) rebuild / heal 4 and
+        // RS(12+4) rebuild / heal 2: every product on the first batch's tables (no scalar
+        // table loads in the loop) / no HighwayHash arithmetic
+        if constexpr (((K == 16 && EX == 4) || (K == 12 && EX == 2)) && C::ST && C::BT > 0 && !C::HQ) {
+            if (a.variant == 431) return launch_vr_ws_t<K, EX, HOUT, Abl<C, 1>>(a, s);
+            if (a.variant == 433) return launch_vr_ws_t<K, EX, HOUT, Abl<C, 3>>(a, s);
+        }
+        // 434: the other survivor-split placement (SPL) on the scalar-table shapes
+        if constexpr (C::ST && C::BT > 0 && !C::HQ && EX >= 1 && (K == 8 || K == 12 || K == 16)) {
+            if (a.variant == 434) return launch_vr_ws_t<K, EX, HOUT, Spl<C, !C::SPL>>(a, s);
         }
         // 429: the other rebuild-role priority (the pair-form shapes without it, as in round
         // 4; the quad-form shapes with it)
@@ -1581,7 +1632,7 @@ struct K8Get : GetShape {
 };
 struct K8Rebuild34 : GetShape {
     static constexpr int G = 16, T = 256, CW = 8, BT = 4, TSP = 1;
-    static constexpr bool ST = true, BUF = true;
+    static constexpr bool ST = true, BUF = true, SPL = true;
 };
 struct K8Heal12 : GetShape {
     static constexpr int G = 16, T = 128, PF = 2, CW = 8, BT = 4, TSP = 1;
@@ -1602,11 +1653,11 @@ struct K16Rebuild12 : GetShape {
 };
 struct K16Rebuild34 : GetShape {
     static constexpr int G = 8, T = 512, CW = 8, BT = 4, TSP = 1;
-    static constexpr bool ST = true, BUF = true;
+    static constexpr bool ST = true, BUF = true, SPL = true;
 };
 struct K16Heal : GetShape {
     static constexpr int G = 8, T = 384, CW = 8, BT = 4, TSP = 1;
-    static constexpr bool ST = true, BUF = true;
+    static constexpr bool ST = true, BUF = true, SPL = true;
 };
 // RS(12+4) and k = 9-11: 8 stripes of 8-byte columns of 512-byte tiles, unaligned rows.
 template <bool UA_>

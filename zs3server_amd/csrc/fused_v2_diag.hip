@@ -21,8 +21,9 @@
 //                   priority) / the RS(12+4) 1 KiB UA shape with PM 1; 405 / 406 Rs84Bulk
 //                   with PM 2 (the younger encode wave of each SIMD pair at 2) / PM 0;
 //                   407 the RS(16+4) bulk shape with PM 2
-//  408              the RS(12+4) 1 KiB UA shape with temporal data loads (NTM 2): a tile's
-//                   last 128-byte line of a row is the next tile's first
+//  408 / 435 / 436  the RS(12+4) 1 KiB UA shape with temporal data loads (NTM 2) / temporal
+//                   parity stores (NTM 1) / both temporal (NTM 0): a tile's last 128-byte
+//                   line of a row is the next tile's first
 #include "fused_v2.hpp"
 
 namespace zs3k {
@@ -83,6 +84,8 @@ bool launch_ehx_diag(int v, const EncArgs& a, hipStream_t s) {
     if (a.k == 12 && a.m == 4 && v == 416) return launch_ws<12, 4, XMap<Rs124Ua1K, 0>>(a, s);
     if (a.k == 12 && a.m == 4 && v == 404) return launch_ws<12, 4, Pm<Rs124Ua1K, 1>>(a, s);
     if (a.k == 12 && a.m == 4 && v == 408) return launch_ws<12, 4, Ntm<Rs124Ua1K, 2>>(a, s);
+    if (a.k == 12 && a.m == 4 && v == 435) return launch_ws<12, 4, Ntm<Rs124Ua1K, 1>>(a, s);
+    if (a.k == 12 && a.m == 4 && v == 436) return launch_ws<12, 4, Ntm<Rs124Ua1K, 0>>(a, s);
     if (v == 419) return launch_ehx_gen_xmap(a, s);
     return false;
 }

@@ -76,15 +76,15 @@ WS_CASES = [(8, 4, 1 << 16, []), (8, 4, 1 << 16, [0, 5]), (8, 4, 1 << 16, [3, 9]
 @pytest.mark.parametrize("k,m,blen,erased", WS_CASES)
 @pytest.mark.parametrize("data_only", [True, False])
 @pytest.mark.parametrize("heal", [False, True])
-@pytest.mark.parametrize("variant", [0, 230, 231, 246, 247, 420, 421, 423, 424, 429, 434])
+@pytest.mark.parametrize("variant", [0, 230, 231, 246, 247, 420, 423, 424, 429, 434])
 def test_verify_reconstruct_ws(oracle, k, m, blen, erased, data_only, heal, variant):
     """Variant 0: the product dispatch; at 17 blocks it takes the small-batch latency
     path (k_reconstruct + one chain per quad; 230 forces it).  231 = the product dispatch
     without that path, asserted to run k_vr_ws for every RS(8+4) GET and heal with 0-4
-    rebuilt rows (zs3_last_path); 246 / 247 / 420 / 421 / 423 = the product shapes with
-    plain survivor loads / 64-bit addresses / the round-4 LDS row stride / the
-    region-interleaved workgroup order / the tables' high dwords from LDS (fused_v2.hpp
-    launch_vr_ws_t)."""
+    rebuilt rows (zs3_last_path); 246 / 247 / 420 / 423 = the product shapes with
+    plain survivor loads / 64-bit addresses / the round-4 LDS row stride / the tables'
+    high dwords from LDS, 424 per-wave stamps, 429 the other rebuild-role priority, 434
+    the other split placement (fused_v2.hpp launch_vr_ws_t)."""
     want = {0: 4, 230: 4}.get(variant, 2)
     with variant_ctx(variant):
         run_verify_case(oracle, k, m, blen, erased, data_only, heal, nb=17, want_path=want)
@@ -114,12 +114,12 @@ WS16_HEAL_CASES = [(16, 4, 1 << 16, [0, 5]), (16, 4, 1 << 16, [3, 17]), (16, 4, 
 
 
 @pytest.mark.parametrize("k,m,blen,erased", WS16_HEAL_CASES)
-@pytest.mark.parametrize("variant", [0, 231, 246, 247, 420, 421, 423, 424, 429, 434])
+@pytest.mark.parametrize("variant", [0, 231, 246, 247, 420, 423, 424, 429, 434])
 def test_heal_ws_rs164(oracle, k, m, blen, erased, variant):
     """RS(16+4) heal (rebuild 1-4 shards and hash them) on k_vr_ws: the product shapes
     (231 = the product dispatch without the small-batch latency path that variant 0 takes
     at 11 blocks) and their memory-policy / layout variants (246 plain loads, 247 64-bit
-    addresses, 420 round-4 LDS stride, 421 region-interleaved workgroups, 423 high table
+    addresses, 420 round-4 LDS stride, 423 high table
     dwords from LDS, 424 per-wave stamps, 429 the rebuild role without issue priority, 434
     survivor splits before the first table wait).  The
     launched family is asserted: tile edges, ragged tails and dead stripes of the
@@ -139,7 +139,7 @@ WS16_GET_CASES = [(16, 4, blen, erased, data_only)
 
 
 @pytest.mark.parametrize("k,m,blen,erased,data_only", WS16_GET_CASES)
-@pytest.mark.parametrize("variant", [0, 231, 246, 247, 420, 421, 423, 424, 429, 434])
+@pytest.mark.parametrize("variant", [0, 231, 246, 247, 420, 423, 424, 429, 434])
 def test_verify_reconstruct_ws_rs164(oracle, k, m, blen, erased, data_only, variant):
     """The RS(16+4) rebuild-1..4 defaults (231: without the small-batch latency path
     that variant 0 takes at 11 blocks) run the warp-specialised kernel (asserted through
@@ -250,12 +250,12 @@ def test_fused_kernel_selected():
                                                   (8, 4, 8 * 640, [2, 10], True), (4, 2, 4 * 512, [1], True),
                                                   (16, 4, 16 * 256, [3, 17], False),
                                                   (16, 4, 16 * 256, [3, 17], True)])
-@pytest.mark.parametrize("variant", [0, 200, 420, 421, 423, 429])
+@pytest.mark.parametrize("variant", [0, 200, 420, 423, 429])
 def test_verify_reconstruct_large_batch(oracle, k, m, blen, erased, heal, variant):
     """4096 stripes through the default launch (k_vr_ws where it applies), the
     first-generation kernel (200, any variant the product GET dispatch does not serve) and
-    the product shapes with the round-4 LDS row stride (420) / the region-interleaved
-    workgroup order (421) / the high table dwords from LDS (423); every stripe checked
+    the product shapes with the round-4 LDS row stride (420) / the high table dwords from
+    LDS (423) / the other rebuild-role priority (429); every stripe checked
     against the oracle, one corrupt survivor flagged."""
     nb = 4096
     R = k + m
@@ -396,11 +396,11 @@ def test_verify_reconstruct_batch_masks(oracle, k, m, blen, heal, variant):
 
 @pytest.mark.parametrize("erased,heal", [([0, 5], False), ([0, 5], True), ([3, 13], True), ([1, 2, 3, 4], False),
                                          ([7], True)])
-@pytest.mark.parametrize("variant", [0, 421, 423, 429, 434])
+@pytest.mark.parametrize("variant", [0, 423, 429, 434])
 def test_verify_reconstruct_rs124_large(oracle, erased, heal, variant):
     """RS(12+4) GET / heal above 1024 stripes on the warp-specialised kernel with
     unaligned rows (S = 1 100: two 512-byte tiles and a 76-byte tail) and the
-    diagnostics forms of those instances (421 region-interleaved workgroups, 423 high
+    diagnostics forms of those instances (423 high
     table dwords from LDS, 429 rebuild role without issue priority, 434 survivor splits
     first); every stripe vs the
     oracle, one corrupt survivor flagged exactly."""

@@ -1411,12 +1411,6 @@ struct Abl : C {
     static constexpr int ABL = A;
     static constexpr bool DIAGMOD = true;
 };
-// Encode non-temporal policy (NTM above k_ehx_ws).
-template <class C, int N>
-struct Ntm : C {
-    static constexpr int NTM = N;
-    static constexpr bool DIAGMOD = true;
-};
 // Encode issue-priority scheme (PM above k_ehx_ws).
 template <class C, int P>
 struct Pm : C {
@@ -1433,18 +1427,16 @@ static bool launch_vr_ws_t(const VrArgs& a, hipStream_t s) {
 #if ZS3_DIAG
     // Diagnostics A/B of a product GET shape (one modifier at a time: a modified shape is
     // not modified again): 420 = the round-4 LDS row stride (TSP 0) on the pair-form
-    // shapes of k = 8 / 12 / 16; 421 = the region-interleaved workgroup order (ws_group, 8
-    // regions; k = 8 / 12 / 16); 423 = the tables' high dwords from LDS (STH) on every
-    // scalar-table shape; 424 = per-wave stamps (WT).  Instantiated for those k only: every modifier multiplies the
-    // diagnostics library by the product GET instances.
+    // shapes of k = 8 / 12 / 16; 423 = the tables' high dwords from LDS (STH) on the
+    // scalar-table shapes of k = 8 / 12 / 16; 424 = per-wave stamps (WT).  Instantiated for those k only:
+    // every modifier multiplies the diagnostics library by the product GET instances.
+    // (421, the region-interleaved workgroup order, measured within +-1 % on k = 8 / 12 /
+    // 16 twice this round and was removed: profiles/r05/ab_get.jsonl, ab_get12_xmap.jsonl.)
     if constexpr (!C::DIAGMOD) {
         if constexpr (C::TSP == 1 && !C::HQ && (K == 8 || K == 12 || K == 16)) {
             if (a.variant == 420) return launch_vr_ws_t<K, EX, HOUT, Tsp0<C>>(a, s);
         }
-        if constexpr (C::XMAP == 0 && (K == 8 || K == 12 || K == 16)) {
-            if (a.variant == 421) return launch_vr_ws_t<K, EX, HOUT, XMap<C, 8>>(a, s);
-        }
-        if constexpr (C::ST && C::BT > 0 && EX > 0) {
+        if constexpr (C::ST && C::BT > 0 && EX > 0 && (K == 8 || K == 12 || K == 16)) {
             if (a.variant == 423) return launch_vr_ws_t<K, EX, HOUT, Sth<C>>(a, s);
         }
         // 424: the product shape with per-wave stamps (k = 8 / 12 / 16)
@@ -1464,7 +1456,9 @@ static bool launch_vr_ws_t(const VrArgs& a, hipStream_t s) {
         }
         // 429: the other rebuild-role priority (the pair-form shapes without it, as in round
         // 4; the quad-form shapes with it)
-        if (a.variant == 429) return launch_vr_ws_t<K, EX, HOUT, RbPrio<C, C::PRIO ? 0 : 1>>(a, s);
+        if constexpr (K == 2 || K == 4 || K == 6 || K == 8 || K == 12 || K == 16) {
+            if (a.variant == 429) return launch_vr_ws_t<K, EX, HOUT, RbPrio<C, C::PRIO ? 0 : 1>>(a, s);
+        }
     }
 #endif
     if constexpr (C::BUF && !C::UA) {

@@ -17,13 +17,12 @@
 //                   (417 = the round-4 product)
 //  416              the RS(12+4) 1 KiB UA shape without XMAP (the round-4 product)
 //  418              XMAP 8 on PairG16 (RS(4+4) / RS(4+2) bulk); 419 XMAP 8 on every GEN shape
-//  403 / 404        the RS(16+4) bulk shape with PM 0 (the encode waves without issue
-//                   priority) / the RS(12+4) 1 KiB UA shape with PM 1; 405 / 406 Rs84Bulk
-//                   with PM 2 (the younger encode wave of each SIMD pair at 2) / PM 0;
-//                   407 the RS(16+4) bulk shape with PM 2
-//  408 / 435 / 436  the RS(12+4) 1 KiB UA shape with temporal data loads (NTM 2) / temporal
-//                   parity stores (NTM 1) / both temporal (NTM 0): a tile's last 128-byte
-//                   line of a row is the next tile's first
+//  403              the RS(16+4) bulk shape with PM 0 (the encode waves without issue
+//                   priority, as before round 5's adoption)
+//  (Measured this round and removed: PM 2 / PM 0 on Rs84Bulk, PM 2 on the RS(16+4) bulk
+//  shape, PM 1 / temporal loads or stores / L2 prefetch 1 or 3 tiles ahead / XMAP 16 on the
+//  RS(12+4) UA shape, the LDS-counter hand-off and the L2 prefetch on Rs84Bulk:
+//  profiles/r05/ab_prio_enc*.jsonl, ab_ntm124.jsonl, ab_enc3.jsonl)
 #include "fused_v2.hpp"
 
 namespace zs3k {
@@ -58,8 +57,6 @@ bool launch_ehx_diag(int v, const EncArgs& a, hipStream_t s) {
             case 412: return launch_ws<8, 4, XMap<Rs84Bulk, 8>>(a, s);
             case 413: return launch_ws<8, 4, XMap<Rs84Bulk, 16>>(a, s);
             case 414: return launch_ws<8, 4, XMap<Rs84Bulk, 32>>(a, s);
-            case 405: return launch_ws<8, 4, Pm<Rs84Bulk, 2>>(a, s);
-            case 406: return launch_ws<8, 4, Pm<Rs84Bulk, 0>>(a, s);
             default: return false;
         }
     }
@@ -77,15 +74,10 @@ bool launch_ehx_diag(int v, const EncArgs& a, hipStream_t s) {
             case 415: return launch_ws<16, 4, Tsp0<Rs164Bulk>>(a, s);
             case 417: return launch_ws<16, 4, XMap<Tsp0<Rs164Bulk>, 0>>(a, s);
             case 403: return launch_ws<16, 4, Pm<Rs164Bulk, 0>>(a, s);
-            case 407: return launch_ws<16, 4, Pm<Rs164Bulk, 2>>(a, s);
             default: return false;
         }
     }
     if (a.k == 12 && a.m == 4 && v == 416) return launch_ws<12, 4, XMap<Rs124Ua1K, 0>>(a, s);
-    if (a.k == 12 && a.m == 4 && v == 404) return launch_ws<12, 4, Pm<Rs124Ua1K, 1>>(a, s);
-    if (a.k == 12 && a.m == 4 && v == 408) return launch_ws<12, 4, Ntm<Rs124Ua1K, 2>>(a, s);
-    if (a.k == 12 && a.m == 4 && v == 435) return launch_ws<12, 4, Ntm<Rs124Ua1K, 1>>(a, s);
-    if (a.k == 12 && a.m == 4 && v == 436) return launch_ws<12, 4, Ntm<Rs124Ua1K, 0>>(a, s);
     if (v == 419) return launch_ehx_gen_xmap(a, s);
     return false;
 }

@@ -1500,9 +1500,10 @@ static hipError_t run_vr(const VrArgs& a, hipStream_t s) {
 // The product GET / heal dispatch serves variant 0 and, in the diagnostics build, the
 // variants that change a product shape's memory policy or layout (launch_vr_ws_t in
 // fused_v2.hpp: 246 plain loads, 247 64-bit addresses, 420 the round-4 LDS stride,
-// 421 XCD-region workgroup order, 423 high table dwords from LDS, 424 per-wave stamps).
+// 423 high table dwords from LDS, 424 per-wave stamps, 429 the other rebuild-role
+// priority, 431 / 433 timing ablations, 434 the other split placement).
 static bool product_get_variant(int v) {
-    return v == 0 || (ZS3_DIAG && (v == 246 || v == 247 || v == 420 || v == 421 || v == 423 || v == 424 || v == 429 ||
+    return v == 0 || (ZS3_DIAG && (v == 246 || v == 247 || v == 420 || v == 423 || v == 424 || v == 429 ||
                           v == 431 || v == 433 || v == 434));
 }
 

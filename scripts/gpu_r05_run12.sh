@@ -1,0 +1,18 @@
+#!/bin/bash
+# Round 5 run 12: the survivor-quad RS(16+4) rebuild 4 / heal 4 kernel (diagnostics 440,
+# vr_quad.hpp): parity first (tile edges, dead stripes, 4096-stripe batches, a corrupt
+# survivor), then the A/B against the product.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest -q -x --timeout 120 --timeout-method thread -m gpu tests/test_gpu_verify.py -k "440 or 441" > gpurun_out/r05_t12.log 2>&1 || { tail -30 gpurun_out/r05_t12.log; exit 1; }
+tail -1 gpurun_out/r05_t12.log
+O=gpurun_out/r05_ab_quad.jsonl
+SHAPE=16:4:2048 VARIANTS=0,440,441 CASES="0,5,9,14;h0,1,16,19;0,1,2,3;h2,7,16,18" timeout -k 10 200 python scripts/get_ab.py > $O 2>&1 || exit 2
+SHAPE=16:4:8192 VARIANTS=0,440,441 CASES="0,5,9,14;h0,1,16,19" timeout -k 10 200 python scripts/get_ab.py >> $O 2>&1 || exit 3
+grep '^{' $O | python -c "
+import json,sys
+for l in sys.stdin:
+    d=json.loads(l); print(d['round'], d['objects'], d['erased'], d['heal'], d['variant'], d['ms'], d['frac'], d['path'], d['bad'])"
+echo run12 done

@@ -1,6 +1,6 @@
 """Per-kernel HBM bytes per launch from request-size counters (scripts/traffic_req.sh).
 Usage: traffic_req.py reads_counter_collection.csv writes_counter_collection.csv out.json
-Only the encode / GET kernels (k_ehx_ws, k_vr_ws) are kept; values are means over launches."""
+Only the encode / GET kernels (k_ehx_ws, k_vr_ws, k_vr_quad) are kept; values are means over launches."""
 import csv
 import json
 import sys
@@ -13,7 +13,7 @@ def load(path):
     with open(path) as f:
         for row in csv.DictReader(f):
             name = row["Kernel_Name"]
-            if "k_ehx_ws" not in name and "k_vr_ws" not in name:
+            if "k_ehx_ws" not in name and "k_vr_ws" not in name and "k_vr_quad" not in name:
                 continue
             per[name][row["Counter_Name"]] += float(row["Counter_Value"])
             seen[name].add(row.get("Dispatch_Id", row.get("Correlation_Id", "")))

@@ -114,14 +114,15 @@ WS16_HEAL_CASES = [(16, 4, 1 << 16, [0, 5]), (16, 4, 1 << 16, [3, 17]), (16, 4, 
 
 
 @pytest.mark.parametrize("k,m,blen,erased", WS16_HEAL_CASES)
-@pytest.mark.parametrize("variant", [0, 231, 246, 247, 420, 423, 424, 429, 434])
+@pytest.mark.parametrize("variant", [0, 231, 246, 247, 420, 423, 424, 429, 434, 440])
 def test_heal_ws_rs164(oracle, k, m, blen, erased, variant):
     """RS(16+4) heal (rebuild 1-4 shards and hash them) on k_vr_ws: the product shapes
     (231 = the product dispatch without the small-batch latency path that variant 0 takes
     at 11 blocks) and their memory-policy / layout variants (246 plain loads, 247 64-bit
     addresses, 420 round-4 LDS stride, 423 high table
     dwords from LDS, 424 per-wave stamps, 429 the rebuild role without issue priority, 434
-    survivor splits before the first table wait).  The
+    survivor splits before the first table wait, 440 the k_vr_ws instance instead of the
+    survivor-quad kernel (vr_quad.hpp) that the product runs for heal 4).  The
     launched family is asserted: tile edges, ragged tails and dead stripes of the
     8-stripe workgroup."""
     want = 4 if variant == 0 else 2
@@ -139,7 +140,7 @@ WS16_GET_CASES = [(16, 4, blen, erased, data_only)
 
 
 @pytest.mark.parametrize("k,m,blen,erased,data_only", WS16_GET_CASES)
-@pytest.mark.parametrize("variant", [0, 231, 246, 247, 420, 423, 424, 429, 434])
+@pytest.mark.parametrize("variant", [0, 231, 246, 247, 420, 423, 424, 429, 434, 440])
 def test_verify_reconstruct_ws_rs164(oracle, k, m, blen, erased, data_only, variant):
     """The RS(16+4) rebuild-1..4 defaults (231: without the small-batch latency path
     that variant 0 takes at 11 blocks) run the warp-specialised kernel (asserted through
@@ -249,14 +250,17 @@ def test_fused_kernel_selected():
 @pytest.mark.parametrize("k,m,blen,erased,heal", [(8, 4, 8 * 640, [], False), (8, 4, 8 * 640, [0, 5], False),
                                                   (8, 4, 8 * 640, [2, 10], True), (4, 2, 4 * 512, [1], True),
                                                   (16, 4, 16 * 256, [3, 17], False),
-                                                  (16, 4, 16 * 256, [3, 17], True)])
-@pytest.mark.parametrize("variant", [0, 200, 420, 423, 429])
+                                                  (16, 4, 16 * 256, [3, 17], True),
+                                                  (16, 4, 16 * 768, [0, 1, 16, 19], True),
+                                                  (16, 4, 16 * 512, [0, 5, 9, 14], False)])
+@pytest.mark.parametrize("variant", [0, 200, 420, 423, 429, 440])
 def test_verify_reconstruct_large_batch(oracle, k, m, blen, erased, heal, variant):
     """4096 stripes through the default launch (k_vr_ws where it applies), the
     first-generation kernel (200, any variant the product GET dispatch does not serve) and
     the product shapes with the round-4 LDS row stride (420) / the high table dwords from
-    LDS (423) / the other rebuild-role priority (429); every stripe checked
-    against the oracle, one corrupt survivor flagged."""
+    LDS (423) / the other rebuild-role priority (429) / the k_vr_ws instances instead of
+    the survivor-quad kernel the product runs for RS(16+4) rebuild and heal 4 (440);
+    every stripe checked against the oracle, one corrupt survivor flagged."""
     nb = 4096
     R = k + m
     S = -(-blen // k)

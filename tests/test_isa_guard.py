@@ -58,7 +58,7 @@ def test_untracked_loads_never_touched_in_flight(tmp_path, diag):
                 cur = None
                 continue
             cur[1].append((i, line))
-    kernels = [(n, b) for n, b in funcs if "k_ehx" in n or "k_vr_ws" in n or "k_ehx_dma" in n]
+    kernels = [(n, b) for n, b in funcs if "k_ehx" in n or "k_vr_ws" in n or "k_vr_quad" in n]
     assert kernels, "no k_ehx instance found in the assembly"
     bad = {n: cal.check(b, n) + cal.sgpr_hazards(b, n) for n, b in kernels}
     assert all(v == 0 for v in bad.values()), bad

@@ -1501,10 +1501,11 @@ static hipError_t run_vr(const VrArgs& a, hipStream_t s) {
 // variants that change a product shape's memory policy or layout (launch_vr_ws_t in
 // fused_v2.hpp: 246 plain loads, 247 64-bit addresses, 420 the round-4 LDS stride,
 // 423 high table dwords from LDS, 424 per-wave stamps, 429 the other rebuild-role
-// priority, 431 / 433 timing ablations, 434 the other split placement).
+// priority, 431 / 433 timing ablations, 434 the other split placement, 440 the k_vr_ws
+// instances for RS(16+4) rebuild / heal 4 instead of the survivor-quad kernel).
 static bool product_get_variant(int v) {
     return v == 0 || (ZS3_DIAG && (v == 246 || v == 247 || v == 420 || v == 423 || v == 424 || v == 429 ||
-                          v == 431 || v == 433 || v == 434));
+                          v == 431 || v == 433 || v == 434 || v == 440));
 }
 
 // GET / heal small-batch path: k_reconstruct rebuilds the missing rows, then one chain

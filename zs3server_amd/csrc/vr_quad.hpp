@@ -37,7 +37,11 @@ namespace shape {
 // pair-form hash waves, conflict-free LDS rows.  (4 stripes of 512-byte tiles, half the
 // steps per byte: 4-12 % slower, profiles/r05/ab_quad.jsonl.)
 struct Quad16 {
-    static constexpr int G = 8, T = 256, CW = 16, TSP = 1, XMAP = 0;
+    static constexpr int G = 8, T = 256, CW = 16, TSP = 1, XMAP = 0, PRIO = 1;
+};
+// Diagnostics: the rebuild quads without issue priority.
+struct Quad16Prio0 : Quad16 {
+    static constexpr int PRIO = 0;
 };
 }  // namespace shape
 
@@ -118,7 +122,9 @@ __attribute__((amdgpu_waves_per_eu(4))) k_vr_quad(VrArgs a) {
         return;
     }
 
-    // ---- rebuild role: quad q (wave-uniform), column o of stripe g
+    // ---- rebuild role: quad q (wave-uniform), column o of stripe g; issue priority over
+    // the hash waves as in k_vr_ws (GetShape PRIO)
+    if constexpr (C::PRIO > 0) __builtin_amdgcn_s_setprio(C::PRIO);
     const int e = tid - NH;
     const int q = __builtin_amdgcn_readfirstlane(e / NQT);
     const int eq = e % NQT;

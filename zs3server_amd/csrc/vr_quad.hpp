@@ -38,6 +38,11 @@ namespace shape {
 // steps per byte: 4-12 % slower, profiles/r05/ab_quad.jsonl.)
 struct Quad16 {
     static constexpr int G = 8, T = 256, CW = 16, TSP = 1, XMAP = 0, PRIO = 1;
+    static constexpr bool RR = true;  // partials read at the start of the step
+};
+// Diagnostics: the partials read at the end of the step, just before they are combined.
+struct Quad16LateRead : Quad16 {
+    static constexpr bool RR = false;
 };
 // Diagnostics: the rebuild quads without issue priority.
 struct Quad16Prio0 : Quad16 {
@@ -199,16 +204,22 @@ __attribute__((amdgpu_waves_per_eu(4))) k_vr_quad(VrArgs a) {
         }
     };
     // rebuilt row q of tile t: the XOR of the four quads' partials -> global (and LDS for
-    // the hash waves when healing)
-    auto reduce = [&](int64_t t) {
+    // the hash waves when healing).  The partials are read at the start of the step
+    // (reduce_read) and combined at its end (reduce_store), so the LDS latency hides
+    // behind the step's products instead of sitting in front of its barrier.
+    Col<NWd> part[NQ];
+    auto reduce_read = [&](int64_t t) {
         const uint8_t* const pr = PB + (t & 1) * NQ * EX * PBB + q * PBB + g * T + o;
-        Col<NWd> y = ld_col<NWd>(pr);
 #pragma unroll
-        for (int qq = 1; qq < NQ; ++qq) {
-            const Col<NWd> v = ld_col<NWd>(pr + qq * EX * PBB);
+        for (int qq = 0; qq < NQ; ++qq) part[qq] = ld_col<NWd>(pr + qq * EX * PBB);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto reduce_store = [&](int64_t t) {
+        Col<NWd> y = part[0];
 #pragma unroll
-            for (int w = 0; w < NWd; ++w) y.w[w] ^= v.w[w];
-        }
+        for (int qq = 1; qq < NQ; ++qq)
+#pragma unroll
+            for (int w = 0; w < NWd; ++w) y.w[w] ^= part[qq].w[w];
         const int so = (int)__builtin_amdgcn_readfirstlane(ooff + (uint32_t)(t * T));
         const VT v = {y.w[0], y.w[1], y.w[2], y.w[3]};
         __builtin_amdgcn_raw_buffer_store_b128(v, rs, (int)vo, so, 2);
@@ -222,20 +233,25 @@ __attribute__((amdgpu_waves_per_eu(4))) k_vr_quad(VrArgs a) {
     compute(0);
     load(1);
     lds_barrier2();
-    vm_wait<0>(x);  // step 1: no store issued yet
+    if constexpr (C::RR) reduce_read(0);  // step 1
+    vm_wait<0>(x);  // (no store issued yet)
     compute(1);
     load(nfull > 2 ? 2 : 1);
-    reduce(0);
+    if constexpr (!C::RR) reduce_read(0);
+    reduce_store(0);
     lds_barrier2();
     for (int64_t s = 2; s < nfull; ++s) {
+        if constexpr (C::RR) reduce_read(s - 1);
         vm_wait<1>(x);  // outstanding: this tile's loads, then step s-1's row store
         compute(s);
         load(s + 1 < nfull ? s + 1 : s);
-        reduce(s - 1);
+        if constexpr (!C::RR) reduce_read(s - 1);
+        reduce_store(s - 1);
         lds_barrier2();
     }
     vm_wait<0>(x);  // the last step's reload: its registers are reused from here on
-    reduce(nfull - 1);  // step nfull
+    reduce_read(nfull - 1);  // step nfull
+    reduce_store(nfull - 1);
     lds_barrier2();
     lds_barrier2();  // step nfull + 1: the hash waves' last rebuilt tile
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -114,7 +114,7 @@ WS16_HEAL_CASES = [(16, 4, 1 << 16, [0, 5]), (16, 4, 1 << 16, [3, 17]), (16, 4, 
 
 
 @pytest.mark.parametrize("k,m,blen,erased", WS16_HEAL_CASES)
-@pytest.mark.parametrize("variant", [0, 231, 246, 247, 420, 423, 424, 429, 434, 440, 442, 443])
+@pytest.mark.parametrize("variant", [0, 231, 246, 247, 420, 423, 424, 429, 434, 440, 442, 443, 444])
 def test_heal_ws_rs164(oracle, k, m, blen, erased, variant):
     """RS(16+4) heal (rebuild 1-4 shards and hash them) on k_vr_ws: the product shapes
     (231 = the product dispatch without the small-batch latency path that variant 0 takes
@@ -140,7 +140,7 @@ WS16_GET_CASES = [(16, 4, blen, erased, data_only)
 
 
 @pytest.mark.parametrize("k,m,blen,erased,data_only", WS16_GET_CASES)
-@pytest.mark.parametrize("variant", [0, 231, 246, 247, 420, 423, 424, 429, 434, 440, 442, 443])
+@pytest.mark.parametrize("variant", [0, 231, 246, 247, 420, 423, 424, 429, 434, 440, 442, 443, 444])
 def test_verify_reconstruct_ws_rs164(oracle, k, m, blen, erased, data_only, variant):
     """The RS(16+4) rebuild-1..4 defaults (231: without the small-batch latency path
     that variant 0 takes at 11 blocks) run the warp-specialised kernel (asserted through
@@ -253,7 +253,7 @@ def test_fused_kernel_selected():
                                                   (16, 4, 16 * 256, [3, 17], True),
                                                   (16, 4, 16 * 768, [0, 1, 16, 19], True),
                                                   (16, 4, 16 * 512, [0, 5, 9, 14], False)])
-@pytest.mark.parametrize("variant", [0, 200, 420, 423, 429, 440, 442, 443])
+@pytest.mark.parametrize("variant", [0, 200, 420, 423, 429, 440, 442, 443, 444])
 def test_verify_reconstruct_large_batch(oracle, k, m, blen, erased, heal, variant):
     """4096 stripes through the default launch (k_vr_ws where it applies), the
     first-generation kernel (200, any variant the product GET dispatch does not serve) and

@@ -39,6 +39,13 @@ namespace shape {
 struct Quad16 {
     static constexpr int G = 8, T = 256, CW = 16, TSP = 1, XMAP = 0, PRIO = 1;
     static constexpr bool RR = true;  // partials read at the start of the step
+    static constexpr bool UL = false;  // survivors and rebuilt rows in one LDS row array
+};
+// Diagnostics: survivors and rebuilt rows in one LDS row array (the heal hash waves' rows
+// at consecutive strides: SQ_LDS_BANK_CONFLICT 8.4 M -> 0 per launch, but heal 4 3-4 %
+// slower, profiles/r05/ab_quad4.jsonl).
+struct Quad16OneArray : Quad16 {
+    static constexpr bool UL = true;
 };
 // Diagnostics: the partials read at the end of the step, just before they are combined.
 struct Quad16LateRead : Quad16 {
@@ -62,13 +69,17 @@ __attribute__((amdgpu_waves_per_eu(4))) k_vr_quad(VrArgs a) {
     constexpr int NT = NH + NQ * NQT;
     constexpr int TS = ws_ts<T, false, C::TSP>();
     constexpr int NPK = T / 32;
-    constexpr int SVB = G * K * TS, RBB = G * EX * TS, PBB = G * T;  // one buffer of each
+    // UL: survivors and rebuilt rows of a stripe in one row array ([2][G*RH][TS]: the
+    // hash waves' rows at consecutive strides, conflict-free); else two arrays
+    constexpr bool UL = C::UL;
+    constexpr int SVB = UL ? G * RH * TS : G * K * TS, RBB = UL ? SVB : G * EX * TS, PBB = G * T;
+    constexpr int SVR = UL ? RH : K, RBR = UL ? RH : EX, RB0 = UL ? K : 0;  // rows per stripe, first rebuilt
     static_assert(NH % 64 == 0 && NQT % 64 == 0 && NWd == 4 && T % 32 == 0, "whole waves, 16-byte columns");
     typedef typename VecOf<NWd>::type VT;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_dyn[];
-    uint8_t* const SV = smem_dyn;                        // [2][G*K][TS]   survivors
-    uint8_t* const RB = SV + 2 * SVB;                    // [2][G*EX][TS]  rebuilt rows (heal)
-    uint8_t* const PB = RB + (HOUT ? 2 * RBB : 0);       // [2][NQ][EX][G*T] partials
+    uint8_t* const SV = smem_dyn;                            // [2][G*SVR][TS] survivors
+    uint8_t* const RB = UL ? SV : SV + 2 * SVB;              // [2][G*RBR][TS] rebuilt rows (heal)
+    uint8_t* const PB = SV + 2 * SVB + (HOUT && !UL ? 2 * RBB : 0);  // [2][NQ][EX][G*T] partials
     __shared__ int32_t srows[K + EX];
 
     const int tid = threadIdx.x;
@@ -86,7 +97,7 @@ __attribute__((amdgpu_waves_per_eu(4))) k_vr_quad(VrArgs a) {
         const int chain = pad ? chain0 - G * RH : chain0;
         const int g = chain / RH, cj = chain % RH;
         const bool reb = cj >= K;
-        const uint8_t* const base = reb ? RB + (g * EX + (cj - K)) * TS : SV + (g * K + cj) * TS;
+        const uint8_t* const base = reb ? RB + (g * RBR + RB0 + (cj - K)) * TS : SV + (g * SVR + cj) * TS;
         const int bufb = reb ? RBB : SVB;
         const int lag = reb ? 2 : 1;
         HHPair st = hh2_init(hh, a.key[0], a.key[1], a.key[2], a.key[3]);
@@ -171,7 +182,7 @@ __attribute__((amdgpu_waves_per_eu(4))) k_vr_quad(VrArgs a) {
     };
     // tile s: survivors to LDS (hash waves), the quad's partials of the four rebuilt rows
     auto compute = [&](int64_t s) {
-        uint8_t* const sv = SV + (s & 1) * SVB + (g * K + SQ * q) * TS + o;
+        uint8_t* const sv = SV + (s & 1) * SVB + (g * SVR + SQ * q) * TS + o;
         Col<NWd> xs[SQ];
 #pragma unroll
         for (int jj = 0; jj < SQ; ++jj) {
@@ -223,7 +234,7 @@ __attribute__((amdgpu_waves_per_eu(4))) k_vr_quad(VrArgs a) {
         const int so = (int)__builtin_amdgcn_readfirstlane(ooff + (uint32_t)(t * T));
         const VT v = {y.w[0], y.w[1], y.w[2], y.w[3]};
         __builtin_amdgcn_raw_buffer_store_b128(v, rs, (int)vo, so, 2);
-        if constexpr (HOUT) st_col<NWd>(RB + (t & 1) * RBB + (g * EX + q) * TS + o, y);
+        if constexpr (HOUT) st_col<NWd>(RB + (t & 1) * RBB + (g * RBR + RB0 + q) * TS + o, y);
     };
     // The next tile's loads are issued unconditionally (the last step reloads its own tile)
     // and before the step's row store, so every wait below retires exactly the loads: the
@@ -265,7 +276,7 @@ static bool launch_vr_quad_t(const VrArgs& a, hipStream_t s) {
     constexpr int RH = 16 + (HOUT ? 4 : 0);
     constexpr int NT = vr_nh<G, RH, false>() + 4 * G * (T / CW);
     constexpr int TS = ws_ts<T, false, C::TSP>();
-    constexpr size_t dyn = (size_t)2 * G * 16 * TS + (HOUT ? (size_t)2 * G * 4 * TS : 0) + (size_t)2 * 4 * 4 * G * T;
+    constexpr size_t dyn = (size_t)2 * G * RH * TS + (size_t)2 * 4 * 4 * G * T;  // either layout
     static_assert(dyn + 4 * 20 <= 163840 && NT <= 1024, "one workgroup's LDS and threads");
     if (a.k != 16 || a.e != 4 || a.ids || HOUT != (a.sums_out != nullptr)) return false;
     if (a.S % T != 0 || a.S / T < 2 || a.block_stride <= 0) return false;

@@ -21,8 +21,9 @@
 //                   priority, as before round 5's adoption)
 //  (Measured this round and removed: PM 2 / PM 0 on Rs84Bulk, PM 2 on the RS(16+4) bulk
 //  shape, PM 1 / temporal loads or stores / L2 prefetch 1 or 3 tiles ahead / XMAP 16 on the
-//  RS(12+4) UA shape, the LDS-counter hand-off and the L2 prefetch on Rs84Bulk:
-//  profiles/r05/ab_prio_enc*.jsonl, ab_ntm124.jsonl, ab_enc3.jsonl)
+//  RS(12+4) UA shape, the pair-form 8 x 512 UA shape on 1 MiB RS(12+4) with or without
+//  XMAP, the LDS-counter hand-off and the L2 prefetch on Rs84Bulk: profiles/r05/
+//  ab_prio_enc*.jsonl, ab_ntm124.jsonl, ab_enc3.jsonl, ab_rs124pair.jsonl)
 #include "fused_v2.hpp"
 
 namespace zs3k {

@@ -24,9 +24,10 @@
 //   hash waves:    survivor chains hash tile s-1 from SV, rebuilt chains tile s-2 from RB
 // Requires S % T == 0, S / T >= 2, no block-id list, buffer-addressable stripe groups
 // (launch_vr_quad); other batches take k_vr_ws.  Measured against the k_vr_ws instances
-// (K16Rebuild34 / K16Heal with SPL, profiles/r05/ab_quad.jsonl): RS(16+4) 2 048 x 1 MiB
-// rebuild 4 0.591-0.597 -> 0.561-0.565 ms, heal 4 0.663-0.669 -> 0.633-0.638; 8 192 x 1 MiB
-// 2.34-2.37 -> 2.27 / 2.62-2.63 -> 2.52 ms.
+// (K16Rebuild34 / K16Heal with SPL; diagnostics 440), with the rebuild quads at issue
+// priority 1 and the partials read at the start of each step (profiles/r05/
+// ab_quad3.jsonl): RS(16+4) 2 048 x 1 MiB rebuild 4 0.595 -> 0.551 ms, heal 4 0.668 ->
+// 0.616; 8 192 x 1 MiB 2.34 -> 2.27 / 2.61 -> 2.47 ms.
 #pragma once
 #include "fused_v2.hpp"
 

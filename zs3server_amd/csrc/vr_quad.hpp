@@ -36,7 +36,8 @@ namespace zs3k {
 namespace shape {
 // 8 stripes of 256-byte tiles, 16-byte columns: 4 quads x 2 waves of rebuild, 4-5
 // pair-form hash waves, conflict-free LDS rows.  (4 stripes of 512-byte tiles, half the
-// steps per byte: 4-12 % slower, profiles/r05/ab_quad.jsonl.)
+// steps per byte: 4-12 % slower, profiles/r05/ab_quad.jsonl; 4 stripes of 256-byte tiles,
+// two workgroups per CU: 5-19 % slower, ab_quad5.jsonl.)
 struct Quad16 {
     static constexpr int G = 8, T = 256, CW = 16, TSP = 1, XMAP = 0, PRIO = 1;
     static constexpr bool RR = true;  // partials read at the start of the step

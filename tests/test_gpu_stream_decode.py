@@ -133,3 +133,47 @@ def test_stream_decode_too_few_shards_reports_the_block(oracle):
     for b in range(nfull):
         if b != 7:
             assert np.array_equal(rows(work, b, E, S, R)[:k], rows(ref, b, E, S, R)[:k]), b
+
+
+@pytest.mark.parametrize("heal", [False, True], ids=["get", "heal"])
+def test_stream_decode_rs164_four_lost(oracle, heal):
+    """RS(16+4) with four shards lost on every block (the survivor-quad kernel's case,
+    vr_quad.hpp) through the streamed path: pattern groups launch on shifted batches,
+    a rotted survivor chunk is flagged at its (block, shard), a short last block takes
+    the k_vr_ws instances (its shard size is not a multiple of 256)."""
+    k, m, nfull, tail = 16, 4, 40, 70001
+    R = k + m
+    ref, sums, S, St = make_object(oracle, k, m, nfull, tail, seed=1604)
+    E = R * S
+    nb = nfull + 1
+    present = np.ones((nb, R), bool)
+    present[:, [0, 7, 16, 19]] = False
+    present[10:20, 7] = True                     # a reader back for ten blocks (3 lost there)
+    present[10:20, 9] = False                    # ... while another drops out (4 lost again)
+    rot_b, rot_row = 23, 11
+    work = ref.copy()
+    for b in range(nb):
+        Sb = S if b < nfull else St
+        r = rows(work, b, E, Sb, R)
+        r[~present[b]] = 0x5A
+    rows(work, rot_b, E, S, R)[rot_row, 4097] ^= 0x02
+    bad = np.full((nb, R), 9, np.int32)
+    status = np.full(nb, 77, np.int32)
+    out = np.zeros((nb, R, 32), np.uint8) if heal else None
+    n = z.Codec(k, m, MiB).stream_decode(work, nfull * MiB + tail, present, not heal, expect=sums, bad=bad,
+                                         sums_out=out, status=status, batch_blocks=16)
+    assert n == nb and (status == 0).all()
+    want_bad = np.zeros((nb, R), np.int32)
+    want_bad[rot_b, rot_row] = 1
+    assert np.array_equal(bad, want_bad), np.argwhere(bad != want_bad)[:5]
+    for b in range(nb):
+        if b == rot_b:
+            continue
+        Sb = S if b < nfull else St
+        got, exp = rows(work, b, E, Sb, R), rows(ref, b, E, Sb, R)
+        for j in range(R):
+            if present[b, j] or j < k or heal:
+                assert np.array_equal(got[j], exp[j]), (b, j)
+        if heal:
+            for j in np.nonzero(~present[b])[0]:
+                assert np.array_equal(out[b, j], sums[b, j]), (b, j)

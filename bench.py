@@ -134,6 +134,29 @@ def committed_traffic(k: int, m: int, nobj: int, blen: int):
     return best if best else (None, None)
 
 
+def roofline_block(k: int, m: int, blen: int, nobj: int, total_objects: int, world: int, kern_ms: float,
+                   traffic, traffic_src) -> dict:
+    """The line's `roofline` object.  Every rank launches the same kernel on its own share
+    (nobj objects), so the roofline is a per-GPU quantity: `achieved` / `frac` (alias
+    `frac_per_gpu`) = one GPU's algorithmic bytes per launch / the slowest rank's average
+    kernel time, against one GPU's HBM peak; `traffic` is per launch on one GPU.  The
+    whole-job view sits beside it: `aggregate_achieved` = the bytes of all ranks' launches /
+    the slowest rank's kernel time, against `aggregate_peak` = N x one GPU's peak."""
+    abytes = nobj * algo_bytes_per_block(k, m, blen)
+    achieved = abytes / (kern_ms * 1e-3) / 1e9
+    agg_bytes = total_objects * algo_bytes_per_block(k, m, blen)
+    agg = agg_bytes / (kern_ms * 1e-3) / 1e9
+    return {"bound": "hbm", "scope": "per_gpu", "n_gpus": world,
+            "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "frac_per_gpu": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic, "traffic_scope": "per_gpu_per_launch", "traffic_source": traffic_src,
+            "kernel": headline_kernel(k, m, blen, nobj),
+            "kernel_ms": round(kern_ms, 4), "kernel_ms_scope": "max_over_ranks",
+            "algo_bytes_per_launch": abytes,
+            "aggregate_achieved": round(agg, 1), "aggregate_peak": HBM_PEAK_GBS * world,
+            "aggregate_frac": round(agg / (HBM_PEAK_GBS * world), 4), "aggregate_algo_bytes": agg_bytes}
+
+
 def _free_port() -> int:
     with socket.socket() as sk:
         sk.bind(("127.0.0.1", 0))
@@ -262,8 +285,6 @@ def main() -> None:
 
     total_bytes = total_objects * blen * args.steps
     value = total_bytes / elapsed / 2 ** 30
-    abytes = nobj * algo_bytes_per_block(k, m, blen)
-    achieved = abytes / (kern_ms * 1e-3) / 1e9
     if rank == 0:
         wl = (f"RS({k}+{m}) Split+Encode+HighwayHash256S bitrot sums, in-place bpool layout, "
               + (f"{total_objects} x {blen} B objects ({total_objects * blen / 2**30:.0f} GiB stream, BASELINE "
@@ -288,13 +309,7 @@ def main() -> None:
                                       + (" (TEST: all ranks on device 0)" if same_dev else ""),
                        "kernel_path": {0: "generic", 1: "first-generation", 2: "warp-specialised",
                                        3: "mixed-wave", 4: "small-batch latency"}.get(path, str(path))},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic,
-                         "traffic_source": traffic_src,
-                         "kernel": headline_kernel(k, m, blen, nobj),
-                         "kernel_ms": round(kern_ms, 4),
-                         "algo_bytes_per_launch": abytes},
+            "roofline": roofline_block(k, m, blen, nobj, total_objects, world, kern_ms, traffic, traffic_src),
         }
         if world == 1 and not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(k, m, blen, args.cpu_seconds)
@@ -320,7 +335,10 @@ def dry_run(args, world: int, rank: int) -> None:
         print(json.dumps({"metric": "dry run (launcher test, no GPU work)", "value": None, "unit": "GiB/s",
                           "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                           "ms_per_step": round(elapsed * 1e3, 3), "dry_run": True,
-                          "ranks_seen": world, "pid": os.getpid()}), flush=True)
+                          "ranks_seen": world, "pid": os.getpid(),
+                          "roofline": roofline_block(args.k, args.m, args.block, args.total_objects // world,
+                                                     args.total_objects, world, elapsed * 1e3, None, None)}),
+              flush=True)
     if world > 1:
         dist.destroy_process_group()
 

@@ -409,6 +409,22 @@ int zs3_selftest(void);
 #define ZS3_PATH_LATENCY    4
 int zs3_last_path(void);
 
+/* Every kernel family this thread's launches used since the previous call with reset != 0
+ * (or since the thread started): bit (1u << ZS3_PATH_*) per family, plus
+ * ZS3_KERNEL_VR_QUAD when the survivor-quad GET / heal kernel (k_vr_quad: RS(16+4) with four
+ * rebuilt rows) served a batch.  Unlike zs3_last_path it survives the later launches of
+ * one call (zs3_stream_decode's short last block), so a caller can check what every batch
+ * of a streamed GET or heal ran on.  reset != 0 clears the set after reading it. */
+#define ZS3_KERNEL_VR_QUAD (1u << 16)
+uint32_t zs3_path_mask(int reset);
+
+/* The stream drivers (zs3_stream_encode*, zs3_stream_decode) keep their pinned host and
+ * device staging buffers for the next call (hipHostMalloc of a batch's slots costs more
+ * than a large stream's own transfers).  At most `max_idle_bytes` stay idle per process
+ * (default 6 GiB); this sets that cap, frees idle buffers past it at once (oldest first)
+ * and returns the bytes freed.  zs3_pool_limit(0) releases every idle buffer. */
+int64_t zs3_pool_limit(uint64_t max_idle_bytes);
+
 #ifdef __cplusplus
 }
 #endif

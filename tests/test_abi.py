@@ -212,3 +212,16 @@ def test_parts_digests_reject_missing_arrays(fn):
     assert getattr(L, fn)(fake, None, fake, 3, fake, None) == -8
     assert getattr(L, fn)(fake, fake, None, 3, fake, None) == -8
     assert getattr(L, fn)(fake, fake, fake, -1, fake, None) == -8
+
+
+def test_path_mask_and_pool_limit_are_host_only():
+    """zs3_path_mask on a thread that launched nothing is empty; zs3_pool_limit with no
+    idle staging frees nothing (neither call touches a GPU)."""
+    import threading
+    got = []
+    t = threading.Thread(target=lambda: got.append(z.path_mask(reset=True)))
+    t.start()
+    t.join()
+    assert got == [0]
+    assert z.pool_limit(1 << 30) == 0
+    assert z.pool_limit(6 << 30) == 0

@@ -40,6 +40,30 @@ def test_self_launch_spawns_n_ranks(n):
     assert out["pid"] != os.getpid()
     # the reduction is a max over ranks: the slowest rank sleeps n * 10 ms
     assert out["ms_per_step"] >= 10 * n
+    # the roofline says which scope each field has: per-GPU fraction
+    # beside the whole-job rate of all ranks' bytes over the slowest rank's kernel time
+    rl = out["roofline"]
+    assert rl["scope"] == "per_gpu" and rl["n_gpus"] == n
+    assert rl["frac_per_gpu"] == rl["frac"]
+    assert rl["traffic_scope"] == "per_gpu_per_launch" and rl["kernel_ms_scope"] == "max_over_ranks"
+    assert rl["aggregate_peak"] == n * rl["peak"]
+    assert rl["aggregate_algo_bytes"] == 65536 * (1 << 20) * 3 // 2 + 65536 * 12 * 32
+    # 65 536 objects over n ranks: the aggregate is the ranks' shares over the same time
+    assert rl["aggregate_achieved"] == pytest.approx(rl["achieved"] * 65536 / (65536 // n), rel=1e-3)
+
+
+def test_roofline_block_scopes():
+    """One GPU's share and the whole job: frac_per_gpu stays the per-GPU fraction while
+    aggregate_achieved sums the ranks' bytes (the --gpus 2 same-device rehearsal line of
+    round 5 printed frac 0.343 beside 3 399 GiB/s with nothing saying which was which)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    a = bench.algo_bytes_per_block(8, 4, 1 << 20)
+    for n in (1, 2, 4, 8):
+        rl = bench.roofline_block(8, 4, 1 << 20, 65536 // n, 65536, n, 18.0 / n, None, None)
+        assert rl["frac_per_gpu"] == pytest.approx((65536 // n) * a / 18e-3 * n / 8e12, rel=1e-3)
+        assert rl["aggregate_achieved"] == pytest.approx(65536 * a / (18.0 / n) * 1e-6, rel=1e-4)
+        assert rl["aggregate_frac"] == pytest.approx(rl["frac_per_gpu"], rel=1e-3)
 
 
 def test_too_few_devices_fails_loudly():

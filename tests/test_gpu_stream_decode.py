@@ -136,44 +136,141 @@ def test_stream_decode_too_few_shards_reports_the_block(oracle):
 
 
 @pytest.mark.parametrize("heal", [False, True], ids=["get", "heal"])
-def test_stream_decode_rs164_four_lost(oracle, heal):
-    """RS(16+4) with four shards lost on every block (the survivor-quad kernel's case,
-    vr_quad.hpp) through the streamed path: pattern groups launch on shifted batches,
-    a rotted survivor chunk is flagged at its (block, shard), a short last block takes
-    the k_vr_ws instances (its shard size is not a multiple of 256)."""
+@pytest.mark.parametrize("pinned", [False, True], ids=["pageable", "pinned"])
+def test_stream_decode_rs164_four_lost(oracle, heal, pinned):
+    """RS(16+4) with four shards to rebuild on most blocks — the survivor-quad kernel's
+    case (vr_quad.hpp) — through the streamed path.  GET loses four DATA rows (GET rebuilds
+    data rows only, so four lost data rows is what reaches k_vr_quad); heal loses two data
+    and two parity rows.  A reader swap in blocks 10-19 changes the pattern (pattern groups
+    launch on shifted batches); GET blocks 25-29 lose a parity row instead of a data row
+    (three rebuilt rows: the k_vr_ws instances), and that lost parity row must stay
+    untouched.  A rotted survivor chunk is flagged at its (block, shard); the short last
+    block takes the k_vr_ws instances (its shard size is not a multiple of 256).  RS(16+4)
+    rows of 1 MiB blocks are 256-byte aligned, so pinned stripes take the per-row DMA path
+    (only rows some block of the batch has go up), pageable ones the staging."""
     k, m, nfull, tail = 16, 4, 40, 70001
     R = k + m
     ref, sums, S, St = make_object(oracle, k, m, nfull, tail, seed=1604)
     E = R * S
     nb = nfull + 1
     present = np.ones((nb, R), bool)
-    present[:, [0, 7, 16, 19]] = False
-    present[10:20, 7] = True                     # a reader back for ten blocks (3 lost there)
-    present[10:20, 9] = False                    # ... while another drops out (4 lost again)
+    if heal:
+        present[:, [0, 7, 16, 19]] = False
+        present[10:20, 7] = True                 # a reader back for ten blocks ...
+        present[10:20, 9] = False                # ... while another drops out (4 lost again)
+    else:
+        present[:, [0, 7, 9, 12]] = False
+        present[10:20, 7] = True
+        present[10:20, 3] = False
+        present[25:30, 12] = True                # three data rows lost, and parity row 17
+        present[25:30, 17] = False
     rot_b, rot_row = 23, 11
-    work = ref.copy()
-    for b in range(nb):
-        Sb = S if b < nfull else St
-        r = rows(work, b, E, Sb, R)
-        r[~present[b]] = 0x5A
-    rows(work, rot_b, E, S, R)[rot_row, 4097] ^= 0x02
-    bad = np.full((nb, R), 9, np.int32)
-    status = np.full(nb, 77, np.int32)
-    out = np.zeros((nb, R, 32), np.uint8) if heal else None
-    n = z.Codec(k, m, MiB).stream_decode(work, nfull * MiB + tail, present, not heal, expect=sums, bad=bad,
-                                         sums_out=out, status=status, batch_blocks=16)
-    assert n == nb and (status == 0).all()
-    want_bad = np.zeros((nb, R), np.int32)
-    want_bad[rot_b, rot_row] = 1
-    assert np.array_equal(bad, want_bad), np.argwhere(bad != want_bad)[:5]
-    for b in range(nb):
-        if b == rot_b:
-            continue
-        Sb = S if b < nfull else St
-        got, exp = rows(work, b, E, Sb, R), rows(ref, b, E, Sb, R)
-        for j in range(R):
-            if present[b, j] or j < k or heal:
-                assert np.array_equal(got[j], exp[j]), (b, j)
+    work_h = z.HostBuffer(nb * E) if pinned else None
+    work = work_h.array if pinned else np.empty(nb * E, np.uint8)
+    try:
+        work[:] = ref
+        for b in range(nb):
+            Sb = S if b < nfull else St
+            r = rows(work, b, E, Sb, R)
+            r[~present[b]] = 0x5A
+        rows(work, rot_b, E, S, R)[rot_row, 4097] ^= 0x02
+        bad = np.full((nb, R), 9, np.int32)
+        status = np.full(nb, 77, np.int32)
+        out = np.zeros((nb, R, 32), np.uint8) if heal else None
+        z.path_mask(reset=True)
+        n = z.Codec(k, m, MiB).stream_decode(work_h if pinned else work, nfull * MiB + tail, present, not heal,
+                                             expect=sums, bad=bad, sums_out=out, status=status, batch_blocks=16)
+        assert n == nb and (status == 0).all()
+        assert z.path_mask() & z.KERNEL_VR_QUAD, "four rebuilt rows ran on the survivor-quad kernel"
+        want_bad = np.zeros((nb, R), np.int32)
+        want_bad[rot_b, rot_row] = 1
+        assert np.array_equal(bad, want_bad), np.argwhere(bad != want_bad)[:5]
+        for b in range(nb):
+            if b == rot_b:
+                continue
+            Sb = S if b < nfull else St
+            got, exp = rows(work, b, E, Sb, R), rows(ref, b, E, Sb, R)
+            for j in range(R):
+                if present[b, j] or j < k or heal:
+                    assert np.array_equal(got[j], exp[j]), (b, j)
+                else:
+                    assert (got[j] == 0x5A).all(), ("DecodeDataBlocks leaves missing parity alone", b, j)
+            if heal:
+                for j in np.nonzero(~present[b])[0]:
+                    assert np.array_equal(out[b, j], sums[b, j]), (b, j)
+    finally:
+        if work_h is not None:
+            work_h.free()
+
+
+@pytest.mark.parametrize("heal", [False, True], ids=["get", "heal"])
+def test_stream_decode_rs84_pinned_rows_and_failed_block(oracle, heal):
+    """RS(8+4) 1 MiB blocks from pinned stripes: S = 131 072 is 256-byte aligned, so rows
+    move by per-row DMA across each batch, and only rows that some block of the batch has
+    are uploaded.  Rows are present in some blocks and missing in others within one batch;
+    one block has too few shards: it reports ErrTooFewShards, the others are served, and
+    nothing comes back into the failed block's stripe (its rows that were never uploaded
+    would otherwise carry whatever the pooled device slot last held)."""
+    k, m, nfull = 8, 4, 48
+    R = k + m
+    ref, sums, S, _ = make_object(oracle, k, m, nfull, 0, seed=8484)
+    E = R * S
+    present = np.ones((nfull, R), bool)
+    present[0:12, 2] = False                     # row 2 lost in the first 12 blocks only
+    present[5:30, 9] = False                     # parity row 9 lost in blocks 5-29
+    present[20:48:3, 6] = False                  # row 6 lost in every third block
+    present[33, [0, 1, 3, 4, 5]] = False         # block 33: five lost, too few shards
+    work_h = z.HostBuffer(nfull * E)
+    try:
+        work = work_h.array
+        work[:] = ref
+        for b in range(nfull):
+            rows(work, b, E, S, R)[~present[b]] = 0x5A
+        before33 = rows(work, 33, E, S, R).copy()
+        bad = np.full((nfull, R), 9, np.int32)
+        status = np.full(nfull, 77, np.int32)
+        out = np.zeros((nfull, R, 32), np.uint8) if heal else None
+        rc = z.Codec(k, m, MiB).stream_decode(work_h, nfull * MiB, present, not heal, expect=sums, bad=bad,
+                                              sums_out=out, status=status, batch_blocks=16)
+        assert rc == -3, rc
+        assert status[33] == -3 and (np.delete(status, 33) == 0).all(), status
+        assert not bad.any()
+        assert np.array_equal(rows(work, 33, E, S, R), before33), "a failed block's stripe is left as it was"
+        for b in range(nfull):
+            if b == 33:
+                continue
+            got, exp = rows(work, b, E, S, R), rows(ref, b, E, S, R)
+            for j in range(R):
+                if present[b, j] or j < k or heal:
+                    assert np.array_equal(got[j], exp[j]), (b, j)
+                else:
+                    assert (got[j] == 0x5A).all(), (b, j)
+            if heal:
+                for j in np.nonzero(~present[b])[0]:
+                    assert np.array_equal(out[b, j], sums[b, j]), (b, j)
         if heal:
-            for j in np.nonzero(~present[b])[0]:
-                assert np.array_equal(out[b, j], sums[b, j]), (b, j)
+            assert not out[33].any(), "no sums for a block that was not healed"
+    finally:
+        work_h.free()
+
+
+def test_stream_decode_argument_checks():
+    """The Python binding checks every buffer's size, dtype and layout before the library
+    touches it through raw pointers: nothing reaches the device."""
+    k, m = 8, 4
+    c = z.Codec(k, m, MiB)
+    R, S = k + m, MiB // k
+    st = np.zeros(2 * R * S, np.uint8)
+    pres = np.ones((2, R), bool)
+    with pytest.raises(ValueError):
+        c.stream_decode(st[:-1], 2 * MiB, pres, True)             # stripes too short
+    with pytest.raises(ValueError):
+        c.stream_decode(st, 2 * MiB, pres[:1], True)              # present for one block
+    with pytest.raises(ValueError):
+        c.stream_decode(st, 2 * MiB, pres, True, bad=np.zeros((2, R), np.int64))
+    with pytest.raises(ValueError):
+        c.stream_decode(st, 2 * MiB, pres, True, expect=np.zeros((2, R, 31), np.uint8))
+    with pytest.raises(ValueError):
+        c.stream_decode(st, 2 * MiB, pres, True, status=np.zeros(4, np.int32)[::2])
+    with pytest.raises(ValueError):
+        c.stream_decode(st.reshape(2, -1)[:, ::2], 2 * MiB, pres, True)

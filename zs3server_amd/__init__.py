@@ -55,7 +55,8 @@ EXPORTS = [
     "zs3_queue_new", "zs3_queue_free", "zs3_queue_submit_encode", "zs3_queue_submit_decode", "zs3_req_wait",
     "zs3_queue_flush", "zs3_queue_stats", "zs3_queue_zero_copy_blocks", "zs3_queue_encode_data", "zs3_queue_decode_data_blocks",
     "zs3_stream_encode_multi", "zs3_split_range", "zs3_md5_parts", "zs3_sha256_parts",
-    "zs3_queue_device_stats", "zs3_stream_decode",
+    "zs3_queue_device_stats", "zs3_stream_decode", "zs3_path_mask",
+    "zs3_pool_limit",
 ]
 # include/zs3gpu_diag.h: exported by the diagnostics build only
 DIAG_EXPORTS = ["zs3_debug_set_variant", "zs3_debug_set_buffer", "zs3_debug_encode_layout_ok"]
@@ -178,6 +179,10 @@ def _load(path):
     L.zs3_stream_encode_multi.argtypes = [vp, vp, C.c_int, vp, i64, vp, vp, i64]
     L.zs3_stream_encode_multi.restype = i64
     L.zs3_stream_decode.argtypes = [vp, vp, i64, vp, C.c_int, vp, vp, vp, vp, i64]
+    L.zs3_path_mask.argtypes = [C.c_int]
+    L.zs3_path_mask.restype = C.c_uint32
+    L.zs3_pool_limit.argtypes = [C.c_uint64]
+    L.zs3_pool_limit.restype = i64
     L.zs3_stream_decode.restype = i64
     L.zs3_split_range.argtypes = [i64, C.c_int, C.c_int, C.POINTER(i64), C.POINTER(i64)]
     L.zs3_split_range.restype = None
@@ -345,14 +350,44 @@ class Codec:
         arrays.  Returns the number of blocks or the first block's status (< 0)."""
         import numpy as np
 
-        def addr(x):
+        # the library reads and writes these buffers through raw pointers: check every size,
+        # dtype and layout here (a short or strided array would be overrun in host memory)
+        if total_len < 0 or batch_blocks <= 0:
+            raise ValueError("stream_decode: total_len >= 0 and batch_blocks > 0")
+        R = self.k + self.m
+        B = self.block_size
+        S = -(-B // self.k)
+        nblocks = -(-total_len // B)
+        need = nblocks * R * S
+
+        def check(x, name, dtype, shape):
             if x is None:
                 return None
-            return x.ptr if isinstance(x, HostBuffer) else x.ctypes.data
+            if not isinstance(x, np.ndarray) or x.dtype != np.dtype(dtype) or not x.flags.c_contiguous:
+                raise ValueError(f"stream_decode: {name} must be a C-contiguous numpy {np.dtype(dtype)} array")
+            if x.size != int(np.prod(shape)):
+                raise ValueError(f"stream_decode: {name} has {x.size} elements, the object needs {shape}")
+            return x.ctypes.data
+
+        if isinstance(stripes, HostBuffer):
+            if not stripes.ptr or stripes.nbytes < need:
+                raise ValueError(f"stream_decode: stripes hold {stripes.nbytes} bytes, {nblocks} blocks need {need}")
+            sp = stripes.ptr
+        else:
+            if (not isinstance(stripes, np.ndarray) or stripes.dtype != np.uint8 or not stripes.flags.c_contiguous
+                    or stripes.nbytes < need):
+                raise ValueError(f"stream_decode: stripes must be a C-contiguous uint8 array of >= {need} bytes")
+            sp = stripes.ctypes.data
         pres = np.ascontiguousarray(np.asarray(present, dtype=bool).astype(np.uint8))
-        return int(self._L.zs3_stream_decode(self._h, addr(stripes), total_len, pres.ctypes.data,
-                                             1 if data_only else 0, addr(expect), addr(bad), addr(sums_out),
-                                             addr(status), batch_blocks))
+        if pres.size != nblocks * R:
+            raise ValueError(f"stream_decode: present has {pres.size} entries, {nblocks} blocks of {R} shards need "
+                             f"{nblocks * R}")
+        e_p = check(expect, "expect", np.uint8, (nblocks, R, 32))
+        b_p = check(bad, "bad", np.int32, (nblocks, R))
+        o_p = check(sums_out, "sums_out", np.uint8, (nblocks, R, 32))
+        s_p = check(status, "status", np.int32, (nblocks,))
+        return int(self._L.zs3_stream_decode(self._h, sp, total_len, pres.ctypes.data, 1 if data_only else 0,
+                                             e_p, b_p, o_p, s_p, batch_blocks))
 
     def decode_data_blocks(self, shards, present, data_only: bool) -> None:
         """Reconstruct in place on a (k+m, S) C-contiguous numpy uint8 array."""
@@ -577,6 +612,21 @@ def selftest() -> None:
 
 def last_path() -> int:
     return lib().zs3_last_path()
+
+
+KERNEL_VR_QUAD = 1 << 16  # include/zs3gpu.h ZS3_KERNEL_VR_QUAD
+
+
+def path_mask(reset: bool = False) -> int:
+    """Every kernel family this thread's launches used since the last reset (zs3_path_mask):
+    bit 1 << ZS3_PATH_* per family, plus KERNEL_VR_QUAD for the survivor-quad GET / heal
+    kernel."""
+    return int(lib().zs3_path_mask(1 if reset else 0))
+
+
+def pool_limit(max_idle_bytes: int) -> int:
+    """zs3_pool_limit: cap (and trim to) the stream drivers' idle staging; bytes freed."""
+    return int(lib().zs3_pool_limit(max_idle_bytes))
 
 
 def set_debug_buffer(t) -> None:

@@ -392,6 +392,21 @@ __attribute__((amdgpu_waves_per_eu(C::WPE))) k_ehx_ws(EncArgs a) {
     }
     if constexpr (PM == 3) {
         if (__builtin_amdgcn_readfirstlane(tid) < NH) __builtin_amdgcn_s_setprio(1);
+    } else if constexpr (PM >= 5 && PM <= 8) {
+        // round 6 (per-wave stamps, profiles/r06/stamps_enc.jsonl): a 12-wave workgroup's
+        // waves share SIMDs as {w, w+4, w+8}, so the pair-form hash waves 2 and 3 are the
+        // ones beside two encode waves ("1H+2E") and pace the step.  5: encode waves 1,
+        // those two hash waves 2; 6: encode waves 1, every hash wave 2; 7: encode waves and
+        // hash waves 2-3 at 1; 8: only hash waves 2-3 at 1.
+        const int wv = (int)__builtin_amdgcn_readfirstlane(tid) >> 6;
+        const bool enc = wv >= NH / 64, hb = !enc && (wv & 3) >= 2 && wv < 4;
+        int pr = 0;
+        if (PM == 5) pr = enc ? 1 : hb ? 2 : 0;
+        if (PM == 6) pr = enc ? 1 : 2;
+        if (PM == 7) pr = enc || hb ? 1 : 0;
+        if (PM == 8) pr = hb ? 1 : 0;
+        if (pr == 1) __builtin_amdgcn_s_setprio(1);
+        if (pr == 2) __builtin_amdgcn_s_setprio(2);
     } else if constexpr (PM == 1 || PM == 2) {
         if (__builtin_amdgcn_readfirstlane(tid) >= NH) {
             if (PM == 2 && __builtin_amdgcn_readfirstlane(tid) >= NH + 256)

@@ -25,6 +25,7 @@
 //  XMAP, the LDS-counter hand-off and the L2 prefetch on Rs84Bulk: profiles/r05/
 //  ab_prio_enc*.jsonl, ab_ntm124.jsonl, ab_enc3.jsonl, ab_rs124pair.jsonl)
 #include "fused_v2.hpp"
+#include "ehx_mx.hpp"
 
 namespace zs3k {
 
@@ -40,6 +41,16 @@ struct Rs84MemOnly : Rs84Bulk {
     static constexpr int EP = 9, ABL = 1;
 };
 struct Rs84Stamped : Rs84Bulk {
+    static constexpr bool WT = true;
+};
+struct Rs84Pf2 : Rs84Bulk {
+    static constexpr int PF = 2;
+};
+struct Rs84Ep1 : Rs84Bulk {
+    static constexpr int EP = 1;
+};
+template <class S>
+struct Stamp : S {
     static constexpr bool WT = true;
 };
 }  // namespace shape
@@ -58,6 +69,34 @@ bool launch_ehx_diag(int v, const EncArgs& a, hipStream_t s) {
             case 412: return launch_ws<8, 4, XMap<Rs84Bulk, 8>>(a, s);
             case 413: return launch_ws<8, 4, XMap<Rs84Bulk, 16>>(a, s);
             case 414: return launch_ws<8, 4, XMap<Rs84Bulk, 32>>(a, s);
+            // round 6: the balanced mixed-role kernel (ehx_mx.hpp), G = 16 / 8 / 32, stamped,
+            // hash reads before the encode
+            case 450: return launch_mx<8, 4, Mix<16>>(a, s);
+            case 451: return launch_mx<8, 4, Mix<8>>(a, s);
+            case 452: return launch_mx<8, 4, Mix<32>>(a, s);
+            case 453: return launch_mx<8, 4, MixWT<Mix<16>>>(a, s);
+            case 454: return launch_mx<8, 4, MixWT<Mix<8>>>(a, s);
+            case 455: return launch_mx<8, 4, MixWT<Mix<32>>>(a, s);
+            case 456: return launch_mx<8, 4, MixRd1<Mix<16>>>(a, s);
+            case 457: return launch_mx<8, 4, MixRd1<Mix<32>>>(a, s);
+            // round 6: issue priority by SIMD mix (fused_v2.hpp PM 5-8) and PM 3 retested
+            // under the XCD-region order
+            case 460: return launch_ws<8, 4, Pm<Rs84Bulk, 3>>(a, s);
+            case 461: return launch_ws<8, 4, Pm<Rs84Bulk, 5>>(a, s);
+            case 462: return launch_ws<8, 4, Pm<Rs84Bulk, 6>>(a, s);
+            case 463: return launch_ws<8, 4, Pm<Rs84Bulk, 7>>(a, s);
+            case 464: return launch_ws<8, 4, Pm<Rs84Bulk, 8>>(a, s);
+            case 465: return launch_ws<8, 4, Stamp<Pm<Rs84Bulk, 5>>>(a, s);
+            case 466: return launch_ws<8, 4, Stamp<Pm<Rs84Bulk, 6>>>(a, s);
+            // two tiles of register prefetch / the data columns to LDS before the encode
+            // and the next tile's loads issued right after (the youngest encode waves wait
+            // 17-22 % of their cycles for their tile's loads)
+            case 467: return launch_ws<8, 4, Rs84Pf2>(a, s);
+            case 468: return launch_ws<8, 4, Rs84Ep1>(a, s);
+            case 469: return launch_ws<8, 4, Pm<Rs84Pf2, 5>>(a, s);
+            case 470: return launch_ws<8, 4, Pm<Rs84Ep1, 5>>(a, s);
+            case 471: return launch_ws<8, 4, Stamp<Rs84Pf2>>(a, s);
+            case 472: return launch_ws<8, 4, Stamp<Rs84Ep1>>(a, s);
             default: return false;
         }
     }

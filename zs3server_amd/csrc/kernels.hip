@@ -32,6 +32,16 @@ using namespace zs3dev;
 
 namespace zs3k {
 
+thread_local uint32_t t_kernel_bits = 0;
+
+void note_kernel(uint32_t bit) { t_kernel_bits |= bit; }
+
+uint32_t kernel_bits(bool reset) {
+    const uint32_t b = t_kernel_bits;
+    if (reset) t_kernel_bits = 0;
+    return b;
+}
+
 hipError_t ensure_dyn_lds(const void* kern, size_t bytes) {
     static std::mutex mu;
     static std::set<std::tuple<const void*, int, size_t>> done;

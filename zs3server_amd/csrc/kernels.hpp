@@ -26,6 +26,14 @@ enum Path : int {
     PATH_LATENCY = 4,   // small batches: k_encode_only + k_hash_lat (kernels.hip)
 };
 
+// Kernel instances a launch can name beyond its family (zs3_path_mask): bits set on the
+// launching thread, read (and cleared with `reset`) by kernel_bits.
+enum KernelBit : uint32_t {
+    KERNEL_VR_QUAD = 1u << 16,  // k_vr_quad (vr_quad.hpp) served a GET / heal batch
+};
+void note_kernel(uint32_t bit);
+uint32_t kernel_bits(bool reset);
+
 // Batched Split+Encode(+HH256) over n_blocks independent blocks.
 // Block b: data bytes at data + b*data_stride, length n (<= k*S; bytes beyond n are
 // implicit zero padding, as reedsolomon.Split), parity row r at

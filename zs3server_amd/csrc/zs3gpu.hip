@@ -36,6 +36,12 @@ const uint8_t kMagicKey[32] = {0x4b, 0xe7, 0x34, 0xfa, 0x8e, 0x23, 0x8a, 0xcd, 0
                                0x44, 0x14, 0x97, 0xe0, 0x9d, 0x13, 0x22, 0xde, 0x36, 0xa0};
 
 thread_local int t_last_path = -1;
+thread_local uint32_t t_path_mask = 0;  // zs3_path_mask
+
+void note_path(int p) {
+    t_last_path = p;
+    if (p >= 0) t_path_mask |= 1u << p;
+}
 #if ZS3_DIAG
 // Diagnostics build only (libzs3gpu_diag.so): per-OS-thread experiment selection, so
 // concurrent callers never see each other's settings.
@@ -522,7 +528,7 @@ int zs3_encode_batch(const zs3_codec* cc, const uint8_t* d_data, int64_t data_st
 #endif
     int path = zs3k::PATH_NONE;
     rc = map_hip(zs3k::launch_encode(a, (hipStream_t)stream, &path));
-    t_last_path = path;
+    note_path(path);
     return rc;
 }
 
@@ -548,7 +554,7 @@ int zs3_reconstruct_batch(const zs3_codec* cc, uint8_t* d_shards, int64_t block_
     a.variant = call_variant();
     int path = zs3k::PATH_NONE;
     rc = map_hip(zs3k::launch_reconstruct(a, (hipStream_t)stream, &path));
-    t_last_path = path;
+    note_path(path);
     return rc;
 }
 
@@ -587,7 +593,7 @@ int zs3_verify_reconstruct_batch(const zs3_codec* cc, uint8_t* d_shards, int64_t
 #endif
     int path = zs3k::PATH_NONE;
     rc = map_hip(zs3k::launch_verify_reconstruct(a, (hipStream_t)stream, &path));
-    t_last_path = path;
+    note_path(path);
     return rc;
 }
 
@@ -722,7 +728,7 @@ int zs3_reconstruct_batch_masks(const zs3_codec* cc, uint8_t* d_shards, int64_t 
     }
     if (d_ids) (void)hipFreeAsync(d_ids, s);
     if (rc) return rc;
-    t_last_path = last;
+    note_path(last);
     return first;
 }
 
@@ -771,7 +777,7 @@ int zs3_verify_reconstruct_batch_masks(const zs3_codec* cc, uint8_t* d_shards, i
     }
     if (d_ids) (void)hipFreeAsync(d_ids, s);
     if (rc) return rc;
-    t_last_path = last;
+    note_path(last);
     return first;
 }
 
@@ -927,8 +933,9 @@ void par_memcpy(uint8_t* dst, const uint8_t* src, size_t n, int threads) {
 // calls: pinning hundreds of MiB of host memory and allocating the device slots cost more
 // than a 4 GiB stream's own transfers (a 4 GiB pageable RS(16+4) stream: 0.35 s, most of
 // it hipHostMalloc; profiles/r05/stream.jsonl).  Idle buffers are reused by the next call
-// on the same device (first fit of at most twice the size asked for); at most
-// kPoolIdleMax bytes stay idle, the rest is freed.
+// on the same device (first fit of at most twice the size asked for); at most g_pool_max
+// bytes stay idle (6 GiB unless the process sets another cap with zs3_pool_limit, which
+// also trims at once), the oldest idle buffers are freed first.
 struct PoolBuf {
     void* p = nullptr;
     size_t cap = 0;
@@ -938,7 +945,7 @@ struct PoolBuf {
 std::mutex g_pool_mu;
 std::vector<PoolBuf> g_pool;  // idle
 size_t g_pool_idle = 0;
-constexpr size_t kPoolIdleMax = (size_t)6 << 30;
+size_t g_pool_max = (size_t)6 << 30;
 
 hipError_t pool_get(bool host, size_t bytes, void** out) {
     int dev = -1;
@@ -958,22 +965,19 @@ hipError_t pool_get(bool host, size_t bytes, void** out) {
     return host ? hipHostMalloc(out, bytes, hipHostMallocDefault) : hipMalloc(out, bytes);
 }
 
-void pool_put(bool host, void* p, size_t bytes) {
-    if (!p) return;
-    int dev = -1;
-    (void)hipGetDevice(&dev);
-    std::vector<PoolBuf> drop;
-    {
-        std::lock_guard<std::mutex> g(g_pool_mu);
-        g_pool.push_back(PoolBuf{p, bytes, host, dev});
-        g_pool_idle += bytes;
-        while (g_pool_idle > kPoolIdleMax && !g_pool.empty()) {
-            drop.push_back(g_pool.front());
-            g_pool_idle -= g_pool.front().cap;
-            g_pool.erase(g_pool.begin());
-        }
+// with g_pool_mu held: move idle buffers past the cap (oldest first) into `drop`
+void pool_evict_locked(std::vector<PoolBuf>& drop) {
+    while (g_pool_idle > g_pool_max && !g_pool.empty()) {
+        drop.push_back(g_pool.front());
+        g_pool_idle -= g_pool.front().cap;
+        g_pool.erase(g_pool.begin());
     }
+}
+
+size_t pool_free(const std::vector<PoolBuf>& drop) {
+    size_t n = 0;
     for (auto& b : drop) {
+        n += b.cap;
         if (b.host) {
             (void)hipHostFree(b.p);
         } else {
@@ -984,6 +988,21 @@ void pool_put(bool host, void* p, size_t bytes) {
             (void)hipSetDevice(cur);
         }
     }
+    return n;
+}
+
+void pool_put(bool host, void* p, size_t bytes) {
+    if (!p) return;
+    int dev = -1;
+    (void)hipGetDevice(&dev);
+    std::vector<PoolBuf> drop;
+    {
+        std::lock_guard<std::mutex> g(g_pool_mu);
+        g_pool.push_back(PoolBuf{p, bytes, host, dev});
+        g_pool_idle += bytes;
+        pool_evict_locked(drop);
+    }
+    (void)pool_free(drop);
 }
 
 bool is_pinned(const void* p) {
@@ -999,6 +1018,16 @@ bool is_pinned(const void* p) {
 
 extern "C" {
 
+int64_t zs3_pool_limit(uint64_t max_idle_bytes) {
+    std::vector<PoolBuf> drop;
+    {
+        std::lock_guard<std::mutex> g(g_pool_mu);
+        g_pool_max = (size_t)max_idle_bytes;
+        pool_evict_locked(drop);
+    }
+    return (int64_t)pool_free(drop);
+}
+
 }  // extern "C"
 
 namespace {
@@ -1011,6 +1040,7 @@ namespace {
 int stream_range(zs3_codec* c, int device, const uint8_t* src, int64_t b0, int64_t b1, uint8_t* h_parity,
                  uint8_t* h_sums, int64_t NB, bool src_pinned, bool out_pinned, int cpu_threads) {
     if (b1 <= b0) return ZS3_OK;
+    NB = std::min(NB, b1 - b0);
     if (hipSetDevice(device) != hipSuccess) return ZS3_ERR_DEVICE;
     const int k = c->k, m = c->m, R = k + m;
     const int64_t B = c->block_size;
@@ -1159,6 +1189,7 @@ int stream_vr_range(zs3_codec* c, uint8_t* h, int64_t nblk, const uint8_t* prese
     const int64_t E = (int64_t)R * S;
     const bool heal = !data_only;
     const bool hash_out = heal && h_sums_out;
+    NB = std::min(NB, nblk);  // a 2-block object does not size (and pool) 128-block slots
     constexpr int NS = 3;
     struct Slot {
         uint8_t* d = nullptr;    // NB stripes | NB*R*32 expected sums | NB*R int32 flags | NB*R*32 heal sums
@@ -1215,6 +1246,8 @@ int stream_vr_range(zs3_codec* c, uint8_t* h, int64_t nblk, const uint8_t* prese
     };
     if (!pinned && rc == ZS3_OK) start_fill(0);
     std::vector<uint8_t> anyp, anyr;
+    std::vector<int32_t> stat((size_t)NB);               // block status when the caller passes none
+    std::vector<std::pair<int64_t, int64_t>> runs;        // (first block, count) served
     for (int64_t i = 0; i < nbatch && rc == ZS3_OK; ++i) {
         Slot& x = sl[i % NS];
         const int64_t bb = i * NB, nb = std::min(NB, nblk - bb);
@@ -1247,6 +1280,7 @@ int stream_vr_range(zs3_codec* c, uint8_t* h, int64_t nblk, const uint8_t* prese
         } else {
             chk(hipMemcpyAsync(x.d, x.hs, (size_t)(nb * E), hipMemcpyHostToDevice, s_in));
         }
+        if (hash_out) chk(hipMemsetAsync(x.d + off_out, 0, (size_t)nb * R * 32, s_in));  // no stale sums
         if (h_expect)
             chk(hipMemcpyAsync(x.d + off_exp, h_expect + bb * R * 32, (size_t)nb * R * 32, hipMemcpyHostToDevice, s_in));
         else
@@ -1254,9 +1288,24 @@ int stream_vr_range(zs3_codec* c, uint8_t* h, int64_t nblk, const uint8_t* prese
         chk(hipEventRecord(x.in_done, s_in));
         chk(hipEventRecord(ev_in, s_in));
         chk(hipStreamWaitEvent(s_comp, ev_in, 0));
+        int32_t* st_b = status ? status + bb : stat.data();
         const int e = zs3_verify_reconstruct_batch_masks(c, x.d, E, S, nb, present + bb * R, data_only, x.d + off_exp,
                                                          (int32_t*)(x.d + off_bad), hash_out ? x.d + off_out : nullptr,
-                                                         status ? status + bb : nullptr, s_comp);
+                                                         st_b, s_comp);
+        // runs of blocks that were served: a block with too few shards gets nothing back
+        // (its rows that were never uploaded hold whatever the pooled slot last held — bytes
+        // of another call — so they must not reach the caller's buffer)
+        runs.clear();
+        for (int64_t b = 0; b < nb;) {
+            if (st_b[b] != 0) {
+                ++b;
+                continue;
+            }
+            int64_t b2 = b;
+            while (b2 < nb && st_b[b2] == 0) ++b2;
+            runs.emplace_back(b, b2 - b);
+            b = b2;
+        }
         if (e == ZS3_ERR_TOO_FEW_SHARDS || e == ZS3_ERR_SHARD_NO_DATA) {
             if (first_block_err == ZS3_OK) first_block_err = e;
         } else if (e && rc == ZS3_OK) {
@@ -1270,13 +1319,16 @@ int stream_vr_range(zs3_codec* c, uint8_t* h, int64_t nblk, const uint8_t* prese
         // blocks: 7.2 vs 30 GiB/s, profiles/r05/stream.jsonl) — the whole stripes (the
         // present rows come back unchanged)
         uint8_t* dst = pinned ? h + bb * E : x.hs;
-        if (rows2d) {
-            for (int j = 0; j < R; ++j)
-                if (anyr[(size_t)j])
-                    chk(hipMemcpy2DAsync(dst + (size_t)j * S, (size_t)E, x.d + (size_t)j * S, (size_t)E, (size_t)S,
-                                         (size_t)nb, hipMemcpyDeviceToHost, s_out));
-        } else {
-            chk(hipMemcpyAsync(dst, x.d, (size_t)(nb * E), hipMemcpyDeviceToHost, s_out));
+        for (const auto& rn : runs) {
+            const int64_t r0 = rn.first, rl = rn.second;
+            if (rows2d) {
+                for (int j = 0; j < R; ++j)
+                    if (anyr[(size_t)j])
+                        chk(hipMemcpy2DAsync(dst + r0 * E + (size_t)j * S, (size_t)E, x.d + r0 * E + (size_t)j * S,
+                                             (size_t)E, (size_t)S, (size_t)rl, hipMemcpyDeviceToHost, s_out));
+            } else {
+                chk(hipMemcpyAsync(dst + r0 * E, x.d + r0 * E, (size_t)(rl * E), hipMemcpyDeviceToHost, s_out));
+            }
         }
         if (h_bad)
             chk(hipMemcpyAsync(h_bad + bb * R, x.d + off_bad, (size_t)nb * R * 4, hipMemcpyDeviceToHost, s_out));
@@ -1289,11 +1341,13 @@ int stream_vr_range(zs3_codec* c, uint8_t* h, int64_t nblk, const uint8_t* prese
             hipEvent_t done = x.out_done;
             uint8_t* hs = x.hs;
             std::vector<uint8_t> pres(present + bb * R, present + (bb + nb) * R);
+            std::vector<uint8_t> served((size_t)nb);
+            for (int64_t b = 0; b < nb; ++b) served[(size_t)b] = st_b[b] == 0;
             x.drain = std::async(std::launch::async, [=]() -> int {
                 if (hipEventSynchronize(done) != hipSuccess) return ZS3_ERR_DEVICE;
                 for (int64_t b = 0; b < nb; ++b)
                     for (int j = 0; j < R; ++j)
-                        if (!pres[(size_t)(b * R + j)] && (j < k || heal))
+                        if (served[(size_t)b] && !pres[(size_t)(b * R + j)] && (j < k || heal))
                             std::memcpy(h + (bb + b) * E + (size_t)j * S, hs + b * E + (size_t)j * S, (size_t)S);
                 return ZS3_OK;
             });
@@ -1515,6 +1569,12 @@ int zs3_selftest(void) {
 }
 
 int zs3_last_path(void) { return t_last_path; }
+
+uint32_t zs3_path_mask(int reset) {
+    const uint32_t m = t_path_mask | zs3k::kernel_bits(reset != 0);
+    if (reset) t_path_mask = 0;
+    return m;
+}
 
 #if ZS3_DIAG
 int zs3_debug_set_variant(int variant) {

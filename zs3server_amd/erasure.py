@@ -494,16 +494,79 @@ class GPUCodec:
 
 
 def gpu_devices() -> list:
-    """The node's GPUs a queue spreads its blocks over: every visible
-    device, or ZS3_QUEUE_DEVICES (a comma list of HIP ordinals) when set."""
+    """The GPUs a queue spreads its blocks over: the current device
+    only (an empty list: the queue's `device` option, -1 = current) unless
+    ZS3_QUEUE_DEVICES (a comma list of HIP ordinals, e.g. "0,1,2,3,4,5,6,7") opts in to
+    several.  The multi-device queue has run on one GPU only ([0, 0]):
+    until a node-level run checks its parity and scaling it is not the default (ADVICE r05;
+    each listed device also takes its own pinned + HBM staging, §2's footprint)."""
     env = os.environ.get("ZS3_QUEUE_DEVICES")
     if env:
         return [int(x) for x in env.split(",") if x.strip()]
-    from . import device_count
-    try:
-        return list(range(max(1, device_count())))
-    except Exception:  # noqa: BLE001 - no device: the single-device default
-        return []
+    return []
+
+
+# ---- per-block routing: host or device (VERDICT r05 item 3) -----------------------------
+# The reference encodes / decodes every block on the calling goroutine's core
+# (cmd/erasure-encode.go:83-111, cmd/erasure-decode.go:230-276, klauspost/reedsolomon +
+# HighwayHash).  Through the queue a block costs a PCIe round trip plus batching, so the
+# device only wins once enough requests are in flight.  Device side (tools/queue_bench,
+# profiles/r05/queue.jsonl, RS(8+4) 1 MiB encode + sums, synchronous submitters): a lone
+# block takes QUEUE_LONE_S (p50 306 us pinned; GET / heal 527 us, DESIGN.md §13.4) and the
+# queue saturates at QUEUE_MAX_BPS per device (33-39 GiB/s at 256 submitters); with T
+# submitters Little's law gives T*B / (lone + (T-1)*B/max): 21.5 / 30.3 / 33.7 GiB/s at
+# T = 16 / 64 / 256 against 20.3 / 30.2 / 33.2 measured.  Host side: one core runs one
+# block at CPU_CORE_BPS (oracle/cpu_ref.cpp, the reference's AVX-512 GFNI + AVX2 structure,
+# BENCH_r05 cpu_baseline.t1: 5.35 GiB/s encode + sums; heal 6.4, §13.4), so T requests on
+# `host_cores` cores run at min(T, host_cores) x that.
+QUEUE_LONE_S = {"encode": 306e-6, "get": 527e-6, "heal": 527e-6}   # 1 MiB RS(8+4) block
+QUEUE_LONE_BYTES = 1 << 20
+QUEUE_FIXED_S = 240e-6               # the part of a lone block that does not scale with its size
+QUEUE_MAX_BPS = 35 * 2**30           # per device (one PCIe x16 link), profiles/r05/queue.jsonl
+CPU_CORE_BPS = {"encode": 5.35 * 2**30, "get": 6.4 * 2**30, "heal": 6.4 * 2**30}
+
+
+def device_codec_Bps(op: str, live: int, block_bytes: int, devices: int = 1) -> float:
+    """Modelled queue throughput (object bytes/s) with `live` synchronous submitters."""
+    if live <= 0 or block_bytes <= 0:
+        return 0.0
+    lone = QUEUE_FIXED_S + (QUEUE_LONE_S[op] - QUEUE_FIXED_S) * block_bytes / QUEUE_LONE_BYTES
+    cap = QUEUE_MAX_BPS * max(1, devices)
+    return live * block_bytes / (lone + (live - 1) * block_bytes / cap)
+
+
+def host_codec_Bps(op: str, live: int, host_cores: int, cpu_Bps: float | None = None) -> float:
+    """The reference structure's throughput: one block per request per core."""
+    r = CPU_CORE_BPS[op] if cpu_Bps is None else cpu_Bps
+    return min(max(0, live), max(0, host_cores)) * r
+
+
+def codec_on_device(op: str, live: int, block_bytes: int, host_cores: int, devices: int = 1,
+                    cpu_Bps: float | None = None) -> bool:
+    """Where the rocm build runs one per-block EncodeData (op "encode"), GET
+    DecodeDataBlocks ("get") or heal DecodeDataAndParityBlocks ("heal") with `live`
+    requests of that kind in flight (this one included): True = the batching queue,
+    False = the reference's own klauspost/reedsolomon + HighwayHash path on the calling
+    goroutine.  `host_cores` = cores the server lets erasure coding use.  A lone 1 MiB
+    request stays on the host (306-527 us through the device against ~190 us on one core);
+    the device takes over once the queue's modelled rate beats min(live, host_cores) cores
+    — with a whole 16-core host budget that is never on one GPU (33-39 GiB/s against 86),
+    with 2 cores from 5 encode submitters, with 4 from 16.  (Legacy 10 MiB blocks: the
+    lone-block time is extrapolated from the 1 MiB measurement — fixed 240 us + the rest
+    scaled by size — and puts even a lone 10 MiB block on the device.)  Monotone: more
+    live requests never move a block back to the host, more host cores never move one to
+    the device."""
+    if live <= 0 or block_bytes <= 0:
+        return False
+    return device_codec_Bps(op, live, block_bytes, devices) > host_codec_Bps(op, live, host_cores, cpu_Bps)
+
+
+def codec_device_threshold(op: str, block_bytes: int, host_cores: int, devices: int = 1, max_live: int = 1 << 16):
+    """Smallest live-request count that codec_on_device sends to the device (None: never)."""
+    for t in range(1, max_live + 1):
+        if codec_on_device(op, t, block_bytes, host_cores, devices):
+            return t
+    return None
 
 
 _GPU_CODECS: dict = {}

@@ -135,53 +135,39 @@ def test_stream_decode_too_few_shards_reports_the_block(oracle):
             assert np.array_equal(rows(work, b, E, S, R)[:k], rows(ref, b, E, S, R)[:k]), b
 
 
-@pytest.mark.parametrize("heal", [False, True], ids=["get", "heal"])
-@pytest.mark.parametrize("pinned", [False, True], ids=["pageable", "pinned"])
-def test_stream_decode_rs164_four_lost(oracle, heal, pinned):
-    """RS(16+4) with four shards to rebuild on most blocks — the survivor-quad kernel's
-    case (vr_quad.hpp) — through the streamed path.  GET loses four DATA rows (GET rebuilds
-    data rows only, so four lost data rows is what reaches k_vr_quad); heal loses two data
-    and two parity rows.  A reader swap in blocks 10-19 changes the pattern (pattern groups
-    launch on shifted batches); GET blocks 25-29 lose a parity row instead of a data row
-    (three rebuilt rows: the k_vr_ws instances), and that lost parity row must stay
-    untouched.  A rotted survivor chunk is flagged at its (block, shard); the short last
-    block takes the k_vr_ws instances (its shard size is not a multiple of 256).  RS(16+4)
-    rows of 1 MiB blocks are 256-byte aligned, so pinned stripes take the per-row DMA path
-    (only rows some block of the batch has go up), pageable ones the staging."""
-    k, m, nfull, tail = 16, 4, 40, 70001
+def _rs164_case(oracle, heal, pinned, nfull, tail, bands, batch_blocks, want_quad):
+    """RS(16+4) streamed GET / heal over per-block patterns `bands` = [(first, last, lost
+    rows)], a rotted survivor chunk in block 23, every byte vs cpu_ref; want_quad: the
+    survivor-quad kernel (vr_quad.hpp) must have served a batch (zs3_path_mask)."""
+    k, m = 16, 4
     R = k + m
     ref, sums, S, St = make_object(oracle, k, m, nfull, tail, seed=1604)
     E = R * S
-    nb = nfull + 1
+    nb = nfull + (1 if tail else 0)
     present = np.ones((nb, R), bool)
-    if heal:
-        present[:, [0, 7, 16, 19]] = False
-        present[10:20, 7] = True                 # a reader back for ten blocks ...
-        present[10:20, 9] = False                # ... while another drops out (4 lost again)
-    else:
-        present[:, [0, 7, 9, 12]] = False
-        present[10:20, 7] = True
-        present[10:20, 3] = False
-        present[25:30, 12] = True                # three data rows lost, and parity row 17
-        present[25:30, 17] = False
+    for lo, hi, lost in bands:
+        present[lo:hi, lost] = False
     rot_b, rot_row = 23, 11
+    assert present[rot_b, rot_row]
     work_h = z.HostBuffer(nb * E) if pinned else None
     work = work_h.array if pinned else np.empty(nb * E, np.uint8)
     try:
         work[:] = ref
         for b in range(nb):
             Sb = S if b < nfull else St
-            r = rows(work, b, E, Sb, R)
-            r[~present[b]] = 0x5A
+            rows(work, b, E, Sb, R)[~present[b]] = 0x5A
         rows(work, rot_b, E, S, R)[rot_row, 4097] ^= 0x02
         bad = np.full((nb, R), 9, np.int32)
         status = np.full(nb, 77, np.int32)
         out = np.zeros((nb, R, 32), np.uint8) if heal else None
         z.path_mask(reset=True)
         n = z.Codec(k, m, MiB).stream_decode(work_h if pinned else work, nfull * MiB + tail, present, not heal,
-                                             expect=sums, bad=bad, sums_out=out, status=status, batch_blocks=16)
+                                             expect=sums, bad=bad, sums_out=out, status=status,
+                                             batch_blocks=batch_blocks)
+        mask = z.path_mask()
         assert n == nb and (status == 0).all()
-        assert z.path_mask() & z.KERNEL_VR_QUAD, "four rebuilt rows ran on the survivor-quad kernel"
+        if want_quad:
+            assert mask & z.KERNEL_VR_QUAD, f"four rebuilt rows ran on the survivor-quad kernel (mask {mask:#x})"
         want_bad = np.zeros((nb, R), np.int32)
         want_bad[rot_b, rot_row] = 1
         assert np.array_equal(bad, want_bad), np.argwhere(bad != want_bad)[:5]
@@ -201,6 +187,40 @@ def test_stream_decode_rs164_four_lost(oracle, heal, pinned):
     finally:
         if work_h is not None:
             work_h.free()
+
+
+@pytest.mark.parametrize("heal", [False, True], ids=["get", "heal"])
+@pytest.mark.parametrize("pinned", [False, True], ids=["pageable", "pinned"])
+def test_stream_decode_rs164_four_lost(oracle, heal, pinned):
+    """RS(16+4) with four shards to rebuild on most blocks, in one batch large enough for
+    the survivor-quad kernel (vr_quad.hpp; pattern groups of up to 1 024 blocks take the
+    small-batch latency path, kernels.hip small_get): blocks 0-1049 lose four DATA rows in
+    GET (GET rebuilds data rows only, so that is what reaches k_vr_quad) and two data + two
+    parity rows in heal, as one run of blocks (a group with a block-id list takes
+    k_vr_ws); blocks 1050-1059 swap a reader (another four-row pattern); GET blocks
+    1060-1064 lose three data rows and parity row 17, which must stay untouched; the short
+    last block takes the k_vr_ws instances (its shard size is not a multiple of 256).
+    RS(16+4) rows of 1 MiB blocks are 256-byte aligned, so pinned stripes take the per-row
+    DMA path (only rows some block of the batch has go up), pageable ones the
+    staging."""
+    if heal:
+        bands = [(0, 1050, [0, 7, 16, 19]), (1050, 1060, [0, 9, 16, 19]), (1060, 1066, [2, 16])]
+    else:
+        bands = [(0, 1050, [0, 7, 9, 12]), (1050, 1060, [0, 3, 9, 12]), (1060, 1065, [0, 7, 9, 17]),
+                 (1065, 1066, [1, 4])]
+    _rs164_case(oracle, heal, pinned, 1065, 70001, bands, batch_blocks=1066, want_quad=True)
+
+
+@pytest.mark.parametrize("heal", [False, True], ids=["get", "heal"])
+def test_stream_decode_rs164_small_batches(oracle, heal):
+    """The same per-block patterns through 16-block batches: every pattern group is small
+    and takes the latency path (reconstruct + one-chain-per-quad hash), groups launch on
+    shifted batches and on block-id lists."""
+    if heal:
+        bands = [(0, 10, [0, 7, 16, 19]), (10, 20, [0, 9, 16, 19]), (20, 41, [0, 7, 16, 19])]
+    else:
+        bands = [(0, 25, [0, 7, 9, 12]), (25, 30, [0, 7, 9, 17]), (30, 41, [0, 7, 9, 12])]
+    _rs164_case(oracle, heal, False, 40, 70001, bands, batch_blocks=16, want_quad=False)
 
 
 @pytest.mark.parametrize("heal", [False, True], ids=["get", "heal"])

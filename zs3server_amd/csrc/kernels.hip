@@ -1515,7 +1515,8 @@ static hipError_t run_vr(const VrArgs& a, hipStream_t s) {
 // instances for RS(16+4) rebuild / heal 4 instead of the survivor-quad kernel).
 static bool product_get_variant(int v) {
     return v == 0 || (ZS3_DIAG && (v == 246 || v == 247 || v == 420 || v == 423 || v == 424 || v == 429 ||
-                          v == 431 || v == 433 || v == 434 || v == 440 || v == 442 || v == 443 || v == 444));
+                          v == 431 || v == 433 || v == 434 || v == 440 || v == 442 || v == 443 || v == 444 ||
+                          v == 445));
 }
 
 // GET / heal small-batch path: k_reconstruct rebuilds the missing rows, then one chain

@@ -42,6 +42,13 @@ struct Quad16 {
     static constexpr int G = 8, T = 256, CW = 16, TSP = 1, XMAP = 0, PRIO = 1;
     static constexpr bool RR = true;  // partials read at the start of the step
     static constexpr bool UL = false;  // survivors and rebuilt rows in one LDS row array
+    // heal: each stripe's survivor rows 128 bytes further apart (below k_vr_quad)
+    static constexpr bool SWZ = true;
+};
+// Diagnostics: heal without the survivor-stripe pad (the round-5 layout: 8.4 M bank
+// conflicts per 2 048-stripe launch, profiles/r05/pmc_compute.json).
+struct Quad16NoSwz : Quad16 {
+    static constexpr bool SWZ = false;
 };
 // Diagnostics: survivors and rebuilt rows in one LDS row array (the heal hash waves' rows
 // at consecutive strides: SQ_LDS_BANK_CONFLICT 8.4 M -> 0 per launch, but heal 4 3-4 %
@@ -74,12 +81,22 @@ __attribute__((amdgpu_waves_per_eu(4))) k_vr_quad(VrArgs a) {
     // UL: survivors and rebuilt rows of a stripe in one row array ([2][G*RH][TS]: the
     // hash waves' rows at consecutive strides, conflict-free); else two arrays
     constexpr bool UL = C::UL;
-    constexpr int SVB = UL ? G * RH * TS : G * K * TS, RBB = UL ? SVB : G * EX * TS, PBB = G * T;
-    constexpr int SVR = UL ? RH : K, RBR = UL ? RH : EX, RB0 = UL ? K : 0;  // rows per stripe, first rebuilt
+    // SWZ (heal, two arrays; round 6): a wave's 32 hash chains run across stripes, so a
+    // ds_read_b128 lane group reads survivor rows of one stripe next to rebuilt rows of the
+    // previous one.  Rows at TS = T + 32 apart are conflict-free only while the group's 8
+    // rows start at 8 distinct 32-byte slots mod 256, which the one-array layout gives
+    // (row j of stripe g at (20 g + j) * 32 mod 256) and two arrays did not (survivor rows
+    // at (16 g + j) * 32 = j * 32: odd stripes collided with the rebuilt rows of the even
+    // ones: SQ_LDS_BANK_CONFLICT 12.9 % of SQ_LDS_IDX_ACTIVE).  128 bytes more
+    // between survivor stripes put row j of stripe g at g * 128 + j * 32 mod 256, the
+    // one-array slots, while the rebuilt rows keep their own array.
+    constexpr int SSTR = UL ? RH * TS : K * TS + (HOUT && C::SWZ ? 128 : 0);  // survivor stripe stride
+    constexpr int SVB = G * SSTR, RBB = UL ? SVB : G * EX * TS, PBB = G * T;
+    constexpr int RBR = UL ? RH : EX, RB0 = UL ? K : 0;  // rebuilt rows per stripe, first rebuilt
     static_assert(NH % 64 == 0 && NQT % 64 == 0 && NWd == 4 && T % 32 == 0, "whole waves, 16-byte columns");
     typedef typename VecOf<NWd>::type VT;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_dyn[];
-    uint8_t* const SV = smem_dyn;                            // [2][G*SVR][TS] survivors
+    uint8_t* const SV = smem_dyn;                            // [2][G][SSTR] survivors
     uint8_t* const RB = UL ? SV : SV + 2 * SVB;              // [2][G*RBR][TS] rebuilt rows (heal)
     uint8_t* const PB = SV + 2 * SVB + (HOUT && !UL ? 2 * RBB : 0);  // [2][NQ][EX][G*T] partials
     __shared__ int32_t srows[K + EX];
@@ -99,7 +116,7 @@ __attribute__((amdgpu_waves_per_eu(4))) k_vr_quad(VrArgs a) {
         const int chain = pad ? chain0 - G * RH : chain0;
         const int g = chain / RH, cj = chain % RH;
         const bool reb = cj >= K;
-        const uint8_t* const base = reb ? RB + (g * RBR + RB0 + (cj - K)) * TS : SV + (g * SVR + cj) * TS;
+        const uint8_t* const base = reb ? RB + (g * RBR + RB0 + (cj - K)) * TS : SV + g * SSTR + cj * TS;
         const int bufb = reb ? RBB : SVB;
         const int lag = reb ? 2 : 1;
         HHPair st = hh2_init(hh, a.key[0], a.key[1], a.key[2], a.key[3]);
@@ -184,7 +201,7 @@ __attribute__((amdgpu_waves_per_eu(4))) k_vr_quad(VrArgs a) {
     };
     // tile s: survivors to LDS (hash waves), the quad's partials of the four rebuilt rows
     auto compute = [&](int64_t s) {
-        uint8_t* const sv = SV + (s & 1) * SVB + (g * SVR + SQ * q) * TS + o;
+        uint8_t* const sv = SV + (s & 1) * SVB + g * SSTR + SQ * q * TS + o;
         Col<NWd> xs[SQ];
 #pragma unroll
         for (int jj = 0; jj < SQ; ++jj) {
@@ -278,7 +295,9 @@ static bool launch_vr_quad_t(const VrArgs& a, hipStream_t s) {
     constexpr int RH = 16 + (HOUT ? 4 : 0);
     constexpr int NT = vr_nh<G, RH, false>() + 4 * G * (T / CW);
     constexpr int TS = ws_ts<T, false, C::TSP>();
-    constexpr size_t dyn = (size_t)2 * G * RH * TS + (size_t)2 * 4 * 4 * G * T;  // either layout
+    // either layout, plus the heal survivor stripes' pad (SWZ)
+    constexpr size_t dyn = (size_t)2 * G * RH * TS + (HOUT && C::SWZ && !C::UL ? (size_t)2 * G * 128 : 0) +
+                           (size_t)2 * 4 * 4 * G * T;
     static_assert(dyn + 4 * 20 <= 163840 && NT <= 1024, "one workgroup's LDS and threads");
     if (a.k != 16 || a.e != 4 || a.ids || HOUT != (a.sums_out != nullptr)) return false;
     if (a.S % T != 0 || a.S / T < 2 || a.block_stride <= 0) return false;

@@ -29,6 +29,14 @@ int zs3_debug_set_buffer(void* d_dbg);
 int zs3_debug_encode_layout_ok(const void* d_data, int64_t data_stride, int64_t block_len, int64_t n_blocks,
                                const void* d_parity, int64_t parity_stride, int64_t parity_bytes);
 
+/* Host-side phase timers of a batching queue since its creation, microseconds summed
+ * over the threads that spent them (all devices of the queue): [0] submitters' lock and
+ * slot reservation (backpressure included), [1] submitters' copy-in, [2] the dispatcher's
+ * launch calls, [3] the completer's wait for batches, [4] waiters' wait for results,
+ * [5] copy-out, [6] sum of the batches' device stream intervals, [7] their union (device
+ * busy time).  Fills us[0 .. n-1]; returns the number of timers. */
+int zs3_debug_queue_timers(const zs3_queue* q, double* us, int n);
+
 #ifdef __cplusplus
 }
 #endif

@@ -8,6 +8,9 @@
 // devices: a comma list of HIP ordinals for a multi-device queue (e.g. 0,0 on one GPU).
 // pinned = 1: every caller's block buffer comes from zs3_host_alloc (the pinned bpool),
 // so the queue DMAs it zero-copy; 0 (default): pageable buffers, staged by memcpy.
+// Built a second time against the diagnostics library (tools/queue_bench_diag, -DQB_DIAG):
+// each line then also carries the queue's host-side phase timers (zs3_debug_queue_timers)
+// over the run, as thread-seconds per second of wall time, and the device's busy fraction.
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -19,6 +22,9 @@
 #include <vector>
 
 #include "../include/zs3gpu.h"
+#ifdef QB_DIAG
+#include "../include/zs3gpu_diag.h"
+#endif
 
 using Clock = std::chrono::steady_clock;
 
@@ -76,6 +82,10 @@ int main(int argc, char** argv) {
             std::atomic<int> errs{0};
             int64_t b0 = 0, n0 = 0, b1 = 0, n1 = 0;
             zs3_queue_stats(q, &b0, &n0);
+#ifdef QB_DIAG
+            double tm0[8] = {}, tm1[8] = {};
+            zs3_debug_queue_timers(q, tm0, 8);
+#endif
             const auto t0 = Clock::now();
             std::vector<std::thread> th;
             for (int t = 0; t < T; ++t)
@@ -92,6 +102,17 @@ int main(int argc, char** argv) {
             std::vector<double> all;
             for (auto& v : lat) all.insert(all.end(), v.begin(), v.end());
             std::sort(all.begin(), all.end());
+#ifdef QB_DIAG
+            zs3_debug_queue_timers(q, tm1, 8);
+            if (rep == 1) {
+                const char* names[8] = {"sub_lock", "sub_copy", "disp_launch", "comp_sync", "wait_ready", "copy_out",
+                                        "gpu_sum", "gpu_busy"};
+                std::printf("{\"path\": \"queue_timers\", \"threads\": %d, \"pinned\": %s, \"wall_s\": %.4f", T,
+                            pinned ? "true" : "false", dt);
+                for (int i = 0; i < 8; ++i) std::printf(", \"%s\": %.3f", names[i], (tm1[i] - tm0[i]) / 1e6 / dt);
+                std::printf("}\n");
+            }
+#endif
             if (rep == 1)
                 std::printf("{\"path\": \"queue_encode_native\", \"devices\": %d, \"pinned\": %s, \"k\": %d, \"m\": %d, \"threads\": %d, \"blocks\": %d, "
                             "\"GiBps\": %.2f, \"block_latency_us_p50\": %.1f, \"block_latency_us_p99\": %.1f, "

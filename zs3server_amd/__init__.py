@@ -59,7 +59,8 @@ EXPORTS = [
     "zs3_pool_limit",
 ]
 # include/zs3gpu_diag.h: exported by the diagnostics build only
-DIAG_EXPORTS = ["zs3_debug_set_variant", "zs3_debug_set_buffer", "zs3_debug_encode_layout_ok"]
+DIAG_EXPORTS = ["zs3_debug_set_variant", "zs3_debug_set_buffer", "zs3_debug_encode_layout_ok",
+                "zs3_debug_queue_timers"]
 
 
 class ZS3Error(Exception):

@@ -105,6 +105,7 @@ struct Slot {
     std::vector<zs3_req*> reqs;
     Clock::time_point opened;
     hipEvent_t done_ev = nullptr;
+    hipEvent_t start_ev = nullptr;  // diagnostics build: the batch's first stream op (timing)
     hipStream_t stream = nullptr;  // per slot: batches overlap each other's copies and kernels
     int launch_status = ZS3_OK;
     bool ready = false;                          // results are in the pinned slot
@@ -114,6 +115,24 @@ struct Slot {
 };
 
 }  // namespace
+
+#if ZS3_DIAG
+enum QTimer {
+    QT_SUB_LOCK,    // submitters: lock + slot reservation (incl. backpressure waits)
+    QT_SUB_COPY,    // submitters: copy-in (memcpy into the pinned slot / zero-copy DMA call)
+    QT_DISP_LAUNCH, // dispatcher: launch_slot (HIP enqueue calls)
+    QT_COMP_SYNC,   // completer: waiting for a batch's done event
+    QT_WAIT_READY,  // waiters: zs3_req_wait until the batch's results are in the slot
+    QT_COPY_OUT,    // waiters / completer: copy-out (finish_req)
+    QT_GPU_SUM,     // sum of the batches' stream intervals (first copy in .. done), us*1000
+    QT_GPU_UNION,   // union of those intervals (device busy time), us*1000
+    QT_N
+};
+inline int64_t qt_now() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+#endif
 
 // One device's part of a queue: its lanes, staging slots, streams and threads.  A queue
 // (zs3_queue, below) holds one per listed device and assigns every submitted block to
@@ -162,6 +181,14 @@ struct DevQ {
     bool comp_stop = false;  // completer: exit once every launched slot is done
     std::thread disp, comp;
     std::atomic<int64_t> n_batches{0}, n_blocks{0}, n_zc{0};
+#if ZS3_DIAG
+    // Host-side phase timers (zs3_debug_queue_timers, tools/queue_bench_diag): thread-ns
+    // summed over the threads that spent them, and the device's busy time (the union of
+    // the launched batches' stream intervals, from timing events).
+    std::atomic<int64_t> tm[QT_N] = {};
+    hipEvent_t ref_ev = nullptr;  // time origin of the stream intervals
+    double last_end_ms = -1.0;    // completer: end of the union so far
+#endif
 
     // region offsets inside a slot (bytes).  ENCODE: [cap][k*S] data rows, then
     // [cap][m*S] parity rows (each direction one contiguous DMA copy of the bytes that
@@ -201,7 +228,12 @@ int ensure_lane(DevQ* q, std::unique_lock<std::mutex>& lk, int lane) {
         s.lane = lane;
         if (rc == ZS3_OK) rc = map_hip(hipHostMalloc((void**)&s.h, bytes, hipHostMallocDefault));
         if (rc == ZS3_OK) rc = map_hip(hipMalloc((void**)&s.d, bytes));
+#if ZS3_DIAG
+        if (rc == ZS3_OK) rc = map_hip(hipEventCreate(&s.done_ev));  // timed: the device busy time
+        if (rc == ZS3_OK) rc = map_hip(hipEventCreate(&s.start_ev));
+#else
         if (rc == ZS3_OK) rc = map_hip(hipEventCreateWithFlags(&s.done_ev, hipEventDisableTiming));
+#endif
         if (rc == ZS3_OK) rc = map_hip(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
         s.claimed.reset(new std::atomic<uint8_t>[(size_t)cap]);
     }
@@ -210,6 +242,7 @@ int ensure_lane(DevQ* q, std::unique_lock<std::mutex>& lk, int lane) {
             if (s.h) (void)hipHostFree(s.h);
             if (s.d) (void)hipFree(s.d);
             if (s.done_ev) (void)hipEventDestroy(s.done_ev);
+            if (s.start_ev) (void)hipEventDestroy(s.start_ev);
             if (s.stream) (void)hipStreamDestroy(s.stream);
         }
     }
@@ -362,6 +395,9 @@ void launch_slot(DevQ* q, Slot* s) {
     };
     uint8_t* dsum = s->d + q->off_sums();
     uint8_t* hsum = s->h + q->off_sums();
+#if ZS3_DIAG
+    if (s->start_ev) chk(map_hip(hipEventRecord(s->start_ev, st)));
+#endif
     if (s->lane == ENC) {
         // full-size blocks: data rows in, one fused launch, parity rows + sums out
         const size_t KS = (size_t)k * S, MS = (size_t)m * S, po = q->off_par();
@@ -521,7 +557,13 @@ void dispatcher(DevQ* q) {
             q->inflight_blocks[lane] += s->nblocks;
             q->cv_space.notify_all();  // submitters may open the next slot
             lk.unlock();
+#if ZS3_DIAG
+            const int64_t t0 = qt_now();
             launch_slot(q, s);
+            q->tm[QT_DISP_LAUNCH] += qt_now() - t0;
+#else
+            launch_slot(q, s);
+#endif
             lk.lock();
             q->launched.push_back(s);
             q->cv_comp.notify_one();
@@ -563,6 +605,14 @@ void dispatcher(DevQ* q) {
 
 // Copy one finished block's results from the pinned slot into its caller's buffers.
 void finish_req(DevQ* q, Slot* s, zs3_req* r) {
+#if ZS3_DIAG
+    const int64_t t0 = qt_now();
+    struct Acc {
+        DevQ* q;
+        int64_t t0;
+        ~Acc() { q->tm[QT_COPY_OUT] += qt_now() - t0; }
+    } acc{q, t0};
+#endif
     int64_t rc = s->launch_status != ZS3_OK ? s->launch_status : r->status;
     const size_t o = (size_t)r->pos * q->E;
     const int k = q->k, R = q->R;
@@ -614,8 +664,24 @@ void completer(DevQ* q) {
         Slot* s = q->launched.front();
         q->launched.pop_front();
         lk.unlock();
+#if ZS3_DIAG
+        const int64_t tc0 = qt_now();
+#endif
         if (hipEventSynchronize(s->done_ev) != hipSuccess && s->launch_status == ZS3_OK)
             s->launch_status = ZS3_ERR_DEVICE;
+#if ZS3_DIAG
+        q->tm[QT_COMP_SYNC] += qt_now() - tc0;
+        float a_ms = 0.f, b_ms = 0.f;
+        if (q->ref_ev && hipEventElapsedTime(&a_ms, q->ref_ev, s->start_ev) == hipSuccess &&
+            hipEventElapsedTime(&b_ms, q->ref_ev, s->done_ev) == hipSuccess && b_ms >= a_ms) {
+            q->tm[QT_GPU_SUM] += (int64_t)((b_ms - a_ms) * 1e6);
+            const double from = std::max<double>(a_ms, q->last_end_ms);
+            if (b_ms > from) q->tm[QT_GPU_UNION] += (int64_t)((b_ms - from) * 1e6);
+            q->last_end_ms = std::max<double>(q->last_end_ms, b_ms);
+        } else {
+            (void)hipGetLastError();
+        }
+#endif
         const size_t n = s->reqs.size();
         std::vector<int> pos(n);  // read before any waiter can finish (and delete) its request
         for (size_t i = 0; i < n; ++i) pos[i] = s->reqs[i]->pos;
@@ -677,6 +743,12 @@ int devq_new(const zs3_codec* c, int device, const zs3_queue_opts* opts, DevQ** 
         delete q;
         return ZS3_ERR_DEVICE;
     }
+#if ZS3_DIAG
+    if (hipEventCreate(&q->ref_ev) != hipSuccess || hipEventRecord(q->ref_ev, nullptr) != hipSuccess) {
+        (void)hipGetLastError();
+        q->ref_ev = nullptr;
+    }
+#endif
     (void)hipSetDevice(prev);
     q->disp = std::thread(dispatcher, q);
     q->comp = std::thread(completer, q);
@@ -704,8 +776,12 @@ void devq_free(DevQ* q) {
             if (s.h) (void)hipHostFree(s.h);
             if (s.d) (void)hipFree(s.d);
             if (s.done_ev) (void)hipEventDestroy(s.done_ev);
+            if (s.start_ev) (void)hipEventDestroy(s.start_ev);
             if (s.stream) (void)hipStreamDestroy(s.stream);
         }
+#if ZS3_DIAG
+    if (q->ref_ev) (void)hipEventDestroy(q->ref_ev);
+#endif
     delete q;
 }
 
@@ -722,6 +798,9 @@ int devq_submit_encode(DevQ* q, uint8_t* h_buf, int64_t len, uint8_t* h_sums, zs
     r->h_sums = h_sums;
     Slot* s;
     bool lone = false;  // no other batch of the lane in flight (zc_mode 1)
+#if ZS3_DIAG
+    const int64_t t0 = qt_now();
+#endif
     {
         std::unique_lock<std::mutex> lk(q->mu);
         const int rc = reserve(q, lk, r, len == q->B);
@@ -733,6 +812,10 @@ int devq_submit_encode(DevQ* q, uint8_t* h_buf, int64_t len, uint8_t* h_sums, zs
         s = r->slot;
         lone = q->inflight_blocks[ENC] == 0;
     }
+#if ZS3_DIAG
+    const int64_t t1 = qt_now();
+    q->tm[QT_SUB_LOCK] += t1 - t0;
+#endif
     // Split (reedsolomon): data rows are the input bytes, zero-padded to k*S (the
     // kernel reads the pad of a full block as zero).  A full block in pinned memory is
     // DMA'd from the caller's buffer on the slot's stream, ahead of the batch's launch.
@@ -755,6 +838,9 @@ int devq_submit_encode(DevQ* q, uint8_t* h_buf, int64_t len, uint8_t* h_sums, zs
         std::memcpy(dst, h_buf, (size_t)len);
         if (q->k * Sb > len) std::memset(dst + len, 0, (size_t)(q->k * Sb - len));
     }
+#if ZS3_DIAG
+    q->tm[QT_SUB_COPY] += qt_now() - t1;
+#endif
     copy_in_done(q, s);
     *req = r;
     return ZS3_OK;
@@ -911,11 +997,17 @@ int64_t zs3_req_wait(zs3_req* r) {
     Slot* s = r->slot;  // not freed before r is finished
     bool own = false;
     {
+#if ZS3_DIAG
+        const int64_t t0 = qt_now();
+#endif
         std::unique_lock<std::mutex> lk(q->mu);
         if (!r->done) q->cv_disp.notify_one();  // a lone waiter: the device may be idle
         q->cv_done.wait(lk, [&] { return r->done || s->ready; });
         if (!r->done) own = s->claimed[r->pos].exchange(1) == 0;
         if (!own) q->cv_done.wait(lk, [&] { return r->done; });
+#if ZS3_DIAG
+        q->tm[QT_WAIT_READY] += qt_now() - t0;
+#endif
     }
     if (own) {  // copy this block's results out on the calling thread
         finish_req(q, s, r);
@@ -956,6 +1048,16 @@ int zs3_queue_device_stats(const zs3_queue* q, int index, int* device, int64_t* 
     if (blocks) *blocks = d->n_blocks.load();
     return ZS3_OK;
 }
+
+#if ZS3_DIAG
+int zs3_debug_queue_timers(const zs3_queue* q, double* us, int n) {
+    if (!q || !us || n < 0) return ZS3_ERR_INVALID_ARG;
+    for (int i = 0; i < n; ++i) us[i] = 0.0;
+    for (const DevQ* d : q->devs)
+        for (int i = 0; i < n && i < QT_N; ++i) us[i] += (double)d->tm[i].load() / 1e3;
+    return QT_N;
+}
+#endif
 
 int64_t zs3_queue_zero_copy_blocks(const zs3_queue* q) {
     if (!q) return ZS3_ERR_INVALID_ARG;

@@ -207,6 +207,8 @@ struct EncShape {
     static constexpr bool GEN = false;   // general M x K coding matrix (not dyadic)
     static constexpr int XMAP = 0;       // workgroup -> stripe-group order (ws_group)
     static constexpr bool DIAGMOD = false;  // a diagnostics modifier of a product shape
+    static constexpr bool HF = true;     // quad-form hash role: fused packet runs (hh_update_n)
+    static constexpr bool HF2 = false;   // pair-form hash role: fused packet runs (hh2_update_n)
 };
 
 // workgroup -> stripe group (XMAP above k_ehx_ws); a bijection on [0, gridDim.x)
@@ -371,8 +373,12 @@ __attribute__((amdgpu_waves_per_eu(C::WPE))) k_ehx_ws(EncArgs a) {
             uint64_t w[NPK];
 #pragma unroll
             for (int i = 0; i < NPK; ++i) w[i] = p[4 * i];
+            if constexpr (C::HF) {
+                hh_update_n<NPK>(st, w, sel);
+            } else {
 #pragma unroll
-            for (int i = 0; i < NPK; ++i) hh_update(st, w[i], sel);
+                for (int i = 0; i < NPK; ++i) hh_update(st, w[i], sel);
+            }
             bar();
         }
         if constexpr (PFD > 0) asm volatile("s_waitcnt vmcnt(0)" : "+v"(sink)::"memory");
@@ -488,6 +494,9 @@ __attribute__((amdgpu_waves_per_eu(C::WPE))) k_ehx_ws(EncArgs a) {
                 for (int i = 0; i < NPK; ++i) w[i] = p[2 * i];
             }
             if constexpr (PM == 4) __builtin_amdgcn_s_setprio(3);
+            if constexpr (C::HF2 && ABL == 0 && PM != 4) {
+                hh2_update_n<NPK>(st, w);
+            } else
 #pragma unroll
             for (int i = 0; i < NPK; ++i) {
                 if constexpr (PM == 4) {
@@ -892,6 +901,7 @@ struct GetShape {
     static constexpr int WPE = 2;        // waves per SIMD the register budget is sized for
     static constexpr int LDSMIN = 83968; // dynamic-LDS floor (83 968: one workgroup per CU)
     static constexpr int PRIO = 1;       // s_setprio of the rebuild role
+    static constexpr bool HF = true;     // quad-form hash role: fused packet runs (hh_update_n)
     static constexpr int ABL = 0;        // diagnostics timing ablations (output differs)
     static constexpr bool SPL = false;   // with ST + BT: survivor splits before the first table wait
     static constexpr bool DIAGMOD = false;  // a diagnostics modifier of a product shape (Tsp0, XMap, ...)
@@ -1022,8 +1032,12 @@ __attribute__((amdgpu_waves_per_eu(C::WPE))) k_vr_ws(VrArgs a) {
             uint64_t w[NPK];
 #pragma unroll
             for (int i = 0; i < NPK; ++i) w[i] = p[4 * i];
+            if constexpr (C::HF) {
+                hh_update_n<NPK>(st, w, sel);
+            } else {
 #pragma unroll
-            for (int i = 0; i < NPK; ++i) hh_update(st, w[i], sel);
+                for (int i = 0; i < NPK; ++i) hh_update(st, w[i], sel);
+            }
             bar();
         }
         pf_drain();

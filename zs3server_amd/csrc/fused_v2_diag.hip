@@ -49,6 +49,15 @@ struct Rs84Pf2 : Rs84Bulk {
 struct Rs84Ep1 : Rs84Bulk {
     static constexpr int EP = 1;
 };
+// round 6: the quad-form hash role without the fused packet runs (hh_update_n)
+template <class S>
+struct Hf0 : S {
+    static constexpr bool HF = false;
+};
+template <class S>
+struct Hf2 : S {
+    static constexpr bool HF2 = true;
+};
 template <class S>
 struct Stamp : S {
     static constexpr bool WT = true;
@@ -97,6 +106,8 @@ bool launch_ehx_diag(int v, const EncArgs& a, hipStream_t s) {
             case 470: return launch_ws<8, 4, Pm<Rs84Ep1, 5>>(a, s);
             case 471: return launch_ws<8, 4, Stamp<Rs84Pf2>>(a, s);
             case 472: return launch_ws<8, 4, Stamp<Rs84Ep1>>(a, s);
+            case 482: return launch_ws<8, 4, Hf0<Rs84Mid>>(a, s);
+            case 483: return launch_ws<8, 4, Hf2<Rs84Bulk>>(a, s);  // pair-form fused packet runs
             default: return false;
         }
     }
@@ -105,6 +116,7 @@ bool launch_ehx_diag(int v, const EncArgs& a, hipStream_t s) {
             case 400: return a.m == 4 && launch_ws<4, 4, PairG16>(a, s);
             case 402: return a.m == 4 && launch_ws<4, 4, Rs84Bulk>(a, s);
             case 418: return a.m == 4 ? launch_ws<4, 4, XMap<PairG16, 8>>(a, s) : launch_ws<4, 2, XMap<PairG16, 8>>(a, s);
+            case 480: return a.m == 2 && launch_ws<4, 2, Hf0<Config2>>(a, s);  // config 2 without hh_update_n
             default: return false;
         }
     }
@@ -118,6 +130,7 @@ bool launch_ehx_diag(int v, const EncArgs& a, hipStream_t s) {
         }
     }
     if (a.k == 12 && a.m == 4 && v == 416) return launch_ws<12, 4, XMap<Rs124Ua1K, 0>>(a, s);
+    if (a.k == 12 && a.m == 4 && v == 481) return launch_ws<12, 4, Hf0<Rs124Ua1K>>(a, s);
     if (v == 419) return launch_ehx_gen_xmap(a, s);
     return false;
 }

@@ -71,6 +71,29 @@ __device__ __forceinline__ void hh_update(HHLane& s, uint64_t w, uint32_t sel_hi
     s.v1 = zipper_add(s.v1, s.v0, dpp_xor1((uint32_t)(s.v0 >> 32)), sel_hi);
 }
 
+// N consecutive Update() steps (round 6): the same arithmetic as N x hh_update with a
+// shorter dependent chain.  Update's last add (v1 += zipper(v0)) and the next packet's
+// first (v1 += mul0 + w) both land on v1; 64-bit adds commute, so the next packet's
+// mul0 + w is added to v1 while the zipper of v0 is still being formed, and the zipper
+// result is added once: per packet the chain v1 -> DPP -> 2 v_perm -> add -> DPP -> 2
+// v_perm -> add -> v1 is 8 dependent instructions instead of 9, with no extra VALU.
+// Between the first and last packet v1 carries the next packet's mul0 + w (V1 below);
+// the state on return is the standard one.
+template <int N>
+__device__ __forceinline__ void hh_update_n(HHLane& s, const uint64_t (&w)[N], uint32_t sel_hi) {
+    uint64_t V1 = add64(s.v1, add64(s.mul0, w[0]));
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        s.mul0 ^= (uint64_t)(uint32_t)V1 * (s.v0 >> 32);
+        s.v0 = add64(s.v0, s.mul1);
+        s.mul1 ^= (uint64_t)(uint32_t)s.v0 * (V1 >> 32);
+        s.v0 = zipper_add(s.v0, V1, dpp_xor1((uint32_t)(V1 >> 32)), sel_hi);
+        const uint64_t base = i + 1 < N ? add64(V1, add64(s.mul0, w[i + 1])) : V1;
+        V1 = zipper_add(base, s.v0, dpp_xor1((uint32_t)(s.v0 >> 32)), sel_hi);
+    }
+    s.v1 = V1;
+}
+
 // Initial state for lane `lane` under key words key[0..3] (C reference Reset).
 __device__ __forceinline__ HHLane hh_init(int lane, uint64_t k0, uint64_t k1, uint64_t k2, uint64_t k3) {
     const uint64_t key = lane == 0 ? k0 : lane == 1 ? k1 : lane == 2 ? k2 : k3;
@@ -109,17 +132,30 @@ __device__ __forceinline__ void hh_packets(HHLane& s, const uint8_t* row, int np
 // Full-tile form: NPK (compile-time) packets, fully unrolled so every ds_read_b64
 // uses an immediate offset and the register rotation of the loop disappears.
 // Next-packet prefetch as above.
+// Round 6: runs of up to 8 packets through hh_update_n (the next run's reads are issued
+// before the current run's arithmetic).
 template <int NPK>
 __device__ __forceinline__ void hh_packets_n(HHLane& s, const uint8_t* row, int lane, uint32_t sel_hi) {
     const uint64_t* p = reinterpret_cast<const uint64_t*>(row) + lane;
-    uint64_t w = p[0];
+    // the longest run of at most 8 packets that divides NPK
+    constexpr int RUN = NPK <= 8 ? NPK : NPK % 8 == 0 ? 8 : NPK % 6 == 0 ? 6 : NPK % 4 == 0 ? 4 : NPK % 2 == 0 ? 2 : 1;
+    static_assert(NPK % RUN == 0, "whole runs");
+    uint64_t w[RUN];
 #pragma unroll
-    for (int i = 1; i < NPK; ++i) {
-        const uint64_t nxt = p[4 * i];
-        hh_update(s, w, sel_hi);
-        w = nxt;
+    for (int i = 0; i < RUN; ++i) w[i] = p[4 * i];
+#pragma unroll
+    for (int r = 0; r < NPK / RUN; ++r) {
+        uint64_t nx[RUN];
+        if (r + 1 < NPK / RUN) {
+#pragma unroll
+            for (int i = 0; i < RUN; ++i) nx[i] = p[4 * ((r + 1) * RUN + i)];
+        }
+        hh_update_n<RUN>(s, w, sel_hi);
+        if (r + 1 < NPK / RUN) {
+#pragma unroll
+            for (int i = 0; i < RUN; ++i) w[i] = nx[i];
+        }
     }
-    hh_update(s, w, sel_hi);
 }
 
 __device__ __forceinline__ uint32_t rotl32(uint32_t x, uint32_t n) {
@@ -218,6 +254,38 @@ __device__ __forceinline__ void hh2_update(HHPair& s, uint64_t w0, uint64_t w1) 
     zipper_pair(s.v0[1], s.v0[0], aA, aB);
     s.v1[1] = add64(s.v1[1], aA);
     s.v1[0] = add64(s.v1[0], aB);
+}
+
+// N consecutive pair-form updates with the next packet's mul0 + w folded into v1 before
+// the second zipper lands (as hh_update_n): the same VALU, one dependent add less per packet.
+template <int N>
+__device__ __forceinline__ void hh2_update_n(HHPair& s, const uint4 (&w)[N]) {
+    uint64_t V1[2];
+    V1[0] = add64(s.v1[0], add64(s.mul0[0], ((uint64_t)w[0].y << 32) | w[0].x));
+    V1[1] = add64(s.v1[1], add64(s.mul0[1], ((uint64_t)w[0].w << 32) | w[0].z));
+#pragma unroll
+    for (int p = 0; p < N; ++p) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            s.mul0[i] ^= (uint64_t)(uint32_t)V1[i] * (s.v0[i] >> 32);
+            s.v0[i] = add64(s.v0[i], s.mul1[i]);
+            s.mul1[i] ^= (uint64_t)(uint32_t)s.v0[i] * (V1[i] >> 32);
+        }
+        uint64_t aA, aB;
+        zipper_pair(V1[1], V1[0], aA, aB);
+        s.v0[1] = add64(s.v0[1], aA);
+        s.v0[0] = add64(s.v0[0], aB);
+        zipper_pair(s.v0[1], s.v0[0], aA, aB);
+        uint64_t b0 = V1[0], b1 = V1[1];
+        if (p + 1 < N) {
+            b0 = add64(b0, add64(s.mul0[0], ((uint64_t)w[p + 1].y << 32) | w[p + 1].x));
+            b1 = add64(b1, add64(s.mul0[1], ((uint64_t)w[p + 1].w << 32) | w[p + 1].z));
+        }
+        V1[1] = add64(b1, aA);
+        V1[0] = add64(b0, aB);
+    }
+    s.v1[0] = V1[0];
+    s.v1[1] = V1[1];
 }
 
 __device__ __forceinline__ HHPair hh2_init(int h, uint64_t k0, uint64_t k1, uint64_t k2, uint64_t k3) {

@@ -520,8 +520,7 @@ __device__ __forceinline__ uint64_t hash_chain_lat(const uint8_t* row, int64_t S
                 if (base >= npk) break;
                 load(w[(s + NS - 1) % NS], base + (int64_t)(NS - 1) * D);
                 if (base + D <= npk) {
-#pragma unroll
-                    for (int j = 0; j < D; ++j) hh_update(st, w[s][j], sel);
+                    hh_update_n<D>(st, w[s], sel);
                 } else {
 #pragma unroll
                     for (int j = 0; j < D; ++j)

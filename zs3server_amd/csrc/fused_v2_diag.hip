@@ -131,6 +131,7 @@ bool launch_ehx_diag(int v, const EncArgs& a, hipStream_t s) {
     }
     if (a.k == 12 && a.m == 4 && v == 416) return launch_ws<12, 4, XMap<Rs124Ua1K, 0>>(a, s);
     if (a.k == 12 && a.m == 4 && v == 481) return launch_ws<12, 4, Hf0<Rs124Ua1K>>(a, s);
+    if (a.k == 12 && a.m == 4 && v == 484) return launch_ws<12, 4, Stamp<Rs124Ua1K>>(a, s);  // per-wave stamps
     if (v == 419) return launch_ehx_gen_xmap(a, s);
     return false;
 }

@@ -10,4 +10,11 @@ grep '^{' $OUT/stamps_rs124.jsonl | python -c "
 import json,sys
 for l in sys.stdin:
     d=json.loads(l); print(d['objects'], d['ms'], d['clock_GHz'], [(p['wave'], p['role'], p['bar_frac'], p['load_frac']) for p in d['per_wave']], d['by_simd_mix'])"
-echo run7 done
+
+SWEEP_SHAPES=8:4:65536 SWEEP_VARIANTS=0,474 SWEEP_REPEAT=3 timeout -k 10 300 python -u scripts/sweep_variants.py \
+    > $OUT/ab_pm4.jsonl 2>&1 || { tail -20 $OUT/ab_pm4.jsonl; exit 2; }
+grep '^{' $OUT/ab_pm4.jsonl | python -c "
+import json,sys
+for l in sys.stdin:
+    d=json.loads(l); print(d['objects'], d['variant'], d['ms'], d['match'])"
+echo run7b done

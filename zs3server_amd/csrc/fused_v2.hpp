@@ -209,6 +209,7 @@ struct EncShape {
     static constexpr bool DIAGMOD = false;  // a diagnostics modifier of a product shape
     static constexpr bool HF = true;     // quad-form hash role: fused packet runs (hh_update_n)
     static constexpr bool HF2 = false;   // pair-form hash role: fused packet runs (hh2_update_n)
+    static constexpr int ALN = 0;        // UA: realign in registers for S % 16 == ALN (below)
 };
 
 // workgroup -> stripe group (XMAP above k_ehx_ws); a bijection on [0, gridDim.x)
@@ -272,7 +273,7 @@ template <int K, int M, class C>
 __global__ void __launch_bounds__((ws_nh<K, M, C::G, C::T, C::HQ>() + C::G * (C::T / ws_cwe<K, C::CWX>())))
 __attribute__((amdgpu_waves_per_eu(C::WPE))) k_ehx_ws(EncArgs a) {
     constexpr int G = C::G, T = C::T, PF = C::PF, PM = C::PM, CWX = C::CWX, NTM = C::NTM, EP = C::EP, PFD = C::PFD,
-                  TSP = C::TSP, ABL = C::ABL;
+                  TSP = C::TSP, ABL = C::ABL, ALN = C::ALN;
     constexpr bool BUF = C::BUF, HQ = C::HQ, WT = C::WT, RING = C::RING, STB = C::STB, UA = C::UA, GEN = C::GEN;
     constexpr int R = K + M;
     constexpr int NH = ws_nh<K, M, G, T, HQ>();  // hash threads
@@ -559,10 +560,24 @@ __attribute__((amdgpu_waves_per_eu(C::WPE))) k_ehx_ws(EncArgs a) {
 
     VT x[PF][K];
     CoefTab ptab[EP == 3 ? K : 1];  // EP = 3: coefficient tables held in registers
+    // ALN (round 6, unaligned rows, 16-byte buffer-addressed columns, one wave per stripe,
+    // PF 1): row j starts r_j = (j*S) mod 16 bytes past a 16-byte boundary, so the column
+    // loads of the round-3 UA form are unaligned and each tile's last line is fetched again
+    // by the next tile (RS(12+4) on 1 MiB blocks: 1.055 x the data rows' bytes, profiles/
+    // r05/traffic_req_rs124.json).  Here lane l loads the ALIGNED 16-byte chunk l+1 of the
+    // row's tile (for r_j != 0), takes chunk l from lane l-1 (DPP wave_shr) — lane 0 from
+    // a carry, the previous tile's last chunk, handed over by DPP wave_ror — and shifts
+    // the pair into place (v_alignbyte); every chunk is loaded once.
+    VT pc[ALN ? K : 1];
+    static_assert(!ALN || (UA && BUF && NWd == 4 && PF == 1 && T == 1024), "ALN: one 16-byte column per lane, one wave per stripe");
     // rows j of tile offset t0u (wave-uniform) at per-lane byte offset vo within the row
-    auto load_buf = [&](VT (&xs)[K], uint32_t vo, int64_t t0u) {
+    auto load_buf = [&](VT (&xs)[K], uint32_t vo_in, int64_t t0u) {
 #pragma unroll
         for (int j = 0; j < K; ++j) {
+            // ALN: chunk l+1 of the aligned tile, i.e. 16 - r_j bytes past the lane's column
+            // (in the voffset, so the rows keep the product's SGPR offsets)
+            const int rj = ALN ? (int)((j * ALN) & 15) : 0;
+            const uint32_t vo = vo_in + (rj ? (uint32_t)(16 - rj) : 0u);
             const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)(j * S + t0u));
             if constexpr (NWd == 4 && (NTM & 1))
                 asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen nt"
@@ -721,6 +736,37 @@ __attribute__((amdgpu_waves_per_eu(C::WPE))) k_ehx_ws(EncArgs a) {
     auto slot_free = [&](int64_t ti) {
         if (RING && ti >= 2) ring_wait(&ring[2 + (ti & 1)], NHW * (uint32_t)(ti >> 1));
     };
+    // ALN: tile ti's loaded chunks (lane l: chunk l+1 of each unaligned row) -> the row's
+    // bytes [ti*T + 16 l, +16); lane 0's carry becomes the tile's last chunk (for ti+1)
+    auto realign = [&](VT (&xs)[K]) {
+        if constexpr (ALN != 0) {
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                const int r = (j * ALN) & 15;
+                if (r == 0) continue;
+                const int q = r >> 2, sh = r & 3;
+                uint32_t cc[8];
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    cc[d] = 0;
+                    cc[4 + d] = xs[j][d];
+                }
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    if (d < q) continue;
+                    // wave_shr:1 (lane l <- lane l-1; lane 0 keeps `old`, the carry), then
+                    // wave_ror:1 (lane 0 <- lane 63: the next tile's carry)
+                    cc[d] = (uint32_t)__builtin_amdgcn_update_dpp((int)pc[j][d], (int)xs[j][d], 0x138, 0xF, 0xF, false);
+                    pc[j][d] = (uint32_t)__builtin_amdgcn_update_dpp((int)pc[j][d], (int)xs[j][d], 0x13C, 0xF, 0xF, false);
+                }
+                VT out;
+#pragma unroll
+                for (int d = 0; d < 4; ++d)
+                    out[d] = sh ? __builtin_amdgcn_alignbyte(cc[q + d + 1], cc[q + d], (uint32_t)sh) : cc[q + d];
+                xs[j] = out;
+            }
+        }
+    };
     // steady step (see k_ehx): wait for loads(ti) only
     auto step = [&](VT (&xs)[K], int64_t ti) {
         Col<NWd> par[M];
@@ -732,6 +778,7 @@ __attribute__((amdgpu_waves_per_eu(C::WPE))) k_ehx_ws(EncArgs a) {
         } else {
             vm_wait<M + (PF - 1) * (K + M)>(xs);
         }
+        realign(xs);
         if constexpr (EP == 1) {
             static_assert(PF == 1 && !RING && PM != 4, "early prefetch: PF = 1, barrier hand-off");
             uint8_t* tl = tile[ti & 1];
@@ -756,6 +803,9 @@ __attribute__((amdgpu_waves_per_eu(C::WPE))) k_ehx_ws(EncArgs a) {
         if (full || part) slot_free(ti);
         vm_wait<0>(xs);
         Col<NWd> par[M];
+        if constexpr (ALN != 0) {
+            if (full) realign(xs);
+        }
         if constexpr (UA) {
             if (part) tail_cols(xs);
         }
@@ -778,6 +828,20 @@ __attribute__((amdgpu_waves_per_eu(C::WPE))) k_ehx_ws(EncArgs a) {
         // loop rather than at the first use inside every step
 #pragma unroll
         for (int i = 0; i < K; ++i) asm volatile("" ::"v"(ptab[i].ab.x), "v"(ptab[i].ab.y), "v"(ptab[i].ab.z), "v"(ptab[i].ab.w), "v"(ptab[i].c));
+    }
+    if constexpr (ALN != 0) {
+        // the first tile's carry: chunk 0 of every row (the 16 bytes ending at its start), the
+        // same address in every lane of the stripe's wave
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            const int rj = (int)((j * ALN) & 15);
+            const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)(j * S - rj));
+            asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen"
+                         : "=v"(pc[j])
+                         : "v"(vo_d - (uint32_t)o), "s"(rs_d), "s"(so)
+                         : "memory");
+        }
+        vm_wait<0>(pc);
     }
 #pragma unroll
     for (int p = 0; p < PF; ++p) prefetch_any(x[p], p);
@@ -815,6 +879,9 @@ static bool launch_ws(const EncArgs& a, hipStream_t s) {
             // the Split padding (n .. k*S) must lie in the last data row's tail tile
             const int64_t tail = a.S % T;
             if ((int64_t)K * a.S - a.n > tail || a.n <= (int64_t)(K - 1) * a.S) return false;
+            // ALN: the instance's row alignments; the last full tile's chunk 64 must lie inside
+            // the row (a tail of at least 16 bytes)
+            if (C::ALN && ((a.S % 16) != C::ALN || tail < 16)) return false;
         } else {
             if ((a.S % 16) != 0 || a.n != (int64_t)K * a.S) return false;
         }

@@ -58,6 +58,11 @@ template <class S>
 struct Hf2 : S {
     static constexpr bool HF2 = true;
 };
+// round 6: RS(12+4) on 1 MiB blocks (S % 16 = 6) with aligned data-row loads realigned
+// in registers (ALN, fused_v2.hpp)
+struct Rs124Aln : Rs124Ua1K {
+    static constexpr int ALN = 6;
+};
 template <class S>
 struct Stamp : S {
     static constexpr bool WT = true;
@@ -108,6 +113,7 @@ bool launch_ehx_diag(int v, const EncArgs& a, hipStream_t s) {
             case 472: return launch_ws<8, 4, Stamp<Rs84Ep1>>(a, s);
             case 482: return launch_ws<8, 4, Hf0<Rs84Mid>>(a, s);
             case 483: return launch_ws<8, 4, Hf2<Rs84Bulk>>(a, s);  // pair-form fused packet runs
+            case 474: return launch_ws<8, 4, Pm<Rs84Bulk, 4>>(a, s);  // progress-equalising priority
             default: return false;
         }
     }
@@ -132,6 +138,8 @@ bool launch_ehx_diag(int v, const EncArgs& a, hipStream_t s) {
     if (a.k == 12 && a.m == 4 && v == 416) return launch_ws<12, 4, XMap<Rs124Ua1K, 0>>(a, s);
     if (a.k == 12 && a.m == 4 && v == 481) return launch_ws<12, 4, Hf0<Rs124Ua1K>>(a, s);
     if (a.k == 12 && a.m == 4 && v == 484) return launch_ws<12, 4, Stamp<Rs124Ua1K>>(a, s);  // per-wave stamps
+    if (a.k == 12 && a.m == 4 && v == 485) return launch_ws<12, 4, Rs124Aln>(a, s);
+    if (a.k == 12 && a.m == 4 && v == 486) return launch_ws<12, 4, Stamp<Rs124Aln>>(a, s);
     if (v == 419) return launch_ehx_gen_xmap(a, s);
     return false;
 }

@@ -106,7 +106,9 @@ struct Slot {
     Clock::time_point opened;
     hipEvent_t done_ev = nullptr;
     hipEvent_t start_ev = nullptr;  // diagnostics build: the batch's first stream op (timing)
-    hipStream_t stream = nullptr;  // per slot: batches overlap each other's copies and kernels
+    hipStream_t stream = nullptr;  // per slot: batches overlap each other's kernels
+    hipEvent_t ev_in = nullptr;    // split streams: the batch's H2D copies are done
+    hipEvent_t ev_comp = nullptr;  // split streams: the batch's kernels are done
     int launch_status = ZS3_OK;
     bool ready = false;                          // results are in the pinned slot
     int nblocks = 0;                             // blocks at launch (inflight_blocks)
@@ -160,6 +162,14 @@ struct DevQ {
     //     pinned pages: GPU-initiated PCIe reads are slower than the DMA engine (256
     //     submitters 16.6 GiB/s).
     int zc_mode = 1;
+    // Copy streams (round 6).  1 (default): every lane has one H2D and one D2H stream
+    // shared by its slots, the slot's own stream runs only the kernels (events chain the
+    // three), so one batch's D2H runs beside the next one's H2D on the other DMA
+    // direction; 0: each slot's stream carries its H2D, kernels and D2H in order
+    // (rounds 2-5).  tools/queue_bench_diag, profiles/r06/queue_split.jsonl.
+    int split = 1;
+    hipStream_t s_in[NLANE] = {nullptr, nullptr, nullptr};
+    hipStream_t s_out[NLANE] = {nullptr, nullptr, nullptr};
 
     std::mutex mu;
     std::condition_variable cv_space;   // a slot became free / open
@@ -224,6 +234,9 @@ int ensure_lane(DevQ* q, std::unique_lock<std::mutex>& lk, int lane) {
     (void)hipGetDevice(&prev);
     std::vector<Slot> v((size_t)nslots);
     int rc = map_hip(hipSetDevice(device));
+    hipStream_t si = nullptr, so = nullptr;
+    if (q->split && rc == ZS3_OK) rc = map_hip(hipStreamCreateWithFlags(&si, hipStreamNonBlocking));
+    if (q->split && rc == ZS3_OK) rc = map_hip(hipStreamCreateWithFlags(&so, hipStreamNonBlocking));
     for (auto& s : v) {
         s.lane = lane;
         if (rc == ZS3_OK) rc = map_hip(hipHostMalloc((void**)&s.h, bytes, hipHostMallocDefault));
@@ -235,6 +248,8 @@ int ensure_lane(DevQ* q, std::unique_lock<std::mutex>& lk, int lane) {
         if (rc == ZS3_OK) rc = map_hip(hipEventCreateWithFlags(&s.done_ev, hipEventDisableTiming));
 #endif
         if (rc == ZS3_OK) rc = map_hip(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+        if (q->split && rc == ZS3_OK) rc = map_hip(hipEventCreateWithFlags(&s.ev_in, hipEventDisableTiming));
+        if (q->split && rc == ZS3_OK) rc = map_hip(hipEventCreateWithFlags(&s.ev_comp, hipEventDisableTiming));
         s.claimed.reset(new std::atomic<uint8_t>[(size_t)cap]);
     }
     if (rc != ZS3_OK) {
@@ -244,11 +259,19 @@ int ensure_lane(DevQ* q, std::unique_lock<std::mutex>& lk, int lane) {
             if (s.done_ev) (void)hipEventDestroy(s.done_ev);
             if (s.start_ev) (void)hipEventDestroy(s.start_ev);
             if (s.stream) (void)hipStreamDestroy(s.stream);
+            if (s.ev_in) (void)hipEventDestroy(s.ev_in);
+            if (s.ev_comp) (void)hipEventDestroy(s.ev_comp);
         }
+        if (si) (void)hipStreamDestroy(si);
+        if (so) (void)hipStreamDestroy(so);
     }
     (void)hipSetDevice(prev);
     lk.lock();
-    if (rc == ZS3_OK) q->slots[lane] = std::move(v);
+    if (rc == ZS3_OK) {
+        q->slots[lane] = std::move(v);
+        q->s_in[lane] = si;
+        q->s_out[lane] = so;
+    }
     q->lane_state[lane] = rc == ZS3_OK ? DevQ::LANE_READY : DevQ::LANE_NONE;
     q->cv_space.notify_all();
     return rc;
@@ -384,8 +407,12 @@ void copy_in_done(DevQ* q, Slot* s) {
 }
 
 // ---- launch of a closed slot (dispatcher thread, no lock held) ----------------------
+// Three phases: every H2D copy of the batch (stream si), its kernels (the slot's stream
+// sc), every D2H copy (so); with split streams events hand the batch from one to the
+// next, otherwise all three are the slot's stream.
 void launch_slot(DevQ* q, Slot* s) {
-    hipStream_t st = s->stream;
+    const hipStream_t sc = s->stream;
+    const hipStream_t si = q->split ? q->s_in[s->lane] : sc, so = q->split ? q->s_out[s->lane] : sc;
     const int k = q->k, m = q->m, R = q->R;
     const int64_t E = q->E, S = q->S;
     const int nf = s->front;
@@ -393,128 +420,155 @@ void launch_slot(DevQ* q, Slot* s) {
     auto chk = [&](int e) {
         if (e != ZS3_OK && rc == ZS3_OK) rc = e;
     };
+    auto hand = [&](hipStream_t from, hipEvent_t ev, hipStream_t to) {
+        if (from == to) return;
+        chk(map_hip(hipEventRecord(ev, from)));
+        chk(map_hip(hipStreamWaitEvent(to, ev, 0)));
+    };
     uint8_t* dsum = s->d + q->off_sums();
     uint8_t* hsum = s->h + q->off_sums();
 #if ZS3_DIAG
-    if (s->start_ev) chk(map_hip(hipEventRecord(s->start_ev, st)));
+    if (s->start_ev) chk(map_hip(hipEventRecord(s->start_ev, si)));
 #endif
     if (s->lane == ENC) {
-        // full-size blocks: data rows in, one fused launch, parity rows + sums out
+        // full-size blocks: data rows in, one fused launch, parity rows + sums out;
+        // staged blocks move by one DMA per run of staged positions each way; zero-copy
+        // blocks were copied in by their submitter (on sc) and get their parity rows
+        // straight back into the caller's buffer.  Short blocks: one launch each.
         const size_t KS = (size_t)k * S, MS = (size_t)m * S, po = q->off_par();
-        if (nf > 0) {
-            // staged blocks: one DMA per run of staged positions each way; zero-copy
-            // blocks were copied in by their submitter and get their parity rows
-            // straight back into the caller's buffer
-            std::vector<uint8_t> zc((size_t)nf, 0);
-            std::vector<CopyEntry> gin, gout;
-            for (zs3_req* r : s->reqs)
-                if (r->pos < nf && r->zc) {
-                    zc[(size_t)r->pos] = 1;
-                    if (r->d_map) {
-                        gin.push_back({r->d_map, s->d + r->pos * KS, r->len});
-                        gout.push_back({s->d + po + r->pos * MS, r->d_map + KS, (int64_t)MS});
-                    }
+        std::vector<uint8_t> zc((size_t)nf, 0);
+        std::vector<CopyEntry> gin, gout;
+        for (zs3_req* r : s->reqs)
+            if (r->pos < nf && r->zc) {
+                zc[(size_t)r->pos] = 1;
+                if (r->d_map) {
+                    gin.push_back({r->d_map, s->d + r->pos * KS, r->len});
+                    gout.push_back({s->d + po + r->pos * MS, r->d_map + KS, (int64_t)MS});
                 }
-            for_runs(zc, nf, [&](int a, int b) {
-                chk(map_hip(hipMemcpyAsync(s->d + a * KS, s->h + a * KS, (size_t)(b - a) * KS, hipMemcpyHostToDevice, st)));
-            });
-            if (!gin.empty()) chk(run_copy_list(gin, st));
-            chk(zs3_encode_batch(q->c, s->d, (int64_t)KS, q->B, nf, s->d + po, (int64_t)MS, dsum, st));
-            for_runs(zc, nf, [&](int a, int b) {
-                chk(map_hip(hipMemcpyAsync(s->h + po + a * MS, s->d + po + a * MS, (size_t)(b - a) * MS,
-                                           hipMemcpyDeviceToHost, st)));
-            });
-            if (!gout.empty()) chk(run_copy_list(gout, st));
-            for (zs3_req* r : s->reqs)
-                if (r->pos < nf && r->zc && !r->d_map)
-                    chk(map_hip(hipMemcpyAsync(r->h_buf + KS, s->d + po + r->pos * MS, MS, hipMemcpyDeviceToHost, st)));
-            chk(map_hip(hipMemcpyAsync(hsum, dsum, (size_t)nf * R * 32, hipMemcpyDeviceToHost, st)));
-        }
-        for (zs3_req* r : s->reqs) {
-            if (r->pos < nf) continue;
-            const size_t o = (size_t)r->pos * KS, op = po + (size_t)r->pos * MS;
-            uint8_t* sb = dsum + (size_t)r->pos * R * 32;
-            chk(map_hip(hipMemcpyAsync(s->d + o, s->h + o, (size_t)(k * r->S), hipMemcpyHostToDevice, st)));
-            chk(zs3_encode_batch(q->c, s->d + o, (int64_t)KS, r->len, 1, s->d + op, (int64_t)MS, sb, st));
-            chk(map_hip(hipMemcpyAsync(s->h + op, s->d + op, (size_t)(m * r->S), hipMemcpyDeviceToHost, st)));
-            chk(map_hip(hipMemcpyAsync(hsum + (size_t)r->pos * R * 32, sb, (size_t)R * 32, hipMemcpyDeviceToHost, st)));
-        }
+            }
+        for_runs(zc, nf, [&](int a, int b) {
+            chk(map_hip(hipMemcpyAsync(s->d + a * KS, s->h + a * KS, (size_t)(b - a) * KS, hipMemcpyHostToDevice, si)));
+        });
+        for (zs3_req* r : s->reqs)
+            if (r->pos >= nf) {
+                const size_t o = (size_t)r->pos * KS;
+                chk(map_hip(hipMemcpyAsync(s->d + o, s->h + o, (size_t)(k * r->S), hipMemcpyHostToDevice, si)));
+            }
+        hand(si, s->ev_in, sc);
+        if (!gin.empty()) chk(run_copy_list(gin, sc));
+        if (nf > 0) chk(zs3_encode_batch(q->c, s->d, (int64_t)KS, q->B, nf, s->d + po, (int64_t)MS, dsum, sc));
+        for (zs3_req* r : s->reqs)
+            if (r->pos >= nf) {
+                const size_t o = (size_t)r->pos * KS, op = po + (size_t)r->pos * MS;
+                chk(zs3_encode_batch(q->c, s->d + o, (int64_t)KS, r->len, 1, s->d + op, (int64_t)MS,
+                                     dsum + (size_t)r->pos * R * 32, sc));
+            }
+        if (!gout.empty()) chk(run_copy_list(gout, sc));
+        hand(sc, s->ev_comp, so);
+        for_runs(zc, nf, [&](int a, int b) {
+            chk(map_hip(hipMemcpyAsync(s->h + po + a * MS, s->d + po + a * MS, (size_t)(b - a) * MS,
+                                       hipMemcpyDeviceToHost, so)));
+        });
+        for (zs3_req* r : s->reqs)
+            if (r->pos < nf && r->zc && !r->d_map)
+                chk(map_hip(hipMemcpyAsync(r->h_buf + KS, s->d + po + r->pos * MS, MS, hipMemcpyDeviceToHost, so)));
+        if (nf > 0) chk(map_hip(hipMemcpyAsync(hsum, dsum, (size_t)nf * R * 32, hipMemcpyDeviceToHost, so)));
+        for (zs3_req* r : s->reqs)
+            if (r->pos >= nf) {
+                const size_t op = po + (size_t)r->pos * MS, so_ = (size_t)r->pos * R * 32;
+                chk(map_hip(hipMemcpyAsync(s->h + op, s->d + op, (size_t)(m * r->S), hipMemcpyDeviceToHost, so)));
+                chk(map_hip(hipMemcpyAsync(hsum + so_, dsum + so_, (size_t)R * 32, hipMemcpyDeviceToHost, so)));
+            }
     } else {
         const int data_only = s->lane == GET ? 1 : 0;
         int32_t* dbad = (int32_t*)(s->d + q->off_bad());
         uint8_t* hbad = s->h + q->off_bad();
         uint8_t* dout = s->lane == HEAL ? s->d + q->off_out() : nullptr;
         uint8_t* hout = s->h + q->off_out();
-        std::vector<uint8_t> pres;
-        std::vector<int32_t> status;
-        if (nf > 0) {
-            std::vector<uint8_t> zc((size_t)nf, 0);
-            std::vector<CopyEntry> gin;
-            for (zs3_req* r : s->reqs)
-                if (r->pos < nf && r->zc) {
-                    zc[(size_t)r->pos] = 1;
-                    if (r->d_map) {
-                        // the survivors, one entry per run of present rows
-                        std::vector<uint8_t> absent((size_t)R);
-                        for (int i = 0; i < R; ++i) absent[(size_t)i] = !r->present[i];
-                        for_runs(absent, R, [&](int a, int b) {
-                            gin.push_back({r->d_map + (size_t)a * S, s->d + (size_t)r->pos * E + (size_t)a * S,
-                                           (int64_t)(b - a) * S});
-                        });
-                    }
+        std::vector<uint8_t> zc((size_t)nf, 0);
+        std::vector<CopyEntry> gin;
+        for (zs3_req* r : s->reqs)
+            if (r->pos < nf && r->zc) {
+                zc[(size_t)r->pos] = 1;
+                if (r->d_map) {
+                    // the survivors, one entry per run of present rows
+                    std::vector<uint8_t> absent((size_t)R);
+                    for (int i = 0; i < R; ++i) absent[(size_t)i] = !r->present[i];
+                    for_runs(absent, R, [&](int a, int b) {
+                        gin.push_back({r->d_map + (size_t)a * S, s->d + (size_t)r->pos * E + (size_t)a * S,
+                                       (int64_t)(b - a) * S});
+                    });
                 }
-            for_runs(zc, nf, [&](int a, int b) {
-                chk(map_hip(hipMemcpyAsync(s->d + (size_t)a * E, s->h + (size_t)a * E, (size_t)(b - a) * E,
-                                           hipMemcpyHostToDevice, st)));
-            });
-            if (!gin.empty()) chk(run_copy_list(gin, st));
-            chk(map_hip(hipMemcpyAsync(dsum, hsum, (size_t)nf * R * 32, hipMemcpyHostToDevice, st)));
-            pres.assign((size_t)nf * R, 0);
-            status.assign((size_t)nf, ZS3_OK);
+            }
+        for_runs(zc, nf, [&](int a, int b) {
+            chk(map_hip(hipMemcpyAsync(s->d + (size_t)a * E, s->h + (size_t)a * E, (size_t)(b - a) * E,
+                                       hipMemcpyHostToDevice, si)));
+        });
+        if (nf > 0) chk(map_hip(hipMemcpyAsync(dsum, hsum, (size_t)nf * R * 32, hipMemcpyHostToDevice, si)));
+        for (zs3_req* r : s->reqs)
+            if (r->pos >= nf) {
+                const size_t o = (size_t)r->pos * E, so_ = (size_t)r->pos * R * 32;
+                chk(map_hip(hipMemcpyAsync(s->d + o, s->h + o, (size_t)(R * r->S), hipMemcpyHostToDevice, si)));
+                chk(map_hip(hipMemcpyAsync(dsum + so_, hsum + so_, (size_t)R * 32, hipMemcpyHostToDevice, si)));
+            }
+        hand(si, s->ev_in, sc);
+        if (nf > 0) {
+            if (!gin.empty()) chk(run_copy_list(gin, sc));
+            std::vector<uint8_t> pres((size_t)nf * R, 0);
+            std::vector<int32_t> status((size_t)nf, ZS3_OK);
             for (zs3_req* r : s->reqs)
                 if (r->pos < nf) std::memcpy(&pres[(size_t)r->pos * R], r->present, (size_t)R);
             const int e = zs3_verify_reconstruct_batch_masks(q->c, s->d, E, S, nf, pres.data(), data_only, dsum, dbad,
-                                                             dout, status.data(), st);
+                                                             dout, status.data(), sc);
             if (e != ZS3_OK && e != ZS3_ERR_TOO_FEW_SHARDS && e != ZS3_ERR_SHARD_NO_DATA) chk(e);
             for (zs3_req* r : s->reqs)
                 if (r->pos < nf) r->status = status[(size_t)r->pos];
-            chk(map_hip(hipMemcpyAsync(hbad, dbad, (size_t)nf * R * 4, hipMemcpyDeviceToHost, st)));
-            if (dout) chk(map_hip(hipMemcpyAsync(hout, dout, (size_t)nf * R * 32, hipMemcpyDeviceToHost, st)));
         }
         for (zs3_req* r : s->reqs) {
             if (r->pos < nf) continue;
             const size_t o = (size_t)r->pos * E;
-            const size_t so = (size_t)r->pos * R * 32, bo = (size_t)r->pos * R * 4;
-            chk(map_hip(hipMemcpyAsync(s->d + o, s->h + o, (size_t)(R * r->S), hipMemcpyHostToDevice, st)));
-            chk(map_hip(hipMemcpyAsync(dsum + so, hsum + so, (size_t)R * 32, hipMemcpyHostToDevice, st)));
+            const size_t so_ = (size_t)r->pos * R * 32, bo = (size_t)r->pos * R * 4;
             int32_t one = ZS3_OK;
             const int e = zs3_verify_reconstruct_batch_masks(q->c, s->d + o, E, r->S, 1, r->present, data_only,
-                                                             dsum + so, (int32_t*)((uint8_t*)dbad + bo),
-                                                             dout ? dout + so : nullptr, &one, st);
+                                                             dsum + so_, (int32_t*)((uint8_t*)dbad + bo),
+                                                             dout ? dout + so_ : nullptr, &one, sc);
             if (e != ZS3_OK && e != ZS3_ERR_TOO_FEW_SHARDS && e != ZS3_ERR_SHARD_NO_DATA) chk(e);
             r->status = one;
-            chk(map_hip(hipMemcpyAsync(hbad + bo, (uint8_t*)dbad + bo, (size_t)R * 4, hipMemcpyDeviceToHost, st)));
-            if (dout) chk(map_hip(hipMemcpyAsync(hout + so, dout + so, (size_t)R * 32, hipMemcpyDeviceToHost, st)));
         }
-        // rebuilt rows back to the pinned slot (only those, per block), or straight into
-        // a zero-copy caller's shard rows (copy-list mode: one launch for the batch)
+        // rebuilt rows to zero-copy callers in copy-list mode: one launch for the batch
         std::vector<CopyEntry> gout;
         for (zs3_req* r : s->reqs) {
-            if (r->status != ZS3_OK) continue;
+            if (r->status != ZS3_OK || !r->zc || !r->d_map) continue;
+            const size_t o = (size_t)r->pos * E;
+            for (int i = 0; i < R; ++i)
+                if (!r->present[i] && (i < k || !data_only))
+                    gout.push_back({s->d + o + (size_t)i * r->S, r->d_map + (size_t)i * r->S, r->S});
+        }
+        if (!gout.empty()) chk(run_copy_list(gout, sc));
+        hand(sc, s->ev_comp, so);
+        if (nf > 0) {
+            chk(map_hip(hipMemcpyAsync(hbad, dbad, (size_t)nf * R * 4, hipMemcpyDeviceToHost, so)));
+            if (dout) chk(map_hip(hipMemcpyAsync(hout, dout, (size_t)nf * R * 32, hipMemcpyDeviceToHost, so)));
+        }
+        for (zs3_req* r : s->reqs) {
+            if (r->pos < nf) continue;
+            const size_t so_ = (size_t)r->pos * R * 32, bo = (size_t)r->pos * R * 4;
+            chk(map_hip(hipMemcpyAsync(hbad + bo, (uint8_t*)dbad + bo, (size_t)R * 4, hipMemcpyDeviceToHost, so)));
+            if (dout) chk(map_hip(hipMemcpyAsync(hout + so_, dout + so_, (size_t)R * 32, hipMemcpyDeviceToHost, so)));
+        }
+        // rebuilt rows back to the pinned slot (only those, per block), or straight into
+        // a zero-copy caller's shard rows
+        for (zs3_req* r : s->reqs) {
+            if (r->status != ZS3_OK || (r->zc && r->d_map)) continue;
             const size_t o = (size_t)r->pos * E;
             uint8_t* hdst = r->zc ? r->h_shards : s->h + o;
             for (int i = 0; i < R; ++i)
-                if (!r->present[i] && (i < k || !data_only)) {
-                    if (r->zc && r->d_map)
-                        gout.push_back({s->d + o + (size_t)i * r->S, r->d_map + (size_t)i * r->S, r->S});
-                    else
-                        chk(map_hip(hipMemcpyAsync(hdst + (size_t)i * r->S, s->d + o + (size_t)i * r->S,
-                                                   (size_t)r->S, hipMemcpyDeviceToHost, st)));
-                }
+                if (!r->present[i] && (i < k || !data_only))
+                    chk(map_hip(hipMemcpyAsync(hdst + (size_t)i * r->S, s->d + o + (size_t)i * r->S, (size_t)r->S,
+                                               hipMemcpyDeviceToHost, so)));
         }
-        if (!gout.empty()) chk(run_copy_list(gout, st));
     }
-    chk(map_hip(hipEventRecord(s->done_ev, st)));
+    chk(map_hip(hipEventRecord(s->done_ev, so)));
     s->launch_status = rc;
     q->n_batches.fetch_add(1);
     q->n_blocks.fetch_add((int64_t)s->reqs.size());
@@ -737,6 +791,7 @@ int devq_new(const zs3_codec* c, int device, const zs3_queue_opts* opts, DevQ** 
     // production server's transport: ADVICE r04)
     if (const char* e = std::getenv("ZS3_QUEUE_ZC")) q->zc_mode = std::max(0, std::min(3, std::atoi(e)));
     if (const char* e = std::getenv("ZS3_QUEUE_PIPE_PCT")) q->pipe_pct = std::max(10, std::min(100, std::atoi(e)));
+    if (const char* e = std::getenv("ZS3_QUEUE_SPLIT")) q->split = std::atoi(e) ? 1 : 0;
 #endif
     int prev = dev;
     if (hipSetDevice(q->device) != hipSuccess) {
@@ -778,7 +833,13 @@ void devq_free(DevQ* q) {
             if (s.done_ev) (void)hipEventDestroy(s.done_ev);
             if (s.start_ev) (void)hipEventDestroy(s.start_ev);
             if (s.stream) (void)hipStreamDestroy(s.stream);
+            if (s.ev_in) (void)hipEventDestroy(s.ev_in);
+            if (s.ev_comp) (void)hipEventDestroy(s.ev_comp);
         }
+    for (int lane = 0; lane < NLANE; ++lane) {
+        if (q->s_in[lane]) (void)hipStreamDestroy(q->s_in[lane]);
+        if (q->s_out[lane]) (void)hipStreamDestroy(q->s_out[lane]);
+    }
 #if ZS3_DIAG
     if (q->ref_ev) (void)hipEventDestroy(q->ref_ev);
 #endif

@@ -184,6 +184,10 @@ struct DevQ {
     int inflight_blocks[NLANE] = {0, 0, 0};  // blocks of the launched, unfinished slots
     std::vector<Slot*> sealed[NLANE];         // closed to new blocks, waiting for copiers
     int pipe_pct = 50;                        // seal at this % of the live blocks (ZS3_QUEUE_PIPE_PCT)
+    // which blocks count as live for the seal point: 0 = the open slot's + the launched
+    // ones (rounds 4-5), 1 = every block submitted to this device and not yet finished,
+    // including submitters parked on backpressure (ZS3_QUEUE_PIPE_LIVE)
+    int pipe_live = 0;
     std::atomic<int> live[NLANE]{};           // blocks assigned to this device, not yet finished
     std::deque<Slot*> launched;
     bool flush = false;
@@ -576,7 +580,9 @@ void launch_slot(DevQ* q, Slot* s) {
 
 // Blocks at which the open slot closes for pipelining (ready_to_close); caller holds mu.
 int pipe_size(const DevQ* q, const Slot* s, int lane) {
-    return zs3q::seal_blocks((int)s->reqs.size() + q->inflight_blocks[lane], q->pipe_pct, q->cap);
+    int live = (int)s->reqs.size() + q->inflight_blocks[lane];
+    if (q->pipe_live) live = std::max(live, q->live[lane].load(std::memory_order_relaxed));
+    return zs3q::seal_blocks(live, q->pipe_pct, q->cap);
 }
 
 bool ready_to_close(DevQ* q, Slot* s, int lane, Clock::time_point now) {
@@ -791,6 +797,7 @@ int devq_new(const zs3_codec* c, int device, const zs3_queue_opts* opts, DevQ** 
     // production server's transport: ADVICE r04)
     if (const char* e = std::getenv("ZS3_QUEUE_ZC")) q->zc_mode = std::max(0, std::min(3, std::atoi(e)));
     if (const char* e = std::getenv("ZS3_QUEUE_PIPE_PCT")) q->pipe_pct = std::max(10, std::min(100, std::atoi(e)));
+    if (const char* e = std::getenv("ZS3_QUEUE_PIPE_LIVE")) q->pipe_live = std::atoi(e) ? 1 : 0;
     if (const char* e = std::getenv("ZS3_QUEUE_SPLIT")) q->split = std::atoi(e) ? 1 : 0;
 #endif
     int prev = dev;

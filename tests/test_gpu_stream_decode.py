@@ -294,3 +294,25 @@ def test_stream_decode_argument_checks():
         c.stream_decode(st, 2 * MiB, pres, True, status=np.zeros(4, np.int32)[::2])
     with pytest.raises(ValueError):
         c.stream_decode(st.reshape(2, -1)[:, ::2], 2 * MiB, pres, True)
+
+
+def test_stream_encode_argument_checks():
+    """The encode stream wrappers check their host buffers' sizes the same way: a source
+    shorter than total_len, or parity / sums arrays shorter than the object's blocks need,
+    are refused before the library reads or writes them."""
+    k, m = 8, 4
+    c = z.Codec(k, m, MiB)
+    S = MiB // k
+    src = np.zeros(2 * MiB, np.uint8)
+    par = np.zeros(2 * m * S, np.uint8)
+    sums = np.zeros(2 * (k + m) * 32, np.uint8)
+    for call in (lambda *a: c.stream_encode(*a), lambda *a: c.stream_encode_multi([0], *a)):
+        with pytest.raises(ValueError):
+            call(src[:-1], 2 * MiB, par, sums)          # source shorter than the stream
+        with pytest.raises(ValueError):
+            call(src, 2 * MiB, par[:-1], sums)          # parity for fewer blocks
+        with pytest.raises(ValueError):
+            call(src, 2 * MiB, par, sums[:-32])         # sums for fewer shards
+        with pytest.raises(ValueError):
+            call(src.reshape(2, -1)[:, ::2], MiB // 2, par, sums)  # strided source
+    assert c.stream_encode(src, 2 * MiB, par, sums) == 2

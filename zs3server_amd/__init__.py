@@ -324,22 +324,43 @@ class Codec:
         _check(S, "EncodeData")
         return S, (out.reshape(self.k + self.m, 32) if sums else None)
 
+    def _stream_encode_args(self, name, src, total_len, parity, sums, batch_blocks):
+        """Addresses of the encode stream's host buffers after checking their sizes: the
+        library reads total_len bytes of src and writes nblocks*m*S parity bytes and
+        nblocks*(k+m)*32 sum bytes through raw pointers (a short buffer would be overrun)."""
+        import numpy as np
+
+        if total_len < 0 or batch_blocks <= 0:
+            raise ValueError(f"{name}: total_len >= 0 and batch_blocks > 0")
+        B, k, m = self.block_size, self.k, self.m
+        S = -(-B // k)
+        nblocks = -(-total_len // B)
+        out = []
+        for x, what, need in ((src, "src", total_len), (parity, "parity", nblocks * m * S),
+                              (sums, "sums", nblocks * (k + m) * 32)):
+            if isinstance(x, HostBuffer):
+                if not x.ptr or x.nbytes < need:
+                    raise ValueError(f"{name}: {what} holds {x.nbytes} bytes, {nblocks} blocks need {need}")
+                out.append(x.ptr)
+            else:
+                if not isinstance(x, np.ndarray) or not x.flags.c_contiguous or x.nbytes < need:
+                    raise ValueError(f"{name}: {what} must be a C-contiguous numpy array of >= {need} bytes")
+                out.append(x.ctypes.data)
+        return out
+
     def stream_encode(self, src, total_len: int, parity, sums, batch_blocks: int = 256) -> int:
         """End-to-end host stream: returns the number of blocks (zs3_stream_encode).
         src/parity/sums are host buffers (numpy arrays or pinned HostBuffer)."""
-        def addr(x):
-            return x.ptr if isinstance(x, HostBuffer) else x.ctypes.data
-        n = self._L.zs3_stream_encode(self._h, addr(src), total_len, addr(parity), addr(sums), batch_blocks)
+        a, p, q = self._stream_encode_args("stream_encode", src, total_len, parity, sums, batch_blocks)
+        n = self._L.zs3_stream_encode(self._h, a, total_len, p, q, batch_blocks)
         return _check(n, "stream_encode")
 
     def stream_encode_multi(self, devices, src, total_len: int, parity, sums, batch_blocks: int = 256) -> int:
         """zs3_stream_encode_multi: the stream split over `devices` (one host thread,
         stream set and pinned slots per device)."""
-        def addr(x):
-            return x.ptr if isinstance(x, HostBuffer) else x.ctypes.data
+        a, p, q = self._stream_encode_args("stream_encode_multi", src, total_len, parity, sums, batch_blocks)
         devs = (C.c_int * len(devices))(*devices)
-        n = self._L.zs3_stream_encode_multi(self._h, devs, len(devices), addr(src), total_len, addr(parity),
-                                            addr(sums), batch_blocks)
+        n = self._L.zs3_stream_encode_multi(self._h, devs, len(devices), a, total_len, p, q, batch_blocks)
         return _check(n, "stream_encode_multi")
 
     def stream_decode(self, stripes, total_len: int, present, data_only: bool, expect=None, bad=None,

@@ -23,6 +23,7 @@
 
 #include <stdlib.h>
 
+#include <algorithm>
 #include <mutex>
 #include <set>
 #include <tuple>
@@ -1727,6 +1728,41 @@ hipError_t launch_fill(uint8_t* out, int64_t stride, int64_t len, int64_t n, uin
     const unsigned gx = (unsigned)((nw + 255) / 256 < 256 ? (nw + 255) / 256 : 256);
     const unsigned gy = (unsigned)(n < 65535 ? n : 65535);
     hipLaunchKernelGGL(k_fill, dim3(gx, gy), dim3(256), 0, s, out, stride, len, n, seed, obj0);
+    return hipGetLastError();
+}
+
+// Rebuilt rows of a batch of stripes, device -> host (zs3_stream_decode on rows that are
+// not 256-byte aligned, zs3gpu.hip stream_vr_range): for blocks b < nb and rows rs.row[],
+// S bytes at b*E + row*S from src to the same offset of dst.  The two bases are congruent
+// mod 16 (the caller checks), so each row is a ragged head, 16-byte words, a ragged tail.
+// The HIP runtime's own D2H of the whole stripes moved 8x the bytes (profiles/r06/dma_sg).
+__global__ void __launch_bounds__(256) k_rows_copy(const uint8_t* src, uint8_t* dst, int64_t E, int64_t S, int64_t nb,
+                                                   RowSet rs) {
+    for (int64_t p = blockIdx.y; p < nb * rs.n; p += gridDim.y) {
+        const int64_t off = (p / rs.n) * E + (int64_t)rs.row[p % rs.n] * S;
+        const uint8_t* sp = src + off;
+        uint8_t* dp = dst + off;
+        const int64_t h = std::min<int64_t>((16 - ((uintptr_t)dp & 15)) & 15, S);
+        const int64_t nw = (S - h) >> 4;
+        const int64_t t0 = h + nw * 16;
+        if (blockIdx.x == 0 && threadIdx.x < h) dp[threadIdx.x] = sp[threadIdx.x];
+        if (blockIdx.x == 0 && threadIdx.x < S - t0) dp[t0 + threadIdx.x] = sp[t0 + threadIdx.x];
+        const uint4* s4 = reinterpret_cast<const uint4*>(sp + h);
+        uint4* d4 = reinterpret_cast<uint4*>(dp + h);
+        for (int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x; w < nw; w += (int64_t)gridDim.x * 256) d4[w] = s4[w];
+    }
+    __threadfence_system();  // host-visible before the batch's completion event
+}
+
+hipError_t launch_rows_copy(const uint8_t* src, uint8_t* dst, int64_t E, int64_t S, int64_t nb, const RowSet& rs,
+                            hipStream_t s) {
+    if (nb <= 0 || rs.n <= 0 || S <= 0) return hipSuccess;
+    if ((((uintptr_t)src - (uintptr_t)dst) & 15) != 0 || rs.n > 32) return hipErrorInvalidValue;
+    const int64_t words = (S + 15) / 16;
+    const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(64, (words + 255) / 256));
+    const int64_t pairs = nb * rs.n;
+    const unsigned gy = (unsigned)(pairs < 65535 ? pairs : 65535);
+    hipLaunchKernelGGL(k_rows_copy, dim3(gx, gy), dim3(256), 0, s, src, dst, E, S, nb, rs);
     return hipGetLastError();
 }
 

@@ -154,6 +154,14 @@ hipError_t launch_verify_reconstruct(const VrArgs& a, hipStream_t s, int* path);
 hipError_t launch_hash(const HashArgs& a, hipStream_t s);
 hipError_t launch_md5(const DigestArgs& a, hipStream_t s);
 hipError_t launch_sha256(const DigestArgs& a, hipStream_t s);
+// k_rows_copy: rows rs.row[0..n) of nb stripes (stride E, rows of S bytes), src -> dst at
+// the same offsets (bases congruent mod 16; n <= 32).
+struct RowSet {
+    int n;
+    int row[32];
+};
+hipError_t launch_rows_copy(const uint8_t* src, uint8_t* dst, int64_t E, int64_t S, int64_t nb, const RowSet& rs,
+                            hipStream_t s);
 hipError_t launch_fill(uint8_t* out, int64_t stride, int64_t len, int64_t n, uint64_t seed,
                        uint64_t obj0, hipStream_t s);
 // out[r] = 1 if any of flags[r*cols .. r*cols+cols) is non-zero, else 0.

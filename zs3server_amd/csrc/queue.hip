@@ -183,11 +183,15 @@ struct DevQ {
     int inflight[NLANE] = {0, 0, 0};
     int inflight_blocks[NLANE] = {0, 0, 0};  // blocks of the launched, unfinished slots
     std::vector<Slot*> sealed[NLANE];         // closed to new blocks, waiting for copiers
-    int pipe_pct = 50;                        // seal at this % of the live blocks (ZS3_QUEUE_PIPE_PCT)
-    // which blocks count as live for the seal point: 0 = the open slot's + the launched
-    // ones (rounds 4-5), 1 = every block submitted to this device and not yet finished,
-    // including submitters parked on backpressure (ZS3_QUEUE_PIPE_LIVE)
-    int pipe_live = 0;
+    // Seal point (ready_to_close): the open slot closes at pipe_pct % of the live blocks.
+    // Round 6 (profiles/r06/queue_pipe.jsonl, queue_pipe_live.jsonl, split copy streams):
+    // 33 % keeps three batches in flight (64 submitters 34.6-35.9 -> 37.8-39.4 GiB/s), and
+    // the live count includes submitters parked on backpressure (pipe_live 1) — counting
+    // only the open + launched blocks shrinks the seal point whenever every slot is busy,
+    // down to 8-block batches at 25 % (256 submitters 10-11 GiB/s).  Diagnostics build:
+    // ZS3_QUEUE_PIPE_PCT, ZS3_QUEUE_PIPE_LIVE (0 = rounds 4-5).
+    int pipe_pct = 33;
+    int pipe_live = 1;
     std::atomic<int> live[NLANE]{};           // blocks assigned to this device, not yet finished
     std::deque<Slot*> launched;
     bool flush = false;
@@ -593,7 +597,8 @@ bool ready_to_close(DevQ* q, Slot* s, int lane, Clock::time_point now) {
     // one's H2D under the other's kernel and D2H, instead of one batch of all of them
     // (1 MiB RS(8+4), 64 submitters: 29.9-30.5 GiB/s at batches of 32 vs 21-24 at 64-128;
     // 256 submitters: 33-35 at 64; profiles/r04/queue_ab3.jsonl), at most the slot's
-    // size (zs3q::slot_blocks: 64 MiB of input)
+    // size (zs3q::slot_blocks: 64 MiB of input); since round 6 at a third of them
+    // (DevQ::pipe_pct), three batches in flight on the split copy streams
     if (s->front + s->back >= pipe_size(q, s, lane)) return true;
     // batch while busy: launch at once while fewer than slots-1 batches are in flight
     // (a small batch is bound by one hash chain's latency, ~0.5 ms for 128 KiB shards,

@@ -1005,6 +1005,16 @@ void pool_put(bool host, void* p, size_t bytes) {
     (void)pool_free(drop);
 }
 
+// The device-side address of pinned host memory (a kernel's view of it), or nullptr.
+uint8_t* host_dev_ptr(void* p) {
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess || !d) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    return (uint8_t*)d;
+}
+
 bool is_pinned(const void* p) {
     hipPointerAttribute_t attr;
     if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
@@ -1194,6 +1204,8 @@ int stream_vr_range(zs3_codec* c, uint8_t* h, int64_t nblk, const uint8_t* prese
     struct Slot {
         uint8_t* d = nullptr;    // NB stripes | NB*R*32 expected sums | NB*R int32 flags | NB*R*32 heal sums
         uint8_t* hs = nullptr;   // pinned staging of NB stripes (pageable caller)
+        uint8_t* hsm = nullptr;  // pinned staging: NB*R*32 expected sums | NB*R int32 flags | NB*R*32 heal sums
+        uint8_t* hs_dev = nullptr;  // hs as a kernel addresses it (k_rows_copy)
         hipEvent_t in_done = nullptr, out_done = nullptr;
         bool used = false;
         std::future<int> fill, drain;
@@ -1213,15 +1225,25 @@ int stream_vr_range(zs3_codec* c, uint8_t* h, int64_t nblk, const uint8_t* prese
     chk(hipEventCreateWithFlags(&ev_comp, hipEventDisableTiming));
     const size_t off_exp = (size_t)NB * E, off_bad = off_exp + (size_t)NB * R * 32, off_out = off_bad + (size_t)NB * R * 4;
     const size_t dbytes = off_out + (size_t)NB * R * 32;
+    // The per-block arrays (expected sums in, flags and heal sums out) are the caller's
+    // own, usually pageable, memory: an async copy to or from pageable memory makes the
+    // host wait for the stream to drain first, which serialised every batch's H2D behind
+    // the previous batch's D2H (rocprofv3 DMA trace, profiles/r06/dma_sg).  They move
+    // through this pinned staging instead; the drain copies the outputs out.
+    const size_t sm_bad = (size_t)NB * R * 32, sm_out = sm_bad + (size_t)NB * R * 4;
+    const size_t smbytes = sm_out + (size_t)NB * R * 32;
     for (auto& x : sl) {
         chk(pool_get(false, dbytes, (void**)&x.d));
+        chk(pool_get(true, smbytes, (void**)&x.hsm));
         if (!pinned) chk(pool_get(true, (size_t)NB * E, (void**)&x.hs));
+        if (x.hs) x.hs_dev = host_dev_ptr(x.hs);
         chk(hipEventCreateWithFlags(&x.in_done, hipEventDisableTiming));
         chk(hipEventCreateWithFlags(&x.out_done, hipEventDisableTiming));
     }
     const int th = std::max(1, cpu_threads / 2);
     const int64_t nbatch = (nblk + NB - 1) / NB;
     const bool rows2d = (S % 256) == 0;  // per-row strided DMA only for aligned rows
+    uint8_t* const h_dev = pinned && !rows2d ? host_dev_ptr(h) : nullptr;
     // rows of a batch: `any_present` to upload, `any_rebuilt` to bring back
     auto rows_of = [&](int64_t bb, int64_t nb, std::vector<uint8_t>& any_present, std::vector<uint8_t>& any_rebuilt) {
         any_present.assign((size_t)R, 0);
@@ -1281,9 +1303,10 @@ int stream_vr_range(zs3_codec* c, uint8_t* h, int64_t nblk, const uint8_t* prese
             chk(hipMemcpyAsync(x.d, x.hs, (size_t)(nb * E), hipMemcpyHostToDevice, s_in));
         }
         if (hash_out) chk(hipMemsetAsync(x.d + off_out, 0, (size_t)nb * R * 32, s_in));  // no stale sums
-        if (h_expect)
-            chk(hipMemcpyAsync(x.d + off_exp, h_expect + bb * R * 32, (size_t)nb * R * 32, hipMemcpyHostToDevice, s_in));
-        else
+        if (h_expect) {
+            std::memcpy(x.hsm, h_expect + bb * R * 32, (size_t)nb * R * 32);  // the slot's last D2H is done
+            chk(hipMemcpyAsync(x.d + off_exp, x.hsm, (size_t)nb * R * 32, hipMemcpyHostToDevice, s_in));
+        } else
             chk(hipMemsetAsync(x.d + off_exp, 0, (size_t)nb * R * 32, s_in));
         chk(hipEventRecord(x.in_done, s_in));
         chk(hipEventRecord(ev_in, s_in));
@@ -1316,9 +1339,20 @@ int stream_vr_range(zs3_codec* c, uint8_t* h, int64_t nblk, const uint8_t* prese
         // rebuilt rows back into the caller's stripes (pinned) or the slot's staging: one
         // strided copy per rebuilt row index, or — for rows that are not 256-byte aligned,
         // which the DMA engine copies strided at a fraction of its rate (RS(12+4) on 1 MiB
-        // blocks: 7.2 vs 30 GiB/s, profiles/r05/stream.jsonl) — the whole stripes (the
-        // present rows come back unchanged)
+        // blocks: 7.2 vs 30 GiB/s, profiles/r05/stream.jsonl) — one k_rows_copy launch per
+        // run of served blocks (round 6: the whole stripes before, 8x the bytes for two
+        // rebuilt rows of RS(12+4); the whole stripes still when the two bases are not
+        // congruent mod 16)
         uint8_t* dst = pinned ? h + bb * E : x.hs;
+        zs3k::RowSet rset{};
+        for (int j = 0; j < R; ++j)
+            if (anyr[(size_t)j]) rset.row[rset.n++] = j;
+        uint8_t* ddst = nullptr;  // dst as the kernel addresses it
+        if (!rows2d) {
+            uint8_t* base = pinned ? h_dev : x.hs_dev;
+            if (base) ddst = base + (pinned ? bb * E : 0);
+        }
+        const bool rows_kernel = ddst && ((((uintptr_t)ddst - (uintptr_t)x.d)) & 15) == 0;
         for (const auto& rn : runs) {
             const int64_t r0 = rn.first, rl = rn.second;
             if (rows2d) {
@@ -1326,29 +1360,38 @@ int stream_vr_range(zs3_codec* c, uint8_t* h, int64_t nblk, const uint8_t* prese
                     if (anyr[(size_t)j])
                         chk(hipMemcpy2DAsync(dst + r0 * E + (size_t)j * S, (size_t)E, x.d + r0 * E + (size_t)j * S,
                                              (size_t)E, (size_t)S, (size_t)rl, hipMemcpyDeviceToHost, s_out));
+            } else if (rows_kernel) {
+                chk(zs3k::launch_rows_copy(x.d + r0 * E, ddst + r0 * E, E, S, rl, rset, s_out));
             } else {
                 chk(hipMemcpyAsync(dst + r0 * E, x.d + r0 * E, (size_t)(rl * E), hipMemcpyDeviceToHost, s_out));
             }
         }
-        if (h_bad)
-            chk(hipMemcpyAsync(h_bad + bb * R, x.d + off_bad, (size_t)nb * R * 4, hipMemcpyDeviceToHost, s_out));
+        if (h_bad) chk(hipMemcpyAsync(x.hsm + sm_bad, x.d + off_bad, (size_t)nb * R * 4, hipMemcpyDeviceToHost, s_out));
         if (hash_out)
-            chk(hipMemcpyAsync(h_sums_out + bb * R * 32, x.d + off_out, (size_t)nb * R * 32, hipMemcpyDeviceToHost, s_out));
+            chk(hipMemcpyAsync(x.hsm + sm_out, x.d + off_out, (size_t)nb * R * 32, hipMemcpyDeviceToHost, s_out));
         chk(hipEventRecord(x.out_done, s_out));
         x.used = true;
-        if (!pinned) {
-            // the rebuilt rows of each block from the staging into the caller's stripes
+        {
+            // after the batch's D2H: flags and heal sums to the caller's arrays, and (pageable
+            // stripes) the rebuilt rows of each served block from the staging
             hipEvent_t done = x.out_done;
-            uint8_t* hs = x.hs;
-            std::vector<uint8_t> pres(present + bb * R, present + (bb + nb) * R);
-            std::vector<uint8_t> served((size_t)nb);
-            for (int64_t b = 0; b < nb; ++b) served[(size_t)b] = st_b[b] == 0;
+            uint8_t* hs = pinned ? nullptr : x.hs;
+            const uint8_t* hsm = x.hsm;
+            std::vector<uint8_t> pres, served;
+            if (!pinned) {
+                pres.assign(present + bb * R, present + (bb + nb) * R);
+                served.resize((size_t)nb);
+                for (int64_t b = 0; b < nb; ++b) served[(size_t)b] = st_b[b] == 0;
+            }
             x.drain = std::async(std::launch::async, [=]() -> int {
                 if (hipEventSynchronize(done) != hipSuccess) return ZS3_ERR_DEVICE;
-                for (int64_t b = 0; b < nb; ++b)
-                    for (int j = 0; j < R; ++j)
-                        if (served[(size_t)b] && !pres[(size_t)(b * R + j)] && (j < k || heal))
-                            std::memcpy(h + (bb + b) * E + (size_t)j * S, hs + b * E + (size_t)j * S, (size_t)S);
+                if (h_bad) std::memcpy(h_bad + bb * R, hsm + sm_bad, (size_t)nb * R * 4);
+                if (hash_out) std::memcpy(h_sums_out + bb * R * 32, hsm + sm_out, (size_t)nb * R * 32);
+                if (hs)
+                    for (int64_t b = 0; b < nb; ++b)
+                        for (int j = 0; j < R; ++j)
+                            if (served[(size_t)b] && !pres[(size_t)(b * R + j)] && (j < k || heal))
+                                std::memcpy(h + (bb + b) * E + (size_t)j * S, hs + b * E + (size_t)j * S, (size_t)S);
                 return ZS3_OK;
             });
         }
@@ -1364,6 +1407,7 @@ int stream_vr_range(zs3_codec* c, uint8_t* h, int64_t nblk, const uint8_t* prese
     for (auto& x : sl) {
         pool_put(false, x.d, dbytes);
         pool_put(true, x.hs, (size_t)NB * E);
+        pool_put(true, x.hsm, smbytes);
         if (x.in_done) (void)hipEventDestroy(x.in_done);
         if (x.out_done) (void)hipEventDestroy(x.out_done);
     }

@@ -511,19 +511,21 @@ def gpu_devices() -> list:
 # (cmd/erasure-encode.go:83-111, cmd/erasure-decode.go:230-276, klauspost/reedsolomon +
 # HighwayHash).  Through the queue a block costs a PCIe round trip plus batching, so the
 # device only wins once enough requests are in flight.  Device side (tools/queue_bench,
-# profiles/r06/queue_split.jsonl, RS(8+4) 1 MiB encode + sums, synchronous submitters,
-# split copy streams): a lone block takes QUEUE_LONE_S (p50 306-310 us pinned; GET / heal
-# 527 us) and the queue saturates at QUEUE_MAX_BPS per device (37-44
-# GiB/s at 256 submitters); with T submitters Little's law gives
-# T*B / (lone + (T-1)*B/max): 23.2 / 33.9 / 38.3 GiB/s at T = 16 / 64 / 256 against
-# 23.6 / 35.6 / 38.4 measured.  Host side: one core runs one
+# profiles/r06/queue_product.jsonl, queue_product2.jsonl: RS(8+4) 1 MiB encode + sums,
+# synchronous submitters, split copy streams, seal point 33 %): a lone block takes
+# QUEUE_LONE_S (p50 305-310 us pinned; GET / heal 527 us) and the queue
+# approaches QUEUE_MAX_BPS per device; with T submitters Little's law gives
+# T*B / (lone + (T-1)*B/max): 23.9 / 35.3 GiB/s at T = 16 / 64 against 22.3 / 40.3-42.9
+# measured (256 submitters: modelled 40.1, measured 30-41: there the box's 16-core share
+# runs 256 submitter threads and the device waits for the host).  The model undershoots
+# the 64-submitter rate: it keeps a block on the host a little longer, never shorter.  Host side: one core runs one
 # block at CPU_CORE_BPS (oracle/cpu_ref.cpp, the reference's AVX-512 GFNI + AVX2 structure,
 # BENCH_r05 cpu_baseline.t1: 5.35 GiB/s encode + sums; heal 6.4, §13.4), so T requests on
 # `host_cores` cores run at min(T, host_cores) x that.
 QUEUE_LONE_S = {"encode": 306e-6, "get": 527e-6, "heal": 527e-6}   # 1 MiB RS(8+4) block
 QUEUE_LONE_BYTES = 1 << 20
 QUEUE_FIXED_S = 240e-6               # the part of a lone block that does not scale with its size
-QUEUE_MAX_BPS = 40 * 2**30           # per device (one PCIe x16 link), profiles/r06/queue_split.jsonl
+QUEUE_MAX_BPS = 42 * 2**30           # per device (one PCIe x16 link), profiles/r06/queue_product*.jsonl
 CPU_CORE_BPS = {"encode": 5.35 * 2**30, "get": 6.4 * 2**30, "heal": 6.4 * 2**30}
 
 
@@ -551,8 +553,8 @@ def codec_on_device(op: str, live: int, block_bytes: int, host_cores: int, devic
     goroutine.  `host_cores` = cores the server lets erasure coding use.  A lone 1 MiB
     request stays on the host (306-527 us through the device against ~190 us on one core);
     the device takes over once the queue's modelled rate beats min(live, host_cores) cores
-    — with a whole 16-core host budget that is never on one GPU (37-44 GiB/s against 86),
-    with 2 cores from 5 encode submitters, with 4 from 14.  (Legacy 10 MiB blocks: the
+    — with a whole 16-core host budget that is never on one GPU (30-43 GiB/s against 86),
+    with 2 cores from 5 encode submitters, with 4 from 13.  (Legacy 10 MiB blocks: the
     lone-block time is extrapolated from the 1 MiB measurement — fixed 240 us + the rest
     scaled by size — and puts even a lone 10 MiB block on the device.)  Monotone: more
     live requests never move a block back to the host, more host cores never move one to

@@ -210,6 +210,8 @@ struct EncShape {
     static constexpr bool HF = true;     // quad-form hash role: fused packet runs (hh_update_n)
     static constexpr bool HF2 = false;   // pair-form hash role: fused packet runs (hh2_update_n)
     static constexpr int ALN = 0;        // UA: realign in registers for S % 16 == ALN (below)
+    static constexpr int STG = 0;        // start stagger: workgroup w waits (w % STG) * SLP * 64 cycles
+    static constexpr int SLP = 0;
 };
 
 // workgroup -> stripe group (XMAP above k_ehx_ws); a bijection on [0, gridDim.x)
@@ -297,6 +299,12 @@ __attribute__((amdgpu_waves_per_eu(C::WPE))) k_ehx_ws(EncArgs a) {
     const int tid = threadIdx.x;
     const int64_t blk0 = (int64_t)ws_group<C::XMAP>() * G;
     const int64_t S = a.S;
+    if constexpr (C::STG > 1) {
+        // start stagger (round 6, diagnostics): the workgroups of one launch wave otherwise
+        // walk the same row offsets of their stripes in lockstep
+        const int ph = (int)(blockIdx.x % C::STG);
+        for (int i = 0; i < ph; ++i) __builtin_amdgcn_s_sleep(C::SLP);
+    }
     for (int i = tid; i < NTAB; i += NT) tabs[i] = GEN ? a.tables[i] : a.dtables[i];
     if (RING && tid < 4) ring[tid] = 0;
     const int64_t nfull = S / T;

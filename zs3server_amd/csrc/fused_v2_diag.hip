@@ -67,6 +67,11 @@ template <class S>
 struct Stamp : S {
     static constexpr bool WT = true;
 };
+// round 6: start stagger of the workgroups (STG phases of SLP * 64 cycles)
+template <class S, int STG_, int SLP_>
+struct Stg : S {
+    static constexpr int STG = STG_, SLP = SLP_;
+};
 }  // namespace shape
 
 bool launch_ehx_diag(int v, const EncArgs& a, hipStream_t s) {
@@ -114,6 +119,9 @@ bool launch_ehx_diag(int v, const EncArgs& a, hipStream_t s) {
             case 482: return launch_ws<8, 4, Hf0<Rs84Mid>>(a, s);
             case 483: return launch_ws<8, 4, Hf2<Rs84Bulk>>(a, s);  // pair-form fused packet runs
             case 474: return launch_ws<8, 4, Pm<Rs84Bulk, 4>>(a, s);  // progress-equalising priority
+            case 487: return launch_ws<8, 4, Stg<Rs84Bulk, 8, 17>>(a, s);   // 8 phases, ~1/8 step apart
+            case 488: return launch_ws<8, 4, Stg<Rs84Bulk, 4, 34>>(a, s);   // 4 phases, ~1/4 step apart
+            case 489: return launch_ws<8, 4, Stg<Rs84Bulk, 16, 120>>(a, s); // 16 phases, ~0.9 step apart
             default: return false;
         }
     }

@@ -67,6 +67,12 @@ template <class S>
 struct Stamp : S {
     static constexpr bool WT = true;
 };
+// round 6: 32 stripes of 128-byte tiles: 12 pair-form hash waves + 4 encode waves, so
+// every SIMD of the 16-wave workgroup holds three hash waves and one encode wave (the
+// 12-wave product puts 2 hash + 1 encode on two SIMDs and 1 + 2 on the others, §14.1)
+struct Rs84G32 : Rs84Bulk {
+    static constexpr int G = 32, T = 128, WPE = 4;
+};
 // round 6: start stagger of the workgroups (STG phases of SLP * 64 cycles)
 template <class S, int STG_, int SLP_>
 struct Stg : S {
@@ -119,6 +125,9 @@ bool launch_ehx_diag(int v, const EncArgs& a, hipStream_t s) {
             case 482: return launch_ws<8, 4, Hf0<Rs84Mid>>(a, s);
             case 483: return launch_ws<8, 4, Hf2<Rs84Bulk>>(a, s);  // pair-form fused packet runs
             case 474: return launch_ws<8, 4, Pm<Rs84Bulk, 4>>(a, s);  // progress-equalising priority
+            case 490: return launch_ws<8, 4, Rs84G32>(a, s);
+            case 491: return launch_ws<8, 4, Pm<Rs84G32, 0>>(a, s);
+            case 492: return launch_ws<8, 4, Stamp<Rs84G32>>(a, s);
             case 487: return launch_ws<8, 4, Stg<Rs84Bulk, 8, 17>>(a, s);   // 8 phases, ~1/8 step apart
             case 488: return launch_ws<8, 4, Stg<Rs84Bulk, 4, 34>>(a, s);   // 4 phases, ~1/4 step apart
             case 489: return launch_ws<8, 4, Stg<Rs84Bulk, 16, 120>>(a, s); // 16 phases, ~0.9 step apart

@@ -125,6 +125,8 @@ bool launch_ehx_diag(int v, const EncArgs& a, hipStream_t s) {
             case 482: return launch_ws<8, 4, Hf0<Rs84Mid>>(a, s);
             case 483: return launch_ws<8, 4, Hf2<Rs84Bulk>>(a, s);  // pair-form fused packet runs
             case 474: return launch_ws<8, 4, Pm<Rs84Bulk, 4>>(a, s);  // progress-equalising priority
+            case 494: return launch_ws<8, 4, Rs84Mid>(a, s);               // the <= 2048-stripe shape
+            case 495: return launch_ws<8, 4, XMap<Rs84Mid, 8>>(a, s);
             case 490: return launch_ws<8, 4, Rs84G32>(a, s);
             case 491: return launch_ws<8, 4, Pm<Rs84G32, 0>>(a, s);
             case 492: return launch_ws<8, 4, Stamp<Rs84G32>>(a, s);

@@ -316,3 +316,38 @@ def test_stream_encode_argument_checks():
         with pytest.raises(ValueError):
             call(src.reshape(2, -1)[:, ::2], MiB // 2, par, sums)  # strided source
     assert c.stream_encode(src, 2 * MiB, par, sums) == 2
+
+
+@pytest.mark.parametrize("pinned", [False, True], ids=["pageable", "pinned"])
+def test_stream_decode_many_rebuilt_rows(oracle, pinned):
+    """RS(30+6) on 1 MiB blocks (S = 34 953, rows not 256-byte aligned): the rebuilt rows go
+    back by k_rows_copy while a batch's union of lost rows fits its 32-row list (blocks 0-7
+    lose rows 0-5) and as whole stripes when it does not (blocks 8-23 each lose 6 rows of a
+    rotating set: 36 distinct rows per batch).  Heal: every lost row rebuilt and hashed."""
+    k, m, nfull = 30, 6, 24
+    R = k + m
+    ref, sums, S, _ = make_object(oracle, k, m, nfull, 0, seed=3006)
+    E = R * S
+    present = np.ones((nfull, R), bool)
+    present[:8, 0:6] = False
+    for b in range(8, nfull):
+        present[b, [(b * 6 + i) % R for i in range(6)]] = False
+    work_h = z.HostBuffer(nfull * E) if pinned else None
+    work = work_h.array if pinned else np.empty(nfull * E, np.uint8)
+    work[:] = ref
+    for b in range(nfull):
+        rows(work, b, E, S, R)[~present[b]] = 0x5A
+    out = np.zeros((nfull, R, 32), np.uint8)
+    bad = np.full((nfull, R), 9, np.int32)
+    try:
+        n = z.Codec(k, m, MiB).stream_decode(work_h if pinned else work, nfull * MiB, present, False, expect=sums,
+                                             bad=bad, sums_out=out, batch_blocks=8)
+        assert n == nfull
+        assert not bad.any()
+        assert np.array_equal(work, ref)
+        for b in range(nfull):
+            for j in np.nonzero(~present[b])[0]:
+                assert np.array_equal(out[b, j], sums[b, j]), (b, j)
+    finally:
+        if work_h is not None:
+            work_h.free()

@@ -1345,10 +1345,13 @@ int stream_vr_range(zs3_codec* c, uint8_t* h, int64_t nblk, const uint8_t* prese
         // congruent mod 16)
         uint8_t* dst = pinned ? h + bb * E : x.hs;
         zs3k::RowSet rset{};
-        for (int j = 0; j < R; ++j)
-            if (anyr[(size_t)j]) rset.row[rset.n++] = j;
+        int nrb = 0;  // rebuilt row indices of the batch (k_rows_copy takes up to 32)
+        for (int j = 0; j < R; ++j) nrb += anyr[(size_t)j] ? 1 : 0;
+        if (nrb <= 32)
+            for (int j = 0; j < R; ++j)
+                if (anyr[(size_t)j]) rset.row[rset.n++] = j;
         uint8_t* ddst = nullptr;  // dst as the kernel addresses it
-        if (!rows2d) {
+        if (!rows2d && nrb <= 32) {
             uint8_t* base = pinned ? h_dev : x.hs_dev;
             if (base) ddst = base + (pinned ? bb * E : 0);
         }

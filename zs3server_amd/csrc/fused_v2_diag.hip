@@ -73,6 +73,9 @@ struct Stamp : S {
 struct Rs84G32 : Rs84Bulk {
     static constexpr int G = 32, T = 128, WPE = 4;
 };
+struct Rs124Ua1K8 : Rs124Ua1K {
+    static constexpr int CWX = 8, WPE = 3;
+};
 // round 6: start stagger of the workgroups (STG phases of SLP * 64 cycles)
 template <class S, int STG_, int SLP_>
 struct Stg : S {
@@ -159,6 +162,11 @@ bool launch_ehx_diag(int v, const EncArgs& a, hipStream_t s) {
     if (a.k == 12 && a.m == 4 && v == 484) return launch_ws<12, 4, Stamp<Rs124Ua1K>>(a, s);  // per-wave stamps
     if (a.k == 12 && a.m == 4 && v == 485) return launch_ws<12, 4, Rs124Aln>(a, s);
     if (a.k == 12 && a.m == 4 && v == 486) return launch_ws<12, 4, Stamp<Rs124Aln>>(a, s);
+    // two encode waves per SIMD (8-byte columns: 8 encode + 4 hash waves, the 168-VGPR
+    // budget) instead of one; and the aligned-row shape (8 stripes of 512) on these rows
+    if (a.k == 12 && a.m == 4 && v == 496) return launch_ws<12, 4, Rs124Ua1K8>(a, s);
+    if (a.k == 12 && a.m == 4 && v == 497) return launch_ws<12, 4, Stamp<Rs124Ua1K8>>(a, s);
+    if (a.k == 12 && a.m == 4 && v == 498) return launch_ws<12, 4, XMap<Rs124AlignedBulk, 8>>(a, s);
     if (v == 419) return launch_ehx_gen_xmap(a, s);
     return false;
 }

@@ -304,7 +304,9 @@ void zs3_split_range(int64_t total, int world, int rank, int64_t* lo, int64_t* h
  * (cmd/erasure-encode.go:83-111, cmd/erasure-decode.go:230-276); one block is far too
  * little work for one device round trip.  A queue gathers the blocks that concurrent
  * callers (OS threads: every goroutine inside cgo holds one) submit into device
- * batches on pinned staging slots, each slot with its own stream:
+ * batches on pinned staging slots; a batch's H2D copies run on its lane's H2D stream,
+ * its kernels on its slot's stream and its D2H copies on the lane's D2H stream, so one
+ * batch's results come back while the next batch goes in:
  *   - a block is copied into the queue's pinned staging by its submitting thread, or,
  *     when the caller's buffer lies inside a zs3_host_alloc allocation (the pinned
  *     bpool), holds a full-size block, opens its batch and no other batch of its lane
@@ -314,9 +316,10 @@ void zs3_split_range(int64_t total, int world, int rank, int64_t* lo, int64_t* h
  *     fast;
  *   - a batch is launched when it is full, when fewer than slots-1 batches of its lane
  *     are in flight (batch while busy), when its oldest block has waited max_wait_us,
- *     or on flush; it is sealed — later blocks open the next batch — once it holds half
- *     of its lane's live blocks (at least 8), so that with T synchronous callers two
- *     batches of ~T/2 alternate and overlap their copies.  A batch holds at most
+ *     or on flush; it is sealed — later blocks open the next batch — once it holds a
+ *     third of its lane's live blocks on that device (submitted and not finished,
+ *     callers waiting for a slot included; at least 8), so that with T synchronous
+ *     callers three batches of ~T/3 overlap their copies and kernels.  A batch holds at most
  *     max(8, 64 MiB / blockSize) blocks (at most 512, and at most max_batch when set):
  *     the staging slots are sized to exactly that;
  *   - several devices (opts.devices): every device has its own slots, streams and

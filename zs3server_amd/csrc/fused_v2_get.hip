@@ -41,8 +41,8 @@ static bool launch_vr_ws_default(const VrArgs& a, hipStream_t s) {
         // rebuild 4 / heal 4 (round 5): the rebuild split over survivor quads, each wave's
         // 16 coefficient tables held for the launch (vr_quad.hpp; 4-5 % over the k_vr_ws
         // instances below, which serve every other batch; diagnostics 440 = those instead)
-        if (a.e == 4 && !(ZS3_DIAG && (a.variant == 440 || (a.variant >= 442 && a.variant <= 445))) &&
-            launch_vr_quad<shape::Quad16>(a, s)) {
+        if (a.e == 4 && !(ZS3_DIAG && (a.variant == 440 || (a.variant >= 442 && a.variant <= 447))) &&
+            launch_vr_quad_product(a, s)) {
             note_kernel(KERNEL_VR_QUAD);
             return true;
         }
@@ -51,6 +51,9 @@ static bool launch_vr_ws_default(const VrArgs& a, hipStream_t s) {
         if (a.variant == 443 && a.e == 4 && launch_vr_quad<shape::Quad16LateRead>(a, s)) return note_kernel(KERNEL_VR_QUAD), true;
         if (a.variant == 444 && a.e == 4 && launch_vr_quad<shape::Quad16OneArray>(a, s)) return note_kernel(KERNEL_VR_QUAD), true;
         if (a.variant == 445 && a.e == 4 && launch_vr_quad<shape::Quad16NoSwz>(a, s)) return note_kernel(KERNEL_VR_QUAD), true;
+        // 446: both instances on Quad16 (heal in the linear workgroup order of round 5)
+        if (a.variant == 446 && a.e == 4 && launch_vr_quad<shape::Quad16>(a, s)) return note_kernel(KERNEL_VR_QUAD), true;
+        if (a.variant == 447 && a.e == 4 && launch_vr_quad<shape::Quad16P2>(a, s)) return note_kernel(KERNEL_VR_QUAD), true;
 #endif
         if (!heal) {
             // verify only: 8 stripes, 256-byte tiles, two tiles of survivor prefetch.

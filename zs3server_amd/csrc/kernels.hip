@@ -1516,7 +1516,7 @@ static hipError_t run_vr(const VrArgs& a, hipStream_t s) {
 static bool product_get_variant(int v) {
     return v == 0 || (ZS3_DIAG && (v == 246 || v == 247 || v == 420 || v == 423 || v == 424 || v == 429 ||
                           v == 431 || v == 433 || v == 434 || v == 440 || v == 442 || v == 443 || v == 444 ||
-                          v == 445));
+                          v == 445 || v == 446 || v == 447));
 }
 
 // GET / heal small-batch path: k_reconstruct rebuilds the missing rows, then one chain

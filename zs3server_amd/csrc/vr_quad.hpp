@@ -64,6 +64,16 @@ struct Quad16LateRead : Quad16 {
 struct Quad16Prio0 : Quad16 {
     static constexpr int PRIO = 0;
 };
+// The heal instance with the XCD-region workgroup order over 8 regions (round 6: heal 4
+// 1-4 % faster at 2 048 / 8 192 x 1 MiB, rebuild 4 within noise either way, diagnostics
+// 446 = without; profiles/r06/ab_quad_x8.jsonl).
+struct Quad16Heal : Quad16 {
+    static constexpr int XMAP = 8;
+};
+// Diagnostics (round 6): issue priority 2 for the rebuild quads.
+struct Quad16P2 : Quad16 {
+    static constexpr int PRIO = 2;
+};
 }  // namespace shape
 
 template <bool HOUT, class C>
@@ -313,6 +323,11 @@ static bool launch_vr_quad_t(const VrArgs& a, hipStream_t s) {
 template <class C = shape::Quad16>
 static bool launch_vr_quad(const VrArgs& a, hipStream_t s) {
     return a.sums_out ? launch_vr_quad_t<true, C>(a, s) : launch_vr_quad_t<false, C>(a, s);
+}
+
+// The product instances: rebuild 4 on Quad16, heal 4 on Quad16Heal.
+static bool launch_vr_quad_product(const VrArgs& a, hipStream_t s) {
+    return a.sums_out ? launch_vr_quad_t<true, shape::Quad16Heal>(a, s) : launch_vr_quad_t<false, shape::Quad16>(a, s);
 }
 
 }  // namespace zs3k

@@ -151,6 +151,7 @@ bool launch_ehx_diag(int v, const EncArgs& a, hipStream_t s) {
     if (a.k == 16 && a.m == 4) {
         switch (v) {
             case 401: return launch_ws<16, 4, XMap<Rs164Bulk, 0>>(a, s);
+            case 499: return launch_ws<16, 4, Stamp<Rs164Bulk>>(a, s);  // per-wave stamps
             case 415: return launch_ws<16, 4, Tsp0<Rs164Bulk>>(a, s);
             case 417: return launch_ws<16, 4, XMap<Tsp0<Rs164Bulk>, 0>>(a, s);
             case 403: return launch_ws<16, 4, Pm<Rs164Bulk, 0>>(a, s);

@@ -73,6 +73,10 @@ struct Stamp : S {
 struct Rs84G32 : Rs84Bulk {
     static constexpr int G = 32, T = 128, WPE = 4;
 };
+template <class S, int N>
+struct Ntm : S {
+    static constexpr int NTM = N;
+};
 struct Rs124Ua1K8 : Rs124Ua1K {
     static constexpr int CWX = 8, WPE = 3;
 };
@@ -168,6 +172,10 @@ bool launch_ehx_diag(int v, const EncArgs& a, hipStream_t s) {
     if (a.k == 12 && a.m == 4 && v == 496) return launch_ws<12, 4, Rs124Ua1K8>(a, s);
     if (a.k == 12 && a.m == 4 && v == 497) return launch_ws<12, 4, Stamp<Rs124Ua1K8>>(a, s);
     if (a.k == 12 && a.m == 4 && v == 498) return launch_ws<12, 4, XMap<Rs124AlignedBulk, 8>>(a, s);
+    // memory policy: temporal data loads (NTM 2: only the parity stores non-temporal), all
+    // temporal (0): do the non-temporal data loads evict the tiles' shared edge lines?
+    if (a.k == 12 && a.m == 4 && v == 500) return launch_ws<12, 4, Ntm<Rs124Ua1K, 2>>(a, s);
+    if (a.k == 12 && a.m == 4 && v == 501) return launch_ws<12, 4, Ntm<Rs124Ua1K, 0>>(a, s);
     if (v == 419) return launch_ehx_gen_xmap(a, s);
     return false;
 }

@@ -212,6 +212,7 @@ struct EncShape {
     static constexpr int ALN = 0;        // UA: realign in registers for S % 16 == ALN (below)
     static constexpr int STG = 0;        // start stagger: workgroup w waits (w % STG) * SLP * 64 cycles
     static constexpr int SLP = 0;
+    static constexpr bool PFE = false;   // quad-form PFD: re-touch each data row's next-tile edge line
 };
 
 // workgroup -> stripe group (XMAP above k_ehx_ws); a bijection on [0, gridDim.x)
@@ -368,6 +369,16 @@ __attribute__((amdgpu_waves_per_eu(C::WPE))) k_ehx_ws(EncArgs a) {
                 pfa[q] = a.data + b * a.data_stride + (int64_t)j * S + (li % LPR) * 128;
             }
         }
+        // PFE (round 6, diagnostics): thread r < G*K re-touches the first byte of data row r's
+        // next tile (the line it shares with the current tile when rows are unaligned) with a
+        // temporal load in each step, after the encode's non-temporal load of the current
+        // tile has marked that line for early eviction
+        const uint8_t* pfe = nullptr;
+        if constexpr (PFD > 0 && C::PFE) {
+            const int r = tid < G * K ? tid : 0, g = r / K, j = r % K;
+            const int64_t b = (blk0 + g) < a.n_blocks ? (blk0 + g) : (a.n_blocks - 1);
+            pfe = a.data + b * a.data_stride + (int64_t)j * S;
+        }
         bar();  // tables (matches the encode role)
         bar();  // step 0: tile 0 being encoded
         for (int64_t s = 1; s <= nfull; ++s) {
@@ -376,6 +387,10 @@ __attribute__((amdgpu_waves_per_eu(C::WPE))) k_ehx_ws(EncArgs a) {
 #pragma unroll
                     for (int q = 0; q < NPL; ++q)
                         asm volatile("global_load_dword %0, %1, off" : "+v"(sink) : "v"(pfa[q] + (s + PFD) * T));
+                }
+                if constexpr (C::PFE) {
+                    if (tid < G * K && s + 1 < nfull)
+                        asm volatile("global_load_dword %0, %1, off" : "+v"(sink) : "v"(pfe + (s + 1) * T));
                 }
             }
             const uint64_t* p = reinterpret_cast<const uint64_t*>(tile[(s - 1) & 1] + row_off);

@@ -81,6 +81,9 @@ template <class S, int N>
 struct Pfd : S {
     static constexpr int PFD = N;
 };
+struct Rs124Pfe : Rs124Ua1K {
+    static constexpr bool PFE = true;
+};
 struct Rs124Ua1K8 : Rs124Ua1K {
     static constexpr int CWX = 8, WPE = 3;
 };
@@ -183,6 +186,7 @@ bool launch_ehx_diag(int v, const EncArgs& a, hipStream_t s) {
     // L2 prefetch one tile ahead (in flight per XCD: 32 CUs x 2 tiles x 48 KiB = 3 MiB of its
     // 4 MiB L2, against 4.5 MiB at two tiles ahead)
     if (a.k == 12 && a.m == 4 && v == 502) return launch_ws<12, 4, Pfd<Rs124Ua1K, 1>>(a, s);
+    if (a.k == 12 && a.m == 4 && v == 503) return launch_ws<12, 4, Rs124Pfe>(a, s);   // edge-line re-touch
     if (v == 419) return launch_ehx_gen_xmap(a, s);
     return false;
 }

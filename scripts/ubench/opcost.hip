@@ -32,6 +32,8 @@ __global__ void __launch_bounds__(256) k(uint32_t* out, uint64_t* clk, uint32_t 
             if constexpr (OP == 9) { uint32_t r; asm volatile("v_add_u32 %0, %1, %2" : "=v"(r) : "v"(a[i]), "v"(a[(i+1)&7])); a[i] = r; }
             if constexpr (OP == 10) { uint32_t r; asm volatile("v_mul_lo_u32 %0, %1, %2" : "=v"(r) : "v"(a[i]), "v"(a[(i+1)&7])); a[i] = r; }
             if constexpr (OP == 11) { uint32_t r; asm volatile("v_alignbit_b32 %0, %1, %2, 8" : "=v"(r) : "v"(a[i]), "v"(a[(i+1)&7])); a[i] = r; }
+            if constexpr (OP == 12) { uint64_t r; asm volatile("v_lshrrev_b64 %0, 3, %1" : "=v"(r) : "v"(q[(i+1)&7])); q[i] = r ^ q[i]; }
+            if constexpr (OP == 13) { uint64_t r; asm volatile("v_lshrrev_b64 %0, 3, %1" : "=v"(r) : "v"(q[(i+1)&7])); q[i] = r; }
         }
     }
     uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
@@ -83,6 +85,8 @@ int main() {
         run<9>("v_add_u32", d, clk, cus, w);
         run<10>("v_mul_lo_u32", d, clk, cus, w);
         run<11>("v_alignbit_b32", d, clk, cus, w);
+        run<12>("lshr_b64+xor64", d, clk, cus, w);
+        run<13>("v_lshrrev_b64", d, clk, cus, w);
     }
     return 0;
 }

@@ -213,6 +213,7 @@ struct EncShape {
     static constexpr int STG = 0;        // start stagger: workgroup w waits (w % STG) * SLP * 64 cycles
     static constexpr int SLP = 0;
     static constexpr bool PFE = false;   // quad-form PFD: re-touch each data row's next-tile edge line
+    static constexpr bool S64 = false;   // dyadic encode: nibble splits of dword pairs by 64-bit shifts
 };
 
 // workgroup -> stripe group (XMAP above k_ehx_ws); a bijection on [0, gridDim.x)
@@ -711,7 +712,7 @@ __attribute__((amdgpu_waves_per_eu(C::WPE))) k_ehx_ws(EncArgs a) {
                 [&](int j) { return xs[j]; }, par, tabs, nullptr, NoHook{}, ptab);
         } else if constexpr (EP == 2) {
             // data rows written right after the first block's table reads
-            encode_dyadic_f<NWd, K, M, true, false, STB>(
+            encode_dyadic_f<NWd, K, M, true, false, STB, false, C::S64>(
                 [&](int j) { return xs[j]; }, par, tabs, const_tables(a.dtables), [&]() {
 #pragma unroll
                     for (int j = 0; j < K; ++j) st_col<NWd>(tl + col_off + j * TS, xs[j]);
@@ -722,7 +723,7 @@ __attribute__((amdgpu_waves_per_eu(C::WPE))) k_ehx_ws(EncArgs a) {
             __builtin_amdgcn_sched_barrier(0);
             __builtin_amdgcn_s_setprio(K / M >= 3 ? 0 : 1);
         } else {
-            encode_dyadic<NWd, K, M, true, false, STB>(xs, par, tabs, const_tables(a.dtables));
+            encode_dyadic<NWd, K, M, true, false, STB, C::S64>(xs, par, tabs, const_tables(a.dtables));
         }
         if constexpr (ABL & 4) {
             // timing ablation: no LDS writes (the hash waves read stale tiles)
@@ -1642,15 +1643,19 @@ struct PairG16 : EncShape {
 // RS(8+4) above 2048 stripes (the BASELINE config-4 bench): PairG16 with buffer-addressed
 // columns and the conflict-free LDS row stride (round 4), and the region-interleaved
 // workgroup order over 8 regions (round 5: each XCD walks its own eighth of the batch;
-// 65 536 x 1 MiB 19.52 -> 18.77 ms, profiles/r05/xmap84.jsonl).
+// 65 536 x 1 MiB 19.52 -> 18.77 ms, profiles/r05/xmap84.jsonl); round 6: the nibble
+// splits of dword pairs by 64-bit shifts (S64: 65 536 x 1 MiB 18.58-18.68 -> 18.20-18.27
+// ms, profiles/r06/ab_split64.jsonl).
 struct Rs84Bulk : PairG16 {
-    static constexpr bool BUF = true;
+    static constexpr bool BUF = true, S64 = true;
     static constexpr int TSP = 1, XMAP = 8;
 };
 // RS(4+4) above 2048 stripes: PairG16 with the conflict-free LDS row stride (round 5:
-// 4 096 / 16 384 x 1 MiB 1.78-1.83 / 7.09-7.14 ms either way, bank conflicts 20 % -> 0).
+// 4 096 / 16 384 x 1 MiB 1.78-1.83 / 7.09-7.14 ms either way, bank conflicts 20 % -> 0);
+// round 6: S64 (16 384: 7.10-7.14 -> 7.07-7.09 ms, profiles/r06/ab_split64b.jsonl).
 struct Rs44Bulk : PairG16 {
     static constexpr int TSP = 1;
+    static constexpr bool S64 = true;
 };
 // RS(8+4) up to 2048 stripes: 4 stripes of 1 KiB tiles, quad-form hash waves, two tiles
 // of prefetch, one workgroup per CU (LDSMIN), the 256-VGPR budget.
@@ -1699,6 +1704,7 @@ struct Config2 : EncShape {
 struct Rs124Ua1K : EncShape {
     static constexpr int G = 4, T = 1024, CWX = 16, NTM = 3, EP = 2, PFD = 2, WPE = 2, TSP = 1, XMAP = 8;
     static constexpr bool BUF = true, HQ = true, UA = true;
+    static constexpr bool S64 = true;  // round 6: 16 384 x 1 MiB 5.43-5.45 -> 5.37-5.42 ms (ab_split64b.jsonl)
 };
 struct Rs124UaSmall : EncShape {
     static constexpr int G = 4, T = 512, NTM = 3;

@@ -45,6 +45,7 @@ struct Rs84Stamped : Rs84Bulk {
 };
 struct Rs84Pf2 : Rs84Bulk {
     static constexpr int PF = 2;
+    static constexpr bool S64 = false;  // (two tiles of registers + S64 spill)
 };
 struct Rs84Ep1 : Rs84Bulk {
     static constexpr int EP = 1;
@@ -80,6 +81,15 @@ struct Ntm : S {
 template <class S, int N>
 struct Pfd : S {
     static constexpr int PFD = N;
+};
+template <class S>
+struct Split64 : S {
+    static constexpr bool S64 = true;
+};
+// the product shapes without the 64-bit nibble splits (round 6 adopted S64 for them)
+template <class S>
+struct Split32 : S {
+    static constexpr bool S64 = false;
 };
 struct Rs124Pfe : Rs124Ua1K {
     static constexpr bool PFE = true;
@@ -141,6 +151,8 @@ bool launch_ehx_diag(int v, const EncArgs& a, hipStream_t s) {
             case 474: return launch_ws<8, 4, Pm<Rs84Bulk, 4>>(a, s);  // progress-equalising priority
             case 494: return launch_ws<8, 4, Rs84Mid>(a, s);               // the <= 2048-stripe shape
             case 495: return launch_ws<8, 4, XMap<Rs84Mid, 8>>(a, s);
+            case 504: return launch_ws<8, 4, Split32<Rs84Bulk>>(a, s);  // without the 64-bit nibble splits
+            case 507: return launch_ws<8, 4, Split64<Rs84Mid>>(a, s);
             case 490: return launch_ws<8, 4, Rs84G32>(a, s);
             case 491: return launch_ws<8, 4, Pm<Rs84G32, 0>>(a, s);
             case 492: return launch_ws<8, 4, Stamp<Rs84G32>>(a, s);
@@ -154,6 +166,7 @@ bool launch_ehx_diag(int v, const EncArgs& a, hipStream_t s) {
         switch (v) {
             case 400: return a.m == 4 && launch_ws<4, 4, PairG16>(a, s);
             case 402: return a.m == 4 && launch_ws<4, 4, Rs84Bulk>(a, s);
+            case 508: return a.m == 4 && launch_ws<4, 4, Split32<Rs44Bulk>>(a, s);
             case 418: return a.m == 4 ? launch_ws<4, 4, XMap<PairG16, 8>>(a, s) : launch_ws<4, 2, XMap<PairG16, 8>>(a, s);
             case 480: return a.m == 2 && launch_ws<4, 2, Hf0<Config2>>(a, s);  // config 2 without hh_update_n
             default: return false;
@@ -163,6 +176,7 @@ bool launch_ehx_diag(int v, const EncArgs& a, hipStream_t s) {
         switch (v) {
             case 401: return launch_ws<16, 4, XMap<Rs164Bulk, 0>>(a, s);
             case 499: return launch_ws<16, 4, Stamp<Rs164Bulk>>(a, s);  // per-wave stamps
+            case 505: return launch_ws<16, 4, Split64<Rs164Bulk>>(a, s);
             case 415: return launch_ws<16, 4, Tsp0<Rs164Bulk>>(a, s);
             case 417: return launch_ws<16, 4, XMap<Tsp0<Rs164Bulk>, 0>>(a, s);
             case 403: return launch_ws<16, 4, Pm<Rs164Bulk, 0>>(a, s);
@@ -187,6 +201,7 @@ bool launch_ehx_diag(int v, const EncArgs& a, hipStream_t s) {
     // 4 MiB L2, against 4.5 MiB at two tiles ahead)
     if (a.k == 12 && a.m == 4 && v == 502) return launch_ws<12, 4, Pfd<Rs124Ua1K, 1>>(a, s);
     if (a.k == 12 && a.m == 4 && v == 503) return launch_ws<12, 4, Rs124Pfe>(a, s);   // edge-line re-touch
+    if (a.k == 12 && a.m == 4 && v == 506) return launch_ws<12, 4, Split32<Rs124Ua1K>>(a, s);
     if (v == 419) return launch_ehx_gen_xmap(a, s);
     return false;
 }

@@ -36,6 +36,22 @@ __device__ __forceinline__ Nib split_nibbles(uint32_t x) {
     return n;
 }
 
+// Two dwords split with 64-bit shifts (round 6): v_lshrrev_b64 issues in ~4.5 cycles
+// where two v_lshrrev_b32 take ~5.5 (profiles/r06/opcost.txt); the high dword's bits that
+// the shift moves into the low one land above every kept field.
+__device__ __forceinline__ void split_nibbles2(uint32_t xlo, uint32_t xhi, Nib& lo, Nib& hi) {
+    const uint64_t x = ((uint64_t)xhi << 32) | xlo;
+    uint64_t t3, t6;  // (the compiler lowers a 64-bit shift to 32-bit ones: stated here)
+    asm("v_lshrrev_b64 %0, 3, %1" : "=v"(t3) : "v"(x));
+    asm("v_lshrrev_b64 %0, 6, %1" : "=v"(t6) : "v"(x));
+    lo.a = xlo & 0x07070707u;
+    hi.a = xhi & 0x07070707u;
+    lo.b = (uint32_t)t3 & 0x07070707u;
+    hi.b = (uint32_t)(t3 >> 32) & 0x07070707u;
+    lo.c = (uint32_t)t6 & 0x03030303u;
+    hi.c = (uint32_t)(t6 >> 32) & 0x03030303u;
+}
+
 // Coefficient tables as held in LDS: 8 dwords per coefficient (32 B aligned),
 // Ta.lo Ta.hi Tb.lo Tb.hi | Tc 0 0 0.
 struct CoefTab {
@@ -197,8 +213,8 @@ struct NoHook {
 };
 // PRE: the K coefficient tables were read once into registers (pre[0..K-1]) before the
 // tile loop: no LDS reads (and no LDS-counter waits) inside the encode.
-template <int NWd, int K, int M, bool SB = true, bool PRS = false, bool ST = false, bool PRE = false, typename XF,
-          typename H0 = NoHook>
+template <int NWd, int K, int M, bool SB = true, bool PRS = false, bool ST = false, bool PRE = false,
+          bool S64 = false, typename XF, typename H0 = NoHook>
 __device__ __forceinline__ void encode_dyadic_f(XF&& getx, Col<NWd> (&out)[M], const uint32_t* dtabs,
                                                 ctab_ptr ctabs = nullptr, H0&& hook0 = NoHook{},
                                                 const CoefTab* pre = nullptr) {
@@ -235,14 +251,47 @@ __device__ __forceinline__ void encode_dyadic_f(XF&& getx, Col<NWd> (&out)[M], c
             }
         }
         auto gf_lookup = [](const Nib& n, const CoefTab& c) { return ST ? gf_lookup_s(n, c) : zs3dev::gf_lookup(n, c); };
+        // S64: the four transformed inputs of dwords w and w+1 split together (split_nibbles2)
+        // when w is even; dword w+1 takes the split that w left in np[]
+        constexpr bool P64 = S64 && M == 4 && NWd % 2 == 0;
+        Nib np[4];
 #pragma unroll
         for (int w = 0; w < NWd; ++w) {
             if constexpr (M == 4) {
-                const uint32_t x3 = xb[3].w[w];
-                const uint32_t X1 = xb[1].w[w] ^ x3, X2 = xb[2].w[w] ^ x3;
-                const uint32_t X0 = xor3(xb[0].w[w], X1, xb[2].w[w]);
-                const Nib n0 = split_nibbles(X0), n1 = split_nibbles(X1);
-                const Nib n2 = split_nibbles(X2), n3 = split_nibbles(x3);
+                Nib n0, n1, n2, n3;
+                if constexpr (P64) {
+                    if (w % 2 == 0) {
+                        uint32_t Xs[2][4];
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) {
+                            const uint32_t x3 = xb[3].w[w + h];
+                            Xs[h][1] = xb[1].w[w + h] ^ x3;
+                            Xs[h][2] = xb[2].w[w + h] ^ x3;
+                            Xs[h][0] = xor3(xb[0].w[w + h], Xs[h][1], xb[2].w[w + h]);
+                            Xs[h][3] = x3;
+                        }
+                        Nib nl[4];
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) split_nibbles2(Xs[0][i], Xs[1][i], nl[i], np[i]);
+                        n0 = nl[0];
+                        n1 = nl[1];
+                        n2 = nl[2];
+                        n3 = nl[3];
+                    } else {
+                        n0 = np[0];
+                        n1 = np[1];
+                        n2 = np[2];
+                        n3 = np[3];
+                    }
+                } else {
+                    const uint32_t x3 = xb[3].w[w];
+                    const uint32_t X1 = xb[1].w[w] ^ x3, X2 = xb[2].w[w] ^ x3;
+                    const uint32_t X0 = xor3(xb[0].w[w], X1, xb[2].w[w]);
+                    n0 = split_nibbles(X0);
+                    n1 = split_nibbles(X1);
+                    n2 = split_nibbles(X2);
+                    n3 = split_nibbles(x3);
+                }
                 const Prod3 P00 = gf_lookup(n0, t[0]), P01 = gf_lookup(n1, t[0]);
                 const Prod3 P02 = gf_lookup(n2, t[0]), P03 = gf_lookup(n3, t[0]);
                 const Prod3 P10 = gf_lookup(n0, t[1]), P12 = gf_lookup(n2, t[1]);
@@ -290,10 +339,10 @@ __device__ __forceinline__ void encode_dyadic_f(XF&& getx, Col<NWd> (&out)[M], c
     }
 }
 
-template <int NWd, int K, int M, bool SB = true, bool PRS = false, bool ST = false>
+template <int NWd, int K, int M, bool SB = true, bool PRS = false, bool ST = false, bool S64 = false>
 __device__ __forceinline__ void encode_dyadic(const Col<NWd> (&x)[K], Col<NWd> (&out)[M], const uint32_t* dtabs,
                                               ctab_ptr ctabs = nullptr) {
-    encode_dyadic_f<NWd, K, M, SB, PRS, ST>([&](int j) { return x[j]; }, out, dtabs, ctabs);
+    encode_dyadic_f<NWd, K, M, SB, PRS, ST, false, S64>([&](int j) { return x[j]; }, out, dtabs, ctabs);
 }
 
 // General (non-dyadic) encode of one column: out[r] = sum_j M[r][j] * x[j] over GF(2^8),

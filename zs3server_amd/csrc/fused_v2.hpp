@@ -214,6 +214,7 @@ struct EncShape {
     static constexpr int SLP = 0;
     static constexpr bool PFE = false;   // quad-form PFD: re-touch each data row's next-tile edge line
     static constexpr bool S64 = false;   // dyadic encode: nibble splits of dword pairs by 64-bit shifts
+    static constexpr bool SMK = false;   // with S64: the split masks from SGPRs (diagnostics)
 };
 
 // workgroup -> stripe group (XMAP above k_ehx_ws); a bijection on [0, gridDim.x)
@@ -712,7 +713,7 @@ __attribute__((amdgpu_waves_per_eu(C::WPE))) k_ehx_ws(EncArgs a) {
                 [&](int j) { return xs[j]; }, par, tabs, nullptr, NoHook{}, ptab);
         } else if constexpr (EP == 2) {
             // data rows written right after the first block's table reads
-            encode_dyadic_f<NWd, K, M, true, false, STB, false, C::S64>(
+            encode_dyadic_f<NWd, K, M, true, false, STB, false, C::S64, C::SMK>(
                 [&](int j) { return xs[j]; }, par, tabs, const_tables(a.dtables), [&]() {
 #pragma unroll
                     for (int j = 0; j < K; ++j) st_col<NWd>(tl + col_off + j * TS, xs[j]);
@@ -723,7 +724,7 @@ __attribute__((amdgpu_waves_per_eu(C::WPE))) k_ehx_ws(EncArgs a) {
             __builtin_amdgcn_sched_barrier(0);
             __builtin_amdgcn_s_setprio(K / M >= 3 ? 0 : 1);
         } else {
-            encode_dyadic<NWd, K, M, true, false, STB, C::S64>(xs, par, tabs, const_tables(a.dtables));
+            encode_dyadic<NWd, K, M, true, false, STB, C::S64, C::SMK>(xs, par, tabs, const_tables(a.dtables));
         }
         if constexpr (ABL & 4) {
             // timing ablation: no LDS writes (the hash waves read stale tiles)

@@ -86,6 +86,10 @@ template <class S>
 struct Split64 : S {
     static constexpr bool S64 = true;
 };
+template <class S>
+struct Smk : S {
+    static constexpr bool SMK = true;
+};
 // the product shapes without the 64-bit nibble splits (round 6 adopted S64 for them)
 template <class S>
 struct Split32 : S {
@@ -153,6 +157,7 @@ bool launch_ehx_diag(int v, const EncArgs& a, hipStream_t s) {
             case 495: return launch_ws<8, 4, XMap<Rs84Mid, 8>>(a, s);
             case 504: return launch_ws<8, 4, Split32<Rs84Bulk>>(a, s);  // without the 64-bit nibble splits
             case 507: return launch_ws<8, 4, Split64<Rs84Mid>>(a, s);
+            case 509: return launch_ws<8, 4, Smk<Rs84Bulk>>(a, s);  // split masks from SGPRs
             case 490: return launch_ws<8, 4, Rs84G32>(a, s);
             case 491: return launch_ws<8, 4, Pm<Rs84G32, 0>>(a, s);
             case 492: return launch_ws<8, 4, Stamp<Rs84G32>>(a, s);

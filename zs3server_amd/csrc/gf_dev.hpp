@@ -39,17 +39,25 @@ __device__ __forceinline__ Nib split_nibbles(uint32_t x) {
 // Two dwords split with 64-bit shifts (round 6): v_lshrrev_b64 issues in ~4.5 cycles
 // where two v_lshrrev_b32 take ~5.5 (profiles/r06/opcost.txt); the high dword's bits that
 // the shift moves into the low one land above every kept field.
+// SMK (diagnostics): the two masks from SGPRs instead of 32-bit literals (4-byte instead of
+// 8-byte VALU encodings).
+template <bool SMK = false>
 __device__ __forceinline__ void split_nibbles2(uint32_t xlo, uint32_t xhi, Nib& lo, Nib& hi) {
     const uint64_t x = ((uint64_t)xhi << 32) | xlo;
     uint64_t t3, t6;  // (the compiler lowers a 64-bit shift to 32-bit ones: stated here)
     asm("v_lshrrev_b64 %0, 3, %1" : "=v"(t3) : "v"(x));
     asm("v_lshrrev_b64 %0, 6, %1" : "=v"(t6) : "v"(x));
-    lo.a = xlo & 0x07070707u;
-    hi.a = xhi & 0x07070707u;
-    lo.b = (uint32_t)t3 & 0x07070707u;
-    hi.b = (uint32_t)(t3 >> 32) & 0x07070707u;
-    lo.c = (uint32_t)t6 & 0x03030303u;
-    hi.c = (uint32_t)(t6 >> 32) & 0x03030303u;
+    uint32_t m7 = 0x07070707u, m3 = 0x03030303u;
+    if constexpr (SMK) {
+        asm("s_mov_b32 %0, 0x7070707" : "=s"(m7));
+        asm("s_mov_b32 %0, 0x3030303" : "=s"(m3));
+    }
+    lo.a = xlo & m7;
+    hi.a = xhi & m7;
+    lo.b = (uint32_t)t3 & m7;
+    hi.b = (uint32_t)(t3 >> 32) & m7;
+    lo.c = (uint32_t)t6 & m3;
+    hi.c = (uint32_t)(t6 >> 32) & m3;
 }
 
 // Coefficient tables as held in LDS: 8 dwords per coefficient (32 B aligned),
@@ -214,7 +222,7 @@ struct NoHook {
 // PRE: the K coefficient tables were read once into registers (pre[0..K-1]) before the
 // tile loop: no LDS reads (and no LDS-counter waits) inside the encode.
 template <int NWd, int K, int M, bool SB = true, bool PRS = false, bool ST = false, bool PRE = false,
-          bool S64 = false, typename XF, typename H0 = NoHook>
+          bool S64 = false, bool SMK = false, typename XF, typename H0 = NoHook>
 __device__ __forceinline__ void encode_dyadic_f(XF&& getx, Col<NWd> (&out)[M], const uint32_t* dtabs,
                                                 ctab_ptr ctabs = nullptr, H0&& hook0 = NoHook{},
                                                 const CoefTab* pre = nullptr) {
@@ -272,7 +280,7 @@ __device__ __forceinline__ void encode_dyadic_f(XF&& getx, Col<NWd> (&out)[M], c
                         }
                         Nib nl[4];
 #pragma unroll
-                        for (int i = 0; i < 4; ++i) split_nibbles2(Xs[0][i], Xs[1][i], nl[i], np[i]);
+                        for (int i = 0; i < 4; ++i) split_nibbles2<SMK>(Xs[0][i], Xs[1][i], nl[i], np[i]);
                         n0 = nl[0];
                         n1 = nl[1];
                         n2 = nl[2];
@@ -339,10 +347,10 @@ __device__ __forceinline__ void encode_dyadic_f(XF&& getx, Col<NWd> (&out)[M], c
     }
 }
 
-template <int NWd, int K, int M, bool SB = true, bool PRS = false, bool ST = false, bool S64 = false>
+template <int NWd, int K, int M, bool SB = true, bool PRS = false, bool ST = false, bool S64 = false, bool SMK = false>
 __device__ __forceinline__ void encode_dyadic(const Col<NWd> (&x)[K], Col<NWd> (&out)[M], const uint32_t* dtabs,
                                               ctab_ptr ctabs = nullptr) {
-    encode_dyadic_f<NWd, K, M, SB, PRS, ST, false, S64>([&](int j) { return x[j]; }, out, dtabs, ctabs);
+    encode_dyadic_f<NWd, K, M, SB, PRS, ST, false, S64, SMK>([&](int j) { return x[j]; }, out, dtabs, ctabs);
 }
 
 // General (non-dyadic) encode of one column: out[r] = sum_j M[r][j] * x[j] over GF(2^8),
